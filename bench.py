@@ -1,0 +1,258 @@
+#!/usr/bin/env python3
+"""bench.py — device-resident L3 ACL classification throughput on MI355X.
+
+Headline (BASELINE.json "metric"): Mpackets/s of device-resident L3 ACL
+classify, 64 B packets, 1 k rules (config C2), with the fraction of the HBM
+roofline.  One step = one classify launch (nffacl_classify_device, the HIP
+path) over the whole per-GPU batch of synthetic 64-byte slots already
+resident in HBM.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c1|c5] [--algo auto|linear|indexed]
+
+N > 1 runs under torch.distributed.run (one rank per GPU, RCCL): rank 0
+generates the rule file and broadcasts its bytes over RCCL (the path's one real
+exchange step, outside the timed region); every rank classifies its own
+resident shard — no data-path collective ("scaling": "weak").
+
+The JSON line carries:
+  roofline     achieved = 68 algorithmic bytes/packet (64 B read + 4 B port
+               write) x packets per launch / mean kernel time
+               (HIP events on the launch stream); peak = 8 TB/s HBM3E;
+               traffic = PMC bytes per launch from profiles/ (if collected)
+  cpu_baseline the oracle (oracle/acl_oracle.c, reference algorithm restated
+               in C) on a bounded sample of the same packets, on this host's
+               cores, rank 0 at N = 1 only
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "nff-go_amd"))
+sys.path.insert(0, str(ROOT))
+
+import numpy as np  # noqa: E402
+
+METRIC = "Mpackets/s device-resident L3 ACL classify, 64B pkts @1k rules; % HBM roofline"
+BYTES_PER_PACKET = 68  # 64 B slot read + 4 B verdict write
+HBM_PEAK_GBPS = 8000.0
+WORKLOADS = {
+    "c1": "C1 firewall.conf (4 text rules -> 4 ip4 + 1 ip6), 64B packets, device-resident",
+    "c2": "C2 1k-rule L3 ACL, 64B packets, device-resident",
+    "c5": "C5 100k-rule L3+L4 ACL with port ranges, 64B packets, device-resident",
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def build_rules(cfg: str):
+    from nffacl import synth
+    if cfg == "c1":
+        text = (ROOT / "tests" / "golden" / "rules" / "firewall.conf").read_text()
+        return text, synth.firewall_rules(text)
+    g = synth.gen_rules(synth.SPECS[cfg if cfg != "c4" else "c2"], synth.RULE_SEEDS[cfg])
+    return g.text, g
+
+
+def pmc_traffic(cfg: str, algo: str, n: int):
+    """HBM bytes per launch from the committed PMC summary, if one matches."""
+    path = ROOT / "profiles" / "pmc_traffic.json"
+    if not path.exists():
+        return None
+    try:
+        d = json.loads(path.read_text())
+        e = d.get(f"{cfg}:{algo}:{n}")
+        return None if e is None else float(e["bytes_per_launch"])
+    except Exception:
+        return None
+
+
+def cpu_baseline(slots: np.ndarray, n: int, a4, a6, budget_s: float):
+    from oracle import oracle
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    cores = max(1, min(cores, 16))  # the GPU box's CPU share for one GPU
+    # calibrate on a small prefix, then size the sample for ~budget_s
+    cal = min(n, 1 << 15)
+    t = time.perf_counter()
+    oracle.classify_slots(slots, 64, cal, a4, a6, threads=cores)
+    rate = cal / max(time.perf_counter() - t, 1e-6)
+    sample = int(min(n, max(cal, rate * budget_s)))
+    t = time.perf_counter()
+    ports, which = oracle.classify_slots_which(slots, 64, sample, a4, a6, threads=cores)
+    dt = time.perf_counter() - t
+    t1 = time.perf_counter()
+    one = min(sample, 1 << 16)
+    oracle.classify_slots(slots, 64, one, a4, a6, threads=1)
+    dt1 = time.perf_counter() - t1
+    hit = which >= 0
+    return {
+        "value": round(sample / dt / 1e6, 3), "unit": "Mpps", "cores": cores, "kind": "port",
+        "sample": f"first {sample} packets of rank 0's batch (oracle/acl_oracle.c, {cores} threads, {dt:.1f}s)",
+        "single_core_mpps": round(one / dt1 / 1e6, 3),
+        "mean_first_match_index": round(float(which[hit].mean()), 1) if hit.any() else None,
+        "match_fraction": round(float(hit.mean()), 4),
+    }, ports[:sample]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c4", "c5"])
+    ap.add_argument("--algo", default="auto", choices=["auto", "linear", "indexed"])
+    ap.add_argument("--packets", type=int, default=1 << 24, help="packets per GPU")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host", action="store_true", help="skip the PCIe-inclusive measurement")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    import nffacl
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+
+    cfg = args.config
+    n = args.packets
+    algo_id = {"auto": nffacl.ALGO_AUTO, "linear": nffacl.ALGO_LINEAR, "indexed": nffacl.ALGO_INDEXED}[args.algo]
+
+    # ---- rules: rank 0 generates, RCCL broadcast of the rule file bytes ----
+    text, gen = build_rules(cfg)
+    if world > 1:
+        blob = torch.zeros(1, dtype=torch.int64, device=dev)
+        if rank == 0:
+            raw = torch.frombuffer(bytearray(text.encode()), dtype=torch.uint8).to(dev)
+            blob[0] = raw.numel()
+        dist.broadcast(blob, 0)
+        if rank != 0:
+            raw = torch.empty(int(blob[0]), dtype=torch.uint8, device=dev)
+        dist.broadcast(raw, 0)
+        text = bytes(raw.cpu().numpy()).decode()
+    rules = nffacl.L3Rules.parse_text(text)
+    n4, n6 = rules.counts()
+    eng = nffacl.Engine(rules, device=local, algo=algo_id)
+    algo_name = {nffacl.ALGO_LINEAR: "linear", nffacl.ALGO_INDEXED: "indexed"}[eng.algo]
+
+    # ---- packets: per-rank shard, resident in HBM before timing ----
+    from nffacl import synth
+    t0 = time.perf_counter()
+    slots = synth.gen_slots(gen, n, synth.PACKET_SEEDS[cfg] + 7919 * rank)
+    log(f"[rank {rank}] generated {n} packets in {time.perf_counter() - t0:.1f}s; rules ip4={n4} ip6={n6}; algo={algo_name}")
+    d_slots = torch.from_numpy(slots).to(dev)
+    port = torch.empty(n, dtype=torch.int32, device=dev)
+    permit = torch.empty((n + 63) // 64, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    for _ in range(args.warmup):
+        eng.classify_device(d_slots, 64, n, port, permit, stream)
+    torch.cuda.synchronize(dev)
+
+    # ---- timed region ----
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t_start = time.perf_counter()
+    for s in range(args.steps):
+        evs[s][0].record(stream)
+        eng.classify_device(d_slots, 64, n, port, permit, stream)
+        evs[s][1].record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    kms = np.array([a.elapsed_time(b) for a, b in evs])  # per-launch kernel time (ms)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # ---- spot parity check (outside timing): GPU verdicts vs oracle sample ----
+    from oracle import oracle, rules_oracle as ro
+    a4, a6 = ro.parse_text_table(text.encode()).arrays()
+    got = port.cpu().numpy().view(np.uint32)
+    rng = np.random.default_rng(rank)
+    idx = np.sort(rng.choice(n, min(n, 4096), replace=False))
+    want = oracle.classify_slots(slots.reshape(n, 64)[idx].reshape(-1), 64, len(idx), a4, a6, threads=4)
+    bit_exact = bool((got[idx] == want).all())
+
+    total = n * world * args.steps
+    value = total / elapsed / 1e6
+    mean_k = float(kms.mean()) / 1e3
+    achieved = BYTES_PER_PACKET * n / mean_k / 1e9
+    out = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "Mpps",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic (deterministic seeds; SURVEY.md §8d mix)",
+        "config": {
+            "workload": WORKLOADS.get(cfg, cfg), "rules_ip4": n4, "rules_ip6": n6,
+            "packets_per_gpu": n, "slot_bytes": 64, "algo": algo_name, "parallelism": f"dp{world}",
+            "table_bytes": eng.table_bytes,
+        },
+        "roofline": {
+            "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBPS, 4),
+            "traffic": pmc_traffic(cfg, algo_name, n),
+            "kernel_ms_mean": round(float(kms.mean()), 5), "kernel_ms_min": round(float(kms.min()), 5),
+            "kernel_ms_max": round(float(kms.max()), 5),
+        },
+        "bit_exact_sample": bit_exact,
+    }
+
+    # ---- PCIe-inclusive rate (not `value`) ----
+    if rank == 0 and not args.no_host:
+        m = min(n, 1 << 22)
+        pinned = torch.from_numpy(slots[: m * 64]).pin_memory().numpy()
+        eng.classify_host(pinned, 64, m)
+        t = time.perf_counter()
+        hp, _ = eng.classify_host(pinned, 64, m)
+        dt = time.perf_counter() - t
+        out["host_inclusive_mpps"] = round(m / dt / 1e6, 1)
+        out["host_inclusive_bit_exact_sample"] = bool((hp[idx[idx < m]] == got[idx[idx < m]]).all())
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cb, cports = cpu_baseline(slots, n, a4, a6, args.cpu_seconds)
+        cb["bit_exact_vs_gpu"] = bool((cports == got[: len(cports)]).all())
+        out["cpu_baseline"] = cb
+    elif rank == 0:
+        out["cpu_baseline"] = None
+
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+    return 0 if bit_exact else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

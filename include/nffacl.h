@@ -1,0 +1,204 @@
+/*
+ * nffacl.h — C-ABI of libnffacl, the MI355X-native replacement for nff-go's
+ * L3/L4 ACL hot path (packet/acl.go + the header parsing of packet/packet.go).
+ *
+ * Every entry point is plain C: pointers, sizes and integer status codes; no
+ * HIP, torch or C++ types cross this boundary (a HIP stream is passed as
+ * `void*`).  A Go cgo package, a Python ctypes binding and the C++ host mirror
+ * (nff-go_amd/csrc/host_api.hpp) all bind exactly these symbols.
+ *
+ * Reference interfaces replaced (paths relative to aregm/nff-go):
+ *   nffacl_rules_load_text      <- packet.GetL3ACLFromTextTable   packet/acl.go:148-178
+ *   nffacl_rules_parse_text     <- same parser, from a memory buffer (acl.go:156-177)
+ *   nffacl_rules_load_json      <- packet.GetL3ACLFromJSON        packet/acl.go:121-134
+ *   nffacl_rules_from_arrays    <- L3Rules{ip4: ..., ip6: ...} literals the reference
+ *                                  tests build directly (acl_internal_test.go:588-593)
+ *   nffacl_rules_get4/get6      <- the unexported ip4/ip6 slices read by the reference
+ *                                  parse tests (acl_internal_test.go:392, 420)
+ *   nffacl_classify_device      <- (*Packet).L3ACLPort / L3ACLPermit  acl.go:495-506,
+ *                                  l3ACL acl.go:522-565, l4ACL acl.go:508-520,
+ *                                  ParseAllKnownL3 packet.go:353-363,
+ *                                  ParseL4ForIPv4/6 packet.go:278-285 — over a batch of
+ *                                  packets resident in HBM
+ *   nffacl_classify_frames_device  same, over packed variable-length frames (IMIX)
+ *   nffacl_classify_host        <- the VectorSeparateFunction body the reference runs per
+ *                                  burst (flow/flow.go:131, 1487-1520;
+ *                                  test/stability/testSingleWorkingFF/testSingleWorkingFF.go:538-546)
+ *                                  — host slots in, verdicts out, PCIe staging inside
+ *   nffacl_engine_swap_rules    <- the atomic *L3Rules pointer swap user code performs
+ *                                  on rule reload (examples/tutorial/step08.go:33-44)
+ *
+ * Verdict semantics (bit-exact with acl.go):
+ *   port  = OutputNumber of the FIRST rule (file order, per address family) that
+ *           matches, 0 if none or the packet is neither IPv4 nor IPv6;
+ *   permit = port > 0.
+ * Packet bytes past the end of the slot/frame read as 0 (the reference reads
+ * whatever mbuf memory follows; the slot convention pins that to zero).
+ *
+ * Status codes: 0 on success, negative on error.  The rule-parser codes are the
+ * negated nff-go common.ErrorCode values (common/error.go:18-50) so a cgo shim
+ * can rebuild the exact NFError{Code} the reference returns.
+ *
+ * Threading: rules objects are immutable after creation and may be shared by
+ * any number of threads.  An engine may be used concurrently from several host
+ * threads (each on its own stream); nffacl_engine_swap_rules may run
+ * concurrently with classification and takes effect for launches issued after
+ * it returns.
+ */
+#ifndef NFFACL_H
+#define NFFACL_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NFFACL_ABI_VERSION 1
+
+/* Only the entry points below are exported from libnffacl.so (built with
+ * -fvisibility=hidden). */
+#if defined(__GNUC__)
+#define NFFACL_API __attribute__((visibility("default")))
+#else
+#define NFFACL_API
+#endif
+
+/* ---- status codes ------------------------------------------------------ */
+enum nffacl_status {
+    NFFACL_OK = 0,
+    /* negated common.ErrorCode (common/error.go:18-50) */
+    NFFACL_ERR_PARSE_RULE_JSON = -11,      /* ParseRuleJSONErr */
+    NFFACL_ERR_FILE = -12,                 /* FileErr */
+    NFFACL_ERR_PARSE_RULE = -13,           /* ParseRuleErr ("Incomplete 5-tuple") */
+    NFFACL_ERR_INCORRECT_ARG_IN_RULES = -14, /* IncorrectArgInRules */
+    NFFACL_ERR_INCORRECT_RULE = -15,       /* IncorrectRule (bad OutputNumber) */
+    /* engine / device errors (no reference counterpart) */
+    NFFACL_ERR_INVALID_ARG = -100,
+    NFFACL_ERR_NOMEM = -101,
+    NFFACL_ERR_HIP = -102,
+    NFFACL_ERR_NO_DEVICE = -103,
+    NFFACL_ERR_UNSUPPORTED = -104
+};
+
+/* ---- rule records (internal representation of acl.go:423-449) --------- */
+
+/* l4Rules, acl.go:423-431 */
+typedef struct nffacl_l4 {
+    uint8_t id;            /* L4 protocol number (types.TCPNumber ...) */
+    uint8_t id_mask;       /* 0 = ANY, 0xff = exact */
+    uint8_t valid;         /* ports constrained (IPv4 rules skip the port test when 0) */
+    uint8_t reserved;      /* must be 0 */
+    uint16_t src_port_min; /* host-order port numbers */
+    uint16_t src_port_max;
+    uint16_t dst_port_min;
+    uint16_t dst_port_max;
+} nffacl_l4; /* 12 bytes */
+
+/* l3Rules4, acl.go:433-440.  Addresses and masks are types.IPv4Address values:
+ * the little-endian uint32 of the four wire bytes (types/ipv4.go:13-28), so
+ * 127.0.0.1 is 0x0100007f exactly as in the reference. */
+typedef struct nffacl_rule4 {
+    uint32_t output_number; /* Go `uint`; the parsers bound it to 32 bits */
+    uint32_t src_addr;
+    uint32_t dst_addr;
+    uint32_t src_mask;
+    uint32_t dst_mask;
+    nffacl_l4 l4;
+} nffacl_rule4; /* 32 bytes */
+
+/* l3Rules6, acl.go:442-449.  Wire byte order. */
+typedef struct nffacl_rule6 {
+    uint32_t output_number;
+    uint8_t src_addr[16];
+    uint8_t dst_addr[16];
+    uint8_t src_mask[16];
+    uint8_t dst_mask[16];
+    nffacl_l4 l4;
+} nffacl_rule6; /* 80 bytes */
+
+typedef struct nffacl_rules nffacl_rules;
+typedef struct nffacl_engine nffacl_engine;
+
+/* ---- rules ------------------------------------------------------------- */
+
+/* GetL3ACLFromTextTable (acl.go:148).  On error *out is NULL and `err`
+ * (if non-NULL) receives the message.  The reference additionally hands back a
+ * partially filled *L3Rules next to the error (acl.go:177); no caller uses it. */
+NFFACL_API int nffacl_rules_load_text(const char *path, nffacl_rules **out, char *err, size_t errlen);
+/* Same grammar, parsing `len` bytes of an in-memory file image. */
+NFFACL_API int nffacl_rules_parse_text(const char *text, size_t len, nffacl_rules **out, char *err,
+                            size_t errlen);
+/* GetL3ACLFromJSON (acl.go:121). */
+NFFACL_API int nffacl_rules_load_json(const char *path, nffacl_rules **out, char *err, size_t errlen);
+NFFACL_API int nffacl_rules_parse_json(const char *text, size_t len, nffacl_rules **out, char *err,
+                            size_t errlen);
+/* Build a rule set from already-parsed records, as the reference tests build
+ * L3Rules literals (arrays are copied; either pointer may be NULL when its
+ * count is 0). */
+NFFACL_API int nffacl_rules_from_arrays(const nffacl_rule4 *r4, size_t n4, const nffacl_rule6 *r6,
+                             size_t n6, nffacl_rules **out);
+NFFACL_API void nffacl_rules_free(nffacl_rules *rules);
+NFFACL_API int nffacl_rules_counts(const nffacl_rules *rules, size_t *n4, size_t *n6);
+NFFACL_API int nffacl_rules_get4(const nffacl_rules *rules, size_t i, nffacl_rule4 *out);
+NFFACL_API int nffacl_rules_get6(const nffacl_rules *rules, size_t i, nffacl_rule6 *out);
+
+/* ---- engine ------------------------------------------------------------ */
+
+/* Matching strategy compiled into the device table. */
+enum nffacl_algo {
+    NFFACL_ALGO_AUTO = 0,   /* library picks (indexed when the rule set allows) */
+    NFFACL_ALGO_LINEAR = 1, /* wave-uniform first-match scan (acl.go's loop order) */
+    NFFACL_ALGO_INDEXED = 2 /* host-compiled interval index + ordered candidate lists */
+};
+
+/* Compile `rules` for HIP device `hip_device` and upload the table. */
+NFFACL_API int nffacl_engine_create(int hip_device, const nffacl_rules *rules, nffacl_engine **out);
+NFFACL_API int nffacl_engine_create_ex(int hip_device, const nffacl_rules *rules, int algo,
+                            nffacl_engine **out);
+/* Compile + upload a new table, then atomically make it the active one.
+ * Launches issued before the call keep using the previous table. */
+NFFACL_API int nffacl_engine_swap_rules(nffacl_engine *eng, const nffacl_rules *rules);
+NFFACL_API void nffacl_engine_destroy(nffacl_engine *eng);
+/* Algorithm actually compiled into the active table (NFFACL_ALGO_LINEAR/INDEXED). */
+NFFACL_API int nffacl_engine_algo(const nffacl_engine *eng);
+/* Bytes of the active device table (rule records + index), for reporting. */
+NFFACL_API int nffacl_engine_table_bytes(const nffacl_engine *eng, uint64_t *bytes);
+
+/* ---- classification ------------------------------------------------------ */
+
+/* Device-resident dense slots: packet i occupies d_slots[i*stride, (i+1)*stride)
+ * with its frame starting at byte 0 (the Ether header) and zero padding after
+ * the frame.  stride % 16 == 0, stride >= 64, d_slots 16-byte aligned.
+ * d_port[i]  <- L3ACLPort (may be NULL)
+ * d_permit_bits[i/64] bit i%64 <- L3ACLPermit (may be NULL; ceil(n/64) words;
+ *   bits past n in the last word are 0).
+ * Asynchronous on `stream` (hipStream_t, NULL = default stream). */
+NFFACL_API int nffacl_classify_device(nffacl_engine *eng, const uint8_t *d_slots, uint32_t stride,
+                           uint64_t n, uint32_t *d_port, uint64_t *d_permit_bits,
+                           void *stream);
+
+/* Device-resident packed frames (IMIX): frame i starts at d_frames + (desc[i] >> 16)
+ * and is (desc[i] & 0xffff) bytes long; bytes past its length read as 0.
+ * Frame starts must be 16-byte aligned (mbuf data rooms are cache-line aligned). */
+NFFACL_API int nffacl_classify_frames_device(nffacl_engine *eng, const uint8_t *d_frames,
+                                  const uint64_t *d_desc, uint64_t n, uint32_t *d_port,
+                                  uint64_t *d_permit_bits, void *stream);
+
+/* Host slots in, host verdicts out: pinned staging + async H2D / kernel / D2H,
+ * double-buffered across chunks.  Synchronous.  h_port / h_permit may be NULL
+ * (h_permit gets one byte per packet, 0 or 1). */
+NFFACL_API int nffacl_classify_host(nffacl_engine *eng, const uint8_t *h_slots, uint32_t stride,
+                         uint64_t n, uint32_t *h_port, uint8_t *h_permit);
+
+/* ---- misc ------------------------------------------------------------- */
+NFFACL_API const char *nffacl_strerror(int status);
+NFFACL_API int nffacl_abi_version(void);
+/* Last HIP / engine error message recorded on this thread ("" if none). */
+NFFACL_API const char *nffacl_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NFFACL_H */

@@ -1,0 +1,369 @@
+// capi.cpp — the extern "C" boundary of libnffacl (declared in include/nffacl.h).
+//
+// No exception crosses this boundary; every entry point returns an nffacl
+// status and records details retrievable with nffacl_last_error().
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "engine.hpp"
+#include "nffacl.h"
+#include "rules.hpp"
+
+using namespace nffacl;
+
+namespace {
+
+void copy_err(char *dst, size_t len, const std::string &msg) {
+    if (!dst || len == 0) return;
+    size_t n = std::min(len - 1, msg.size());
+    std::memcpy(dst, msg.data(), n);
+    dst[n] = '\0';
+}
+
+int finish_parse(bool ok, nffacl_rules *r, const ParseError &pe, nffacl_rules **out, char *err,
+                 size_t errlen) {
+    if (!ok) {
+        delete r;
+        *out = nullptr;
+        std::string msg = pe.message + " (" + std::to_string(-pe.code) + ")";  // NFError.Error()
+        copy_err(err, errlen, msg);
+        set_last_error(msg);
+        return pe.code;
+    }
+    copy_err(err, errlen, "");
+    *out = r;
+    return NFFACL_OK;
+}
+
+bool read_file(const char *path, std::vector<char> &buf, std::string &msg) {
+    FILE *f = std::fopen(path, "rb");
+    if (!f) {
+        msg = std::string("file error during rules parsing: open ") + path + ": " + std::strerror(errno);
+        return false;
+    }
+    char tmp[1 << 16];
+    size_t got;
+    while ((got = std::fread(tmp, 1, sizeof tmp, f)) > 0) buf.insert(buf.end(), tmp, tmp + got);
+    const bool bad = std::ferror(f) != 0;
+    std::fclose(f);
+    if (bad) {
+        msg = std::string("file error during rules parsing: read ") + path;
+        return false;
+    }
+    return true;
+}
+
+template <class Parser>
+int load_with(const char *path, nffacl_rules **out, char *err, size_t errlen, Parser parser) {
+    if (!path || !out) return NFFACL_ERR_INVALID_ARG;
+    *out = nullptr;
+    std::vector<char> buf;
+    std::string msg;
+    if (!read_file(path, buf, msg)) {
+        msg += " (12)";
+        copy_err(err, errlen, msg);
+        set_last_error(msg);
+        return NFFACL_ERR_FILE;
+    }
+    nffacl_rules *r = new (std::nothrow) nffacl_rules();
+    if (!r) return NFFACL_ERR_NOMEM;
+    ParseError pe;
+    bool ok = parser(buf.data(), buf.size(), *r, pe);
+    return finish_parse(ok, r, pe, out, err, errlen);
+}
+
+bool pointer_is_pinned(const void *p) {
+    hipPointerAttribute_t attr;
+    if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return attr.type == hipMemoryTypeHost;
+}
+
+}  // namespace
+
+#define HIP_CHECK(expr)                                                                  \
+    do {                                                                                 \
+        hipError_t e_ = (expr);                                                          \
+        if (e_ != hipSuccess) {                                                          \
+            set_last_error(std::string(#expr) + ": " + hipGetErrorString(e_));            \
+            return NFFACL_ERR_HIP;                                                       \
+        }                                                                                \
+    } while (0)
+
+extern "C" {
+
+int nffacl_abi_version(void) { return NFFACL_ABI_VERSION; }
+
+const char *nffacl_last_error(void) { return last_error(); }
+
+const char *nffacl_strerror(int s) {
+    switch (s) {
+    case NFFACL_OK: return "ok";
+    case NFFACL_ERR_PARSE_RULE_JSON: return "JSON error during rules parsing (ParseRuleJSONErr)";
+    case NFFACL_ERR_FILE: return "file error during rules parsing (FileErr)";
+    case NFFACL_ERR_PARSE_RULE: return "Incomplete 5-tuple for rule parsing (ParseRuleErr)";
+    case NFFACL_ERR_INCORRECT_ARG_IN_RULES: return "incorrect argument in rules (IncorrectArgInRules)";
+    case NFFACL_ERR_INCORRECT_RULE: return "incorrect rule result (IncorrectRule)";
+    case NFFACL_ERR_INVALID_ARG: return "invalid argument";
+    case NFFACL_ERR_NOMEM: return "out of memory";
+    case NFFACL_ERR_HIP: return "HIP runtime error";
+    case NFFACL_ERR_NO_DEVICE: return "no HIP device";
+    case NFFACL_ERR_UNSUPPORTED: return "unsupported";
+    default: return "unknown status";
+    }
+}
+
+// ---- rules -----------------------------------------------------------------
+
+int nffacl_rules_load_text(const char *path, nffacl_rules **out, char *err, size_t errlen) {
+    return load_with(path, out, err, errlen, parse_text_table);
+}
+
+int nffacl_rules_parse_text(const char *text, size_t len, nffacl_rules **out, char *err,
+                            size_t errlen) {
+    if (!out || (!text && len)) return NFFACL_ERR_INVALID_ARG;
+    nffacl_rules *r = new (std::nothrow) nffacl_rules();
+    if (!r) return NFFACL_ERR_NOMEM;
+    ParseError pe;
+    bool ok = parse_text_table(text ? text : "", len, *r, pe);
+    return finish_parse(ok, r, pe, out, err, errlen);
+}
+
+int nffacl_rules_load_json(const char *path, nffacl_rules **out, char *err, size_t errlen) {
+    return load_with(path, out, err, errlen, parse_json);
+}
+
+int nffacl_rules_parse_json(const char *text, size_t len, nffacl_rules **out, char *err,
+                            size_t errlen) {
+    if (!out || (!text && len)) return NFFACL_ERR_INVALID_ARG;
+    nffacl_rules *r = new (std::nothrow) nffacl_rules();
+    if (!r) return NFFACL_ERR_NOMEM;
+    ParseError pe;
+    bool ok = parse_json(text ? text : "", len, *r, pe);
+    return finish_parse(ok, r, pe, out, err, errlen);
+}
+
+int nffacl_rules_from_arrays(const nffacl_rule4 *r4, size_t n4, const nffacl_rule6 *r6, size_t n6,
+                             nffacl_rules **out) {
+    if (!out || (!r4 && n4) || (!r6 && n6)) return NFFACL_ERR_INVALID_ARG;
+    nffacl_rules *r = new (std::nothrow) nffacl_rules();
+    if (!r) return NFFACL_ERR_NOMEM;
+    r->ip4.assign(r4, r4 + n4);
+    r->ip6.assign(r6, r6 + n6);
+    *out = r;
+    return NFFACL_OK;
+}
+
+void nffacl_rules_free(nffacl_rules *rules) { delete rules; }
+
+int nffacl_rules_counts(const nffacl_rules *rules, size_t *n4, size_t *n6) {
+    if (!rules) return NFFACL_ERR_INVALID_ARG;
+    if (n4) *n4 = rules->ip4.size();
+    if (n6) *n6 = rules->ip6.size();
+    return NFFACL_OK;
+}
+
+int nffacl_rules_get4(const nffacl_rules *rules, size_t i, nffacl_rule4 *out) {
+    if (!rules || !out || i >= rules->ip4.size()) return NFFACL_ERR_INVALID_ARG;
+    *out = rules->ip4[i];
+    return NFFACL_OK;
+}
+
+int nffacl_rules_get6(const nffacl_rules *rules, size_t i, nffacl_rule6 *out) {
+    if (!rules || !out || i >= rules->ip6.size()) return NFFACL_ERR_INVALID_ARG;
+    *out = rules->ip6[i];
+    return NFFACL_OK;
+}
+
+// ---- engine ----------------------------------------------------------------
+
+int nffacl_engine_create_ex(int hip_device, const nffacl_rules *rules, int algo, nffacl_engine **out) {
+    if (!rules || !out) return NFFACL_ERR_INVALID_ARG;
+    *out = nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
+        (void)hipGetLastError();
+        set_last_error("no HIP device visible");
+        return NFFACL_ERR_NO_DEVICE;
+    }
+    if (hip_device < 0 || hip_device >= count) return NFFACL_ERR_INVALID_ARG;
+    HIP_CHECK(hipSetDevice(hip_device));
+    nffacl_engine *eng = new (std::nothrow) nffacl_engine();
+    if (!eng) return NFFACL_ERR_NOMEM;
+    eng->device = hip_device;
+    eng->algo_req = algo;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, hip_device) == hipSuccess && cus > 0)
+        eng->num_cus = cus;
+    DevTable *t = nullptr;
+    int st = upload_table(hip_device, *rules, algo, t);
+    if (st != NFFACL_OK) {
+        delete eng;
+        return st;
+    }
+    eng->active = t;
+    *out = eng;
+    return NFFACL_OK;
+}
+
+int nffacl_engine_create(int hip_device, const nffacl_rules *rules, nffacl_engine **out) {
+    return nffacl_engine_create_ex(hip_device, rules, NFFACL_ALGO_AUTO, out);
+}
+
+int nffacl_engine_swap_rules(nffacl_engine *eng, const nffacl_rules *rules) {
+    if (!eng || !rules) return NFFACL_ERR_INVALID_ARG;
+    DevTable *t = nullptr;
+    int st = upload_table(eng->device, *rules, eng->algo_req, t);
+    if (st != NFFACL_OK) return st;
+    DevTable *old_retired = nullptr;
+    {
+        std::lock_guard<std::mutex> g(eng->table_mu);
+        old_retired = eng->retired;
+        eng->retired = eng->active;
+        eng->active = t;
+    }
+    if (old_retired) {
+        // Launches that used it were issued before the previous swap returned.
+        HIP_CHECK(hipSetDevice(eng->device));
+        HIP_CHECK(hipDeviceSynchronize());
+        delete old_retired;
+    }
+    return NFFACL_OK;
+}
+
+void nffacl_engine_destroy(nffacl_engine *eng) {
+    if (!eng) return;
+    (void)hipSetDevice(eng->device);
+    (void)hipDeviceSynchronize();
+    delete eng->active;
+    delete eng->retired;
+    for (int b = 0; b < 2; ++b) {
+        if (eng->h_stage[b]) (void)hipHostFree(eng->h_stage[b]);
+        if (eng->h_port[b]) (void)hipHostFree(eng->h_port[b]);
+        if (eng->d_slots[b]) (void)hipFree(eng->d_slots[b]);
+        if (eng->d_port[b]) (void)hipFree(eng->d_port[b]);
+        if (eng->streams[b]) (void)hipStreamDestroy(eng->streams[b]);
+        if (eng->done[b]) (void)hipEventDestroy(eng->done[b]);
+    }
+    delete eng;
+}
+
+int nffacl_engine_algo(const nffacl_engine *eng) {
+    if (!eng || !eng->active) return NFFACL_ERR_INVALID_ARG;
+    return eng->active->meta.algo;
+}
+
+int nffacl_engine_table_bytes(const nffacl_engine *eng, uint64_t *bytes) {
+    if (!eng || !eng->active || !bytes) return NFFACL_ERR_INVALID_ARG;
+    *bytes = eng->active->bytes;
+    return NFFACL_OK;
+}
+
+// ---- classification ---------------------------------------------------------
+
+static DevTable *acquire_table(nffacl_engine *eng) {
+    std::lock_guard<std::mutex> g(eng->table_mu);
+    return eng->active;
+}
+
+int nffacl_classify_device(nffacl_engine *eng, const uint8_t *d_slots, uint32_t stride, uint64_t n,
+                           uint32_t *d_port, uint64_t *d_permit_bits, void *stream) {
+    if (!eng) return NFFACL_ERR_INVALID_ARG;
+    if (n == 0) return NFFACL_OK;
+    if (!d_slots || stride < 64 || (stride % 16) != 0 ||
+        (reinterpret_cast<uintptr_t>(d_slots) % 16) != 0)
+        return NFFACL_ERR_INVALID_ARG;
+    if (!d_port && !d_permit_bits) return NFFACL_OK;
+    HIP_CHECK(hipSetDevice(eng->device));
+    return launch_slots(eng, acquire_table(eng), d_slots, stride, n, d_port, d_permit_bits,
+                        static_cast<hipStream_t>(stream));
+}
+
+int nffacl_classify_frames_device(nffacl_engine *eng, const uint8_t *d_frames, const uint64_t *d_desc,
+                                  uint64_t n, uint32_t *d_port, uint64_t *d_permit_bits, void *stream) {
+    if (!eng) return NFFACL_ERR_INVALID_ARG;
+    if (n == 0) return NFFACL_OK;
+    if (!d_frames || !d_desc || (reinterpret_cast<uintptr_t>(d_frames) % 16) != 0)
+        return NFFACL_ERR_INVALID_ARG;
+    if (!d_port && !d_permit_bits) return NFFACL_OK;
+    HIP_CHECK(hipSetDevice(eng->device));
+    return launch_frames(eng, acquire_table(eng), d_frames, d_desc, n, d_port, d_permit_bits,
+                         static_cast<hipStream_t>(stream));
+}
+
+static int ensure_host_pipeline(nffacl_engine *eng, uint32_t stride) {
+    const size_t chunk = size_t(1) << 20;  // packets per pipeline stage
+    if (eng->chunk == chunk && eng->staged_stride >= stride) return NFFACL_OK;
+    for (int b = 0; b < 2; ++b) {
+        if (eng->h_stage[b]) { (void)hipHostFree(eng->h_stage[b]); eng->h_stage[b] = nullptr; }
+        if (eng->d_slots[b]) { (void)hipFree(eng->d_slots[b]); eng->d_slots[b] = nullptr; }
+    }
+    for (int b = 0; b < 2; ++b) {
+        HIP_CHECK(hipHostMalloc(reinterpret_cast<void **>(&eng->h_stage[b]), chunk * stride, hipHostMallocDefault));
+        HIP_CHECK(hipMalloc(reinterpret_cast<void **>(&eng->d_slots[b]), chunk * stride));
+        if (!eng->h_port[b]) HIP_CHECK(hipHostMalloc(reinterpret_cast<void **>(&eng->h_port[b]), chunk * 4, hipHostMallocDefault));
+        if (!eng->d_port[b]) HIP_CHECK(hipMalloc(reinterpret_cast<void **>(&eng->d_port[b]), chunk * 4));
+        if (!eng->streams[b]) HIP_CHECK(hipStreamCreateWithFlags(&eng->streams[b], hipStreamNonBlocking));
+        if (!eng->done[b]) HIP_CHECK(hipEventCreateWithFlags(&eng->done[b], hipEventDisableTiming));
+    }
+    eng->chunk = chunk;
+    eng->staged_stride = stride;
+    return NFFACL_OK;
+}
+
+int nffacl_classify_host(nffacl_engine *eng, const uint8_t *h_slots, uint32_t stride, uint64_t n,
+                         uint32_t *h_port, uint8_t *h_permit) {
+    if (!eng) return NFFACL_ERR_INVALID_ARG;
+    if (n == 0) return NFFACL_OK;
+    if (!h_slots || stride < 64 || (stride % 16) != 0) return NFFACL_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> g(eng->host_mu);
+    HIP_CHECK(hipSetDevice(eng->device));
+    int st = ensure_host_pipeline(eng, stride);
+    if (st != NFFACL_OK) return st;
+    DevTable *t = acquire_table(eng);
+    const bool direct = pointer_is_pinned(h_slots);
+    const uint64_t chunk = eng->chunk;
+    const uint64_t nchunks = (n + chunk - 1) / chunk;
+    uint64_t pending_chunk[2] = {~0ull, ~0ull};
+    auto drain = [&](int b) -> int {
+        if (pending_chunk[b] == ~0ull) return NFFACL_OK;
+        HIP_CHECK(hipEventSynchronize(eng->done[b]));
+        const uint64_t c = pending_chunk[b];
+        const uint64_t first = c * chunk;
+        const uint64_t cnt = std::min<uint64_t>(chunk, n - first);
+        if (h_port) std::memcpy(h_port + first, eng->h_port[b], cnt * 4);
+        if (h_permit)
+            for (uint64_t i = 0; i < cnt; ++i) h_permit[first + i] = eng->h_port[b][i] != 0;
+        pending_chunk[b] = ~0ull;
+        return NFFACL_OK;
+    };
+    for (uint64_t c = 0; c < nchunks; ++c) {
+        const int b = static_cast<int>(c & 1);
+        if ((st = drain(b)) != NFFACL_OK) return st;
+        const uint64_t first = c * chunk;
+        const uint64_t cnt = std::min<uint64_t>(chunk, n - first);
+        const uint8_t *src = h_slots + first * stride;
+        if (!direct) {
+            std::memcpy(eng->h_stage[b], src, cnt * stride);
+            src = eng->h_stage[b];
+        }
+        HIP_CHECK(hipMemcpyAsync(eng->d_slots[b], src, cnt * stride, hipMemcpyHostToDevice, eng->streams[b]));
+        st = launch_slots(eng, t, eng->d_slots[b], stride, cnt, eng->d_port[b], nullptr, eng->streams[b]);
+        if (st != NFFACL_OK) return st;
+        HIP_CHECK(hipMemcpyAsync(eng->h_port[b], eng->d_port[b], cnt * 4, hipMemcpyDeviceToHost, eng->streams[b]));
+        HIP_CHECK(hipEventRecord(eng->done[b], eng->streams[b]));
+        pending_chunk[b] = c;
+    }
+    for (int b = 0; b < 2; ++b)
+        if ((st = drain(b)) != NFFACL_OK) return st;
+    return NFFACL_OK;
+}
+
+}  // extern "C"

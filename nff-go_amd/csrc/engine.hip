@@ -1,0 +1,342 @@
+// engine.hip — HIP kernels (gfx950 / CDNA4) and the device engine of libnffacl.
+//
+// Hot path replaced: (*Packet).l3ACL, packet/acl.go:522-565 (+ l4ACL :508-520,
+// ParseAllKnownL3 packet/packet.go:353-363, ParseL4ForIPv4/6 :278-285), run
+// over a batch of packets resident in HBM instead of one mbuf at a time.
+//
+// Execution model (one wave64 = 64 consecutive packets, one packet per lane):
+//  * each lane loads its 64-byte slot with four 16-byte loads and extracts the
+//    header fields with funnel shifts (every field after the Ethernet header
+//    is at a wire offset = 2 mod 4);
+//  * LINEAR: the rule records are wave-uniform, so they stream through the
+//    scalar data cache (s_load) and every rule costs a handful of VALU ops
+//    on all 64 packets at once; a 64-bit ballot of still-undecided lanes ends
+//    the scan as soon as every packet of the wave has its first match;
+//  * INDEXED: see classify_indexed() — per-lane interval search + ordered
+//    candidate lists, tables staged in LDS;
+//  * the verdict vector is written as one u32 port per packet (coalesced) and
+//    one 64-bit permit word per wave (ballot of port > 0).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+
+#include "compile.hpp"
+#include "engine.hpp"
+
+namespace nffacl {
+
+thread_local std::string g_last_error;
+
+void set_last_error(const std::string &s) { g_last_error = s; }
+const char *last_error() { return g_last_error.c_str(); }
+
+namespace dev {
+
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+
+__device__ __forceinline__ uint32_t funnel16(uint32_t hi, uint32_t lo) {
+    // ({hi,lo} >> 16)[31:0] : wire bytes 4k+2 .. 4k+5 as a LE dword
+    return __builtin_amdgcn_alignbit(hi, lo, 16);
+}
+
+// Byte-swap each 16-bit half: LE dword of wire bytes [p0 p1 p2 p3] ->
+// (p0<<8|p1) | (p2<<8|p3) << 16 = sport | dport << 16 (SwapBytesUint16,
+// packet/packet.go:713-715, applied by l4ACL acl.go:511, 515).
+__device__ __forceinline__ uint32_t swap_halves(uint32_t w) {
+    return ((w & 0x00FF00FFu) << 8) | ((w >> 8) & 0x00FF00FFu);
+}
+
+// Non-zero iff some port of `ports` (sport | dport << 16) is outside
+// [lo, hi] per half (l4ACL, acl.go:512-518).
+__device__ __forceinline__ uint32_t port_miss(uint32_t ports, uint32_t lo, uint32_t hi) {
+    u16x2 p = __builtin_bit_cast(u16x2, ports);
+    u16x2 l = __builtin_bit_cast(u16x2, lo);
+    u16x2 h = __builtin_bit_cast(u16x2, hi);
+    u16x2 c = __builtin_elementwise_min(__builtin_elementwise_max(p, l), h);
+    return __builtin_bit_cast(uint32_t, c) ^ ports;
+}
+
+// Header fields of one packet (Appendix A of SURVEY.md).
+struct Fields {
+    bool is4, is6;
+    uint32_t proto;
+    uint32_t ports;     // sport | dport << 16 (host order)
+    uint32_t s[4], t[4];  // src / dst words (IPv4 uses [0])
+};
+
+// Parse the header fields from the first 64 bytes (d[0..15]) of a packet.
+// `far(k)` returns the little-endian dwords k and k+1 of the packet (bytes past
+// the slot/frame end as 0) for the rare IPv4 header whose IHL != 5 puts the L4
+// ports somewhere other than bytes 34..37; it runs in a divergent branch that
+// only lanes with IP options take.
+template <class FarDwords>
+__device__ __forceinline__ void parse_fields(const uint32_t (&d)[16], bool live, Fields &f,
+                                             FarDwords far) {
+    // ParseAllKnownL3: EtherType at wire bytes 12-13 (packet.go:238-243, 264-269)
+    const uint32_t et = d[3] & 0xFFFFu;
+    f.is4 = live && et == 0x0008u;  // 0x0800 on the wire
+    f.is6 = live && et == 0xDD86u;  // 0x86DD on the wire
+    // IPv4: proto byte 23, src 26..29, dst 30..33, L4 at 14 + 4*IHL (packet.go:278-280)
+    // IPv6: proto byte 20, src 22..37, dst 38..53, L4 at 54 (packet.go:283-285)
+    const uint32_t ihl = (d[3] >> 16) & 0xFu;
+    uint32_t pw = f.is6 ? funnel16(d[14], d[13]) : funnel16(d[9], d[8]);
+    if (f.is4 && ihl != 5u) {
+        uint32_t lo, hi;
+        far(3u + ihl, lo, hi);  // L4 bytes 14+4*IHL .. 17+4*IHL = dword 3+IHL, byte 2
+        pw = funnel16(hi, lo);
+    }
+    f.ports = swap_halves(pw);
+    f.proto = f.is6 ? (d[5] & 0xFFu) : (d[5] >> 24);
+    if (f.is6) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            f.s[k] = funnel16(d[6 + k], d[5 + k]);
+            f.t[k] = funnel16(d[10 + k], d[9 + k]);
+        }
+    } else {
+        f.s[0] = funnel16(d[7], d[6]);
+        f.t[0] = funnel16(d[8], d[7]);
+#pragma unroll
+        for (int k = 1; k < 4; ++k) { f.s[k] = 0; f.t[k] = 0; }
+    }
+}
+
+// Dwords k and k+1 of a packet whose readable, zero-padded extent is `lim`
+// bytes from `base` (4-byte aligned); bytes at or past `lim` read as 0.
+__device__ __forceinline__ void far_dwords(const uint8_t *base, uint32_t lim, uint32_t k,
+                                           uint32_t &lo, uint32_t &hi) {
+    const uint32_t *p = reinterpret_cast<const uint32_t *>(base);
+    auto masked = [&](uint32_t j) -> uint32_t {
+        const int rem = static_cast<int>(lim) - static_cast<int>(4 * j);
+        if (rem <= 0) return 0u;
+        const uint32_t v = p[j];
+        return rem >= 4 ? v : (v & ((1u << (8 * rem)) - 1u));
+    };
+    lo = masked(k);
+    hi = masked(k + 1);
+}
+
+// LINEAR: first-match scan in rule order, wave-uniform records.
+__device__ __forceinline__ uint32_t classify_linear(const Fields &f,
+                                                     const uint32_t *__restrict__ rec4, uint32_t n4,
+                                                     const uint32_t *__restrict__ rec6, uint32_t n6) {
+    uint32_t res = 0;
+    bool pend = f.is4;
+    if (ballot(pend)) {
+        for (uint32_t r = 0; r < n4; ++r) {
+            const uint32_t *R = rec4 + r * kRec4Dwords;
+            uint32_t m = ((f.s[0] ^ R[0]) & R[1]) | ((f.t[0] ^ R[2]) & R[3]);
+            const uint32_t meta = R[4];
+            const uint32_t idm = (meta >> 8) & 0xFFu;
+            if (idm) m |= (f.proto ^ meta) & idm;
+            if (meta & kMetaPortCheck) m |= port_miss(f.ports, R[5], R[6]);
+            const bool take = pend && m == 0u;
+            if (ballot(take)) {
+                if (take) { res = R[7]; pend = false; }
+                if (!ballot(pend)) break;
+            }
+        }
+    }
+    pend = f.is6;
+    if (ballot(pend)) {
+        for (uint32_t r = 0; r < n6; ++r) {
+            const uint32_t *R = rec6 + r * kRec6Dwords;
+            uint32_t m = ((f.s[0] ^ R[0]) & R[4]) | ((f.s[1] ^ R[1]) & R[5]) |
+                         ((f.s[2] ^ R[2]) & R[6]) | ((f.s[3] ^ R[3]) & R[7]) |
+                         ((f.t[0] ^ R[8]) & R[12]) | ((f.t[1] ^ R[9]) & R[13]) |
+                         ((f.t[2] ^ R[10]) & R[14]) | ((f.t[3] ^ R[11]) & R[15]);
+            const uint32_t meta = R[16];
+            const uint32_t idm = (meta >> 8) & 0xFFu;
+            if (idm) m |= (f.proto ^ meta) & idm;
+            if (meta & kMetaPortCheck) m |= port_miss(f.ports, R[17], R[18]);
+            const bool take = pend && m == 0u;
+            if (ballot(take)) {
+                if (take) { res = R[19]; pend = false; }
+                if (!ballot(pend)) break;
+            }
+        }
+    }
+    return res;
+}
+
+__device__ __forceinline__ uint32_t lane_id() {
+    return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
+
+// Dense slots: packet i at slots + i*stride; the first 64 bytes are loaded
+// with four 16-byte non-temporal loads (read once, never re-used).
+__device__ __forceinline__ void load16(const uint8_t *__restrict__ p, uint32_t (&d)[16]) {
+    const u32x4 *q = reinterpret_cast<const u32x4 *>(p);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const u32x4 v = __builtin_nontemporal_load(q + j);
+        d[4 * j + 0] = v.x;
+        d[4 * j + 1] = v.y;
+        d[4 * j + 2] = v.z;
+        d[4 * j + 3] = v.w;
+    }
+}
+
+// Zero the bytes of d[] at or past `len`.
+__device__ __forceinline__ void clip16(uint32_t (&d)[16], uint32_t len) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int rem = static_cast<int>(len) - 4 * k;  // valid bytes in dword k
+        const uint32_t keep = rem >= 4 ? 0xFFFFFFFFu : (rem <= 0 ? 0u : ((1u << (8 * rem)) - 1u));
+        d[k] &= keep;
+    }
+}
+
+struct LinearArgs {
+    const uint32_t *rec4;
+    uint32_t n4;
+    const uint32_t *rec6;
+    uint32_t n6;
+};
+
+// One wave = 64 consecutive packets per grid-stride step.
+#define NFFACL_WAVE_LOOP(n)                                                                   \
+    const uint32_t lane = lane_id();                                                          \
+    const uint32_t wpb = blockDim.x >> 6;                                                     \
+    const uint64_t wave0 = uint64_t(blockIdx.x) * wpb +                                       \
+                           __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);                  \
+    const uint64_t nwaves = uint64_t(gridDim.x) * wpb;                                        \
+    for (uint64_t base = wave0 * 64; base < (n); base += nwaves * 64)
+
+__device__ __forceinline__ void store_verdicts(uint64_t base, uint32_t lane, bool live, uint32_t res,
+                                               uint32_t *__restrict__ port_out,
+                                               uint64_t *__restrict__ permit_out) {
+    if (live && port_out) port_out[base + lane] = res;
+    const uint64_t permit = ballot(live && res != 0u);
+    if (permit_out && lane == 0) permit_out[base >> 6] = permit;
+}
+
+__global__ void __launch_bounds__(256)
+k_linear_slots(const uint8_t *__restrict__ slots, uint32_t stride, uint64_t n, LinearArgs a,
+               uint32_t *__restrict__ port_out, uint64_t *__restrict__ permit_out) {
+    NFFACL_WAVE_LOOP(n) {
+        const uint64_t idx = base + lane;
+        const bool live = idx < n;
+        const uint8_t *pkt = slots + (live ? idx : 0) * stride;
+        uint32_t d[16];
+        load16(pkt, d);
+        Fields f;
+        parse_fields(d, live, f, [&](uint32_t k, uint32_t &lo, uint32_t &hi) {
+            far_dwords(pkt, stride, k, lo, hi);
+        });
+        const uint32_t res = classify_linear(f, a.rec4, a.n4, a.rec6, a.n6);
+        store_verdicts(base, lane, live, res, port_out, permit_out);
+    }
+}
+
+// Packed frames: desc = offset << 16 | length; bytes >= length read as 0.
+__global__ void __launch_bounds__(256)
+k_linear_frames(const uint8_t *__restrict__ frames, const uint64_t *__restrict__ desc, uint64_t n,
+                LinearArgs a, uint32_t *__restrict__ port_out, uint64_t *__restrict__ permit_out) {
+    NFFACL_WAVE_LOOP(n) {
+        const uint64_t idx = base + lane;
+        const bool live = idx < n;
+        const uint64_t ds = live ? desc[idx] : 0;
+        const uint32_t len = static_cast<uint32_t>(ds & 0xFFFFu);
+        const uint8_t *pkt = frames + (ds >> 16);
+        uint32_t d[16];
+        load16(pkt, d);
+        clip16(d, len);
+        Fields f;
+        parse_fields(d, live, f, [&](uint32_t k, uint32_t &lo, uint32_t &hi) {
+            far_dwords(pkt, len, k, lo, hi);
+        });
+        const uint32_t res = classify_linear(f, a.rec4, a.n4, a.rec6, a.n6);
+        store_verdicts(base, lane, live, res, port_out, permit_out);
+    }
+}
+
+}  // namespace dev
+
+// ---------------------------------------------------------------------------
+// Host side of the engine
+// ---------------------------------------------------------------------------
+
+#define HIP_TRY(expr)                                                                    \
+    do {                                                                                 \
+        hipError_t e_ = (expr);                                                          \
+        if (e_ != hipSuccess) {                                                          \
+            set_last_error(std::string(#expr) + ": " + hipGetErrorString(e_));            \
+            return NFFACL_ERR_HIP;                                                       \
+        }                                                                                \
+    } while (0)
+
+DevTable::~DevTable() {
+    if (d_blob) (void)hipFree(d_blob);
+}
+
+int upload_table(int device, const nffacl_rules &rules, int algo, DevTable *&out) {
+    CompiledTable ct;
+    std::string err;
+    if (!compile_table(rules, algo, ct, err)) {
+        set_last_error("compile: " + err);
+        return NFFACL_ERR_INVALID_ARG;
+    }
+    HIP_TRY(hipSetDevice(device));
+    DevTable *t = new DevTable();
+    t->meta = std::move(ct);
+    t->bytes = t->meta.blob.size() * sizeof(uint32_t);
+    hipError_t e = hipMalloc(reinterpret_cast<void **>(&t->d_blob), t->bytes);
+    if (e != hipSuccess) {
+        set_last_error(std::string("hipMalloc(table): ") + hipGetErrorString(e));
+        delete t;
+        return NFFACL_ERR_NOMEM;
+    }
+    e = hipMemcpy(t->d_blob, t->meta.blob.data(), t->bytes, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        set_last_error(std::string("hipMemcpy(table): ") + hipGetErrorString(e));
+        delete t;
+        return NFFACL_ERR_HIP;
+    }
+    out = t;
+    return NFFACL_OK;
+}
+
+static uint32_t grid_for(const nffacl_engine *eng, uint64_t n, uint32_t block, uint32_t per_cu) {
+    const uint64_t waves_needed = (n + 63) / 64;
+    const uint64_t blocks_needed = (waves_needed * 64 + block - 1) / block;
+    const uint64_t cap = uint64_t(eng->num_cus) * per_cu;
+    return static_cast<uint32_t>(std::max<uint64_t>(1, std::min(blocks_needed, cap)));
+}
+
+int launch_slots(nffacl_engine *eng, const DevTable *t, const uint8_t *d_slots, uint32_t stride,
+                 uint64_t n, uint32_t *d_port, uint64_t *d_permit, hipStream_t stream) {
+    if (n == 0) return NFFACL_OK;
+    const uint32_t block = 256;
+    dev::LinearArgs a{t->d_blob + t->meta.off_rec4, t->meta.n4, t->d_blob + t->meta.off_rec6,
+                      t->meta.n6};
+    const uint32_t grid = grid_for(eng, n, block, 8);
+    hipLaunchKernelGGL(dev::k_linear_slots, dim3(grid), dim3(block), 0, stream, d_slots, stride,
+                       n, a, d_port, d_permit);
+    HIP_TRY(hipGetLastError());
+    return NFFACL_OK;
+}
+
+int launch_frames(nffacl_engine *eng, const DevTable *t, const uint8_t *d_frames,
+                  const uint64_t *d_desc, uint64_t n, uint32_t *d_port, uint64_t *d_permit,
+                  hipStream_t stream) {
+    if (n == 0) return NFFACL_OK;
+    const uint32_t block = 256;
+    dev::LinearArgs a{t->d_blob + t->meta.off_rec4, t->meta.n4, t->d_blob + t->meta.off_rec6,
+                      t->meta.n6};
+    const uint32_t grid = grid_for(eng, n, block, 8);
+    hipLaunchKernelGGL(dev::k_linear_frames, dim3(grid), dim3(block), 0, stream, d_frames, d_desc,
+                       n, a, d_port, d_permit);
+    HIP_TRY(hipGetLastError());
+    return NFFACL_OK;
+}
+
+}  // namespace nffacl

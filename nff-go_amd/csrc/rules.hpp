@@ -1,0 +1,54 @@
+// rules.hpp — host-side rule set of libnffacl (internal).
+//
+// nffacl_rules is the C-ABI handle for the reference's *packet.L3Rules
+// (packet/acl.go:451-455): two ordered slices, one per address family, in the
+// order the rule file lists them.  Records keep the reference's field meaning
+// exactly (see include/nffacl.h); the device compiler (compile.cpp) derives its
+// own layouts from them.
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "nffacl.h"
+
+struct nffacl_rules {
+    std::vector<nffacl_rule4> ip4;
+    std::vector<nffacl_rule6> ip6;
+};
+
+namespace nffacl {
+
+// One line of a rule file after field splitting: acl.go:55-62 rawL3Rule.
+struct RawL3Rule {
+    std::string src_addr, dst_addr, id, src_port, dst_port, output_number;
+};
+
+struct ParseError {
+    int code = NFFACL_OK;  // negated common.ErrorCode
+    std::string message;
+};
+
+// rawL3Parse (acl.go:226-355).  Appends to `out`; returns false and fills
+// `err` at the first bad rule.
+bool raw_l3_parse(const std::vector<RawL3Rule> &raw, nffacl_rules &out, ParseError &err);
+
+// GetL3ACLFromTextTable body (acl.go:156-177) over an in-memory file image.
+bool parse_text_table(const char *data, size_t len, nffacl_rules &out, ParseError &err);
+
+// GetL3ACLFromJSON body (acl.go:129-133) over an in-memory file image.
+bool parse_json(const char *data, size_t len, nffacl_rules &out, ParseError &err);
+
+// go1.13 net.ParseCIDR restricted to what rawL3Parse consumes: the masked
+// network address (4 bytes for dotted-quad input, 16 for IPv6 syntax) and the
+// mask.  Returns false where Go returns an error.
+bool go_parse_cidr(const std::string &s, std::vector<uint8_t> &ip, std::vector<uint8_t> &mask);
+
+// go1.13 strings.Fields (unicode.IsSpace separators).
+std::vector<std::string> go_fields(const std::string &line);
+
+// go1.13 strconv.ParseUint(s, 10, bits).
+bool go_parse_uint10(const std::string &s, int bits, uint64_t &out);
+
+}  // namespace nffacl

@@ -1,0 +1,298 @@
+"""nffacl — Python binding of libnffacl (ctypes over include/nffacl.h).
+
+Used by the parity tests, bench.py and __graft_entry__.  Names mirror the
+reference API this path replaces (packet/acl.go):
+
+  GetL3ACLFromTextTable(filename) -> (L3Rules, NFError|None)   acl.go:148
+  GetL3ACLFromJSON(filename)      -> (L3Rules, NFError|None)   acl.go:121
+  Engine(rules).L3ACLPort / L3ACLPermit over whole packet batches
+                                   (acl.go:495-506, run on the GPU)
+
+There is no CPU fallback: every verdict comes from the HIP kernels in
+libnffacl.so.  Importing this module fails loudly if the library is missing.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+import numpy as np
+
+_HERE = Path(__file__).resolve().parent
+LIB_PATH = Path(os.environ.get("NFFACL_LIB", _HERE.parent / "libnffacl.so"))
+
+if not LIB_PATH.exists():
+    raise ImportError(
+        f"libnffacl.so not found at {LIB_PATH}; build it with `make -C nff-go_amd` "
+        "(or __graft_entry__.build()).  There is no CPU fallback.")
+
+_lib = ctypes.CDLL(str(LIB_PATH))
+
+# ---- status codes (include/nffacl.h) -----------------------------------------
+OK = 0
+ERR_PARSE_RULE_JSON = -11
+ERR_FILE = -12
+ERR_PARSE_RULE = -13
+ERR_INCORRECT_ARG_IN_RULES = -14
+ERR_INCORRECT_RULE = -15
+ERR_INVALID_ARG = -100
+ERR_NOMEM = -101
+ERR_HIP = -102
+ERR_NO_DEVICE = -103
+ERR_UNSUPPORTED = -104
+
+ALGO_AUTO, ALGO_LINEAR, ALGO_INDEXED = 0, 1, 2
+
+# ---- record layouts ------------------------------------------------------------
+_L4 = [("id", "u1"), ("id_mask", "u1"), ("valid", "u1"), ("reserved", "u1"),
+       ("src_port_min", "<u2"), ("src_port_max", "<u2"),
+       ("dst_port_min", "<u2"), ("dst_port_max", "<u2")]
+RULE4 = np.dtype([("output_number", "<u4"), ("src_addr", "<u4"), ("dst_addr", "<u4"),
+                  ("src_mask", "<u4"), ("dst_mask", "<u4")] + _L4)
+RULE6 = np.dtype([("output_number", "<u4"), ("src_addr", "u1", 16), ("dst_addr", "u1", 16),
+                  ("src_mask", "u1", 16), ("dst_mask", "u1", 16)] + _L4)
+assert RULE4.itemsize == 32 and RULE6.itemsize == 80
+
+_vp, _sz, _u32, _u64, _i = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
+_pp = ctypes.POINTER(ctypes.c_void_p)
+
+
+def _sig(name, res, *args):
+    f = getattr(_lib, name)
+    f.restype = res
+    f.argtypes = list(args)
+    return f
+
+
+_rules_load_text = _sig("nffacl_rules_load_text", _i, ctypes.c_char_p, _pp, ctypes.c_char_p, _sz)
+_rules_parse_text = _sig("nffacl_rules_parse_text", _i, ctypes.c_char_p, _sz, _pp, ctypes.c_char_p, _sz)
+_rules_load_json = _sig("nffacl_rules_load_json", _i, ctypes.c_char_p, _pp, ctypes.c_char_p, _sz)
+_rules_parse_json = _sig("nffacl_rules_parse_json", _i, ctypes.c_char_p, _sz, _pp, ctypes.c_char_p, _sz)
+_rules_from_arrays = _sig("nffacl_rules_from_arrays", _i, _vp, _sz, _vp, _sz, _pp)
+_rules_free = _sig("nffacl_rules_free", None, _vp)
+_rules_counts = _sig("nffacl_rules_counts", _i, _vp, ctypes.POINTER(_sz), ctypes.POINTER(_sz))
+_rules_get4 = _sig("nffacl_rules_get4", _i, _vp, _sz, _vp)
+_rules_get6 = _sig("nffacl_rules_get6", _i, _vp, _sz, _vp)
+_engine_create_ex = _sig("nffacl_engine_create_ex", _i, _i, _vp, _i, _pp)
+_engine_swap = _sig("nffacl_engine_swap_rules", _i, _vp, _vp)
+_engine_destroy = _sig("nffacl_engine_destroy", None, _vp)
+_engine_algo = _sig("nffacl_engine_algo", _i, _vp)
+_engine_table_bytes = _sig("nffacl_engine_table_bytes", _i, _vp, ctypes.POINTER(_u64))
+_classify_device = _sig("nffacl_classify_device", _i, _vp, _vp, _u32, _u64, _vp, _vp, _vp)
+_classify_frames = _sig("nffacl_classify_frames_device", _i, _vp, _vp, _vp, _u64, _vp, _vp, _vp)
+_classify_host = _sig("nffacl_classify_host", _i, _vp, _vp, _u32, _u64, _vp, _vp)
+_strerror = _sig("nffacl_strerror", ctypes.c_char_p, _i)
+_last_error = _sig("nffacl_last_error", ctypes.c_char_p)
+_abi_version = _sig("nffacl_abi_version", _i)
+
+EXPORTED_SYMBOLS = [
+    "nffacl_rules_load_text", "nffacl_rules_parse_text", "nffacl_rules_load_json",
+    "nffacl_rules_parse_json", "nffacl_rules_from_arrays", "nffacl_rules_free",
+    "nffacl_rules_counts", "nffacl_rules_get4", "nffacl_rules_get6",
+    "nffacl_engine_create", "nffacl_engine_create_ex", "nffacl_engine_swap_rules",
+    "nffacl_engine_destroy", "nffacl_engine_algo", "nffacl_engine_table_bytes",
+    "nffacl_classify_device", "nffacl_classify_frames_device", "nffacl_classify_host",
+    "nffacl_strerror", "nffacl_abi_version", "nffacl_last_error",
+]
+
+
+def abi_version() -> int:
+    return _abi_version()
+
+
+class NFError(Exception):
+    """Mirror of common.NFError (common/error.go:54-66): Code is the positive
+    common.ErrorCode for parser errors; engine errors keep the negative status."""
+
+    def __init__(self, status: int, message: str):
+        self.status = status
+        self.code = -status if -15 <= status <= -11 else status
+        self.message = message
+        super().__init__(message)
+
+
+def _raise(status: int, what: str = ""):
+    detail = (_last_error() or b"").decode(errors="replace")
+    msg = f"{what}: {_strerror(status).decode()}" + (f" [{detail}]" if detail else "")
+    raise NFError(status, msg)
+
+
+def _ptr(x) -> int | None:
+    """Raw pointer of a torch tensor / numpy array / int / None."""
+    if x is None:
+        return None
+    if isinstance(x, int):
+        return x
+    if hasattr(x, "data_ptr"):
+        return x.data_ptr()
+    if isinstance(x, np.ndarray):
+        return x.ctypes.data
+    raise TypeError(f"cannot take a pointer of {type(x)}")
+
+
+class L3Rules:
+    """Owner of an nffacl_rules handle (the reference's *packet.L3Rules)."""
+
+    def __init__(self, handle):
+        self._h = handle
+
+    def __del__(self):
+        h, self._h = getattr(self, "_h", None), None
+        if h:
+            _rules_free(h)
+
+    @property
+    def handle(self):
+        return self._h
+
+    @staticmethod
+    def _parse(fn, *args):
+        out = ctypes.c_void_p()
+        err = ctypes.create_string_buffer(512)
+        st = fn(*args, ctypes.byref(out), err, len(err))
+        if st != OK:
+            raise NFError(st, err.value.decode(errors="replace"))
+        return L3Rules(out.value)
+
+    @classmethod
+    def from_text_file(cls, path) -> "L3Rules":
+        return cls._parse(_rules_load_text, str(path).encode())
+
+    @classmethod
+    def parse_text(cls, text: bytes | str) -> "L3Rules":
+        b = text.encode() if isinstance(text, str) else bytes(text)
+        return cls._parse(_rules_parse_text, b, len(b))
+
+    @classmethod
+    def from_json_file(cls, path) -> "L3Rules":
+        return cls._parse(_rules_load_json, str(path).encode())
+
+    @classmethod
+    def parse_json(cls, text: bytes | str) -> "L3Rules":
+        b = text.encode() if isinstance(text, str) else bytes(text)
+        return cls._parse(_rules_parse_json, b, len(b))
+
+    @classmethod
+    def from_arrays(cls, ip4=None, ip6=None) -> "L3Rules":
+        a4 = np.ascontiguousarray(ip4 if ip4 is not None else np.zeros(0, RULE4), RULE4)
+        a6 = np.ascontiguousarray(ip6 if ip6 is not None else np.zeros(0, RULE6), RULE6)
+        out = ctypes.c_void_p()
+        st = _rules_from_arrays(a4.ctypes.data if len(a4) else None, len(a4),
+                                a6.ctypes.data if len(a6) else None, len(a6), ctypes.byref(out))
+        if st != OK:
+            _raise(st, "nffacl_rules_from_arrays")
+        return L3Rules(out.value)
+
+    def counts(self):
+        n4, n6 = _sz(), _sz()
+        st = _rules_counts(self._h, ctypes.byref(n4), ctypes.byref(n6))
+        if st != OK:
+            _raise(st, "nffacl_rules_counts")
+        return n4.value, n6.value
+
+    def ip4(self) -> np.ndarray:
+        n4, _ = self.counts()
+        a = np.zeros(n4, RULE4)
+        for i in range(n4):
+            _rules_get4(self._h, i, a[i:i + 1].ctypes.data)
+        return a
+
+    def ip6(self) -> np.ndarray:
+        _, n6 = self.counts()
+        a = np.zeros(n6, RULE6)
+        for i in range(n6):
+            _rules_get6(self._h, i, a[i:i + 1].ctypes.data)
+        return a
+
+
+def GetL3ACLFromTextTable(filename):
+    """(rules, err) like the Go API; rules is None on error."""
+    try:
+        return L3Rules.from_text_file(filename), None
+    except NFError as e:
+        return None, e
+
+
+def GetL3ACLFromJSON(filename):
+    try:
+        return L3Rules.from_json_file(filename), None
+    except NFError as e:
+        return None, e
+
+
+class Engine:
+    """A compiled rule table resident on one HIP device."""
+
+    def __init__(self, rules: L3Rules, device: int = 0, algo: int = ALGO_AUTO):
+        out = ctypes.c_void_p()
+        st = _engine_create_ex(device, rules.handle, algo, ctypes.byref(out))
+        if st != OK:
+            _raise(st, "nffacl_engine_create")
+        self._h = out.value
+        self.device = device
+
+    def close(self):
+        h, self._h = getattr(self, "_h", None), None
+        if h:
+            _engine_destroy(h)
+
+    def __del__(self):
+        self.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    @property
+    def algo(self) -> int:
+        return _engine_algo(self._h)
+
+    @property
+    def table_bytes(self) -> int:
+        b = _u64()
+        st = _engine_table_bytes(self._h, ctypes.byref(b))
+        if st != OK:
+            _raise(st, "nffacl_engine_table_bytes")
+        return b.value
+
+    def swap_rules(self, rules: L3Rules):
+        st = _engine_swap(self._h, rules.handle)
+        if st != OK:
+            _raise(st, "nffacl_engine_swap_rules")
+
+    def classify_device(self, slots, stride: int, n: int, port=None, permit_bits=None, stream=None):
+        """Asynchronous on `stream` (a torch.cuda.Stream, raw handle or None)."""
+        s = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
+        st = _classify_device(self._h, _ptr(slots), stride, n, _ptr(port), _ptr(permit_bits), s)
+        if st != OK:
+            _raise(st, "nffacl_classify_device")
+
+    def classify_frames_device(self, frames, desc, n: int, port=None, permit_bits=None, stream=None):
+        s = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
+        st = _classify_frames(self._h, _ptr(frames), _ptr(desc), n, _ptr(port), _ptr(permit_bits), s)
+        if st != OK:
+            _raise(st, "nffacl_classify_frames_device")
+
+    def classify_host(self, slots: np.ndarray, stride: int, n: int | None = None):
+        """Host slots (uint8, n*stride bytes) -> (port uint32[n], permit uint8[n])."""
+        slots = np.ascontiguousarray(slots, np.uint8)
+        if n is None:
+            n = slots.size // stride
+        if slots.size < n * stride:
+            raise ValueError("slot buffer too small")
+        port = np.zeros(n, np.uint32)
+        permit = np.zeros(n, np.uint8)
+        st = _classify_host(self._h, slots.ctypes.data, stride, n, port.ctypes.data, permit.ctypes.data)
+        if st != OK:
+            _raise(st, "nffacl_classify_host")
+        return port, permit
+
+    # Batch forms of the reference's per-packet API (acl.go:495-506)
+    def L3ACLPort(self, slots: np.ndarray, stride: int):
+        return self.classify_host(slots, stride)[0]
+
+    def L3ACLPermit(self, slots: np.ndarray, stride: int):
+        return self.classify_host(slots, stride)[1].astype(bool)

@@ -1,0 +1,341 @@
+"""HIP path vs the CPU oracle — bit-exact verdicts (run on an MI355X: -m gpu).
+
+Every verdict here comes from libnffacl's HIP kernels through the C-ABI
+(nffacl.Engine -> nffacl_classify_*).  The oracle (oracle/acl_oracle.c, pinned
+by tests/test_oracle.py against the reference's KATs) is only the checker.
+"""
+import json
+
+import numpy as np
+import pytest
+
+import nffacl
+from nffacl import synth
+from oracle import oracle, rules_oracle as ro
+
+pytestmark = pytest.mark.gpu
+
+ALGOS = [nffacl.ALGO_LINEAR, nffacl.ALGO_INDEXED]
+THREADS = 16
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    torch.cuda.init()
+    return torch
+
+
+def to_dev(torch, arr: np.ndarray):
+    return torch.from_numpy(np.ascontiguousarray(arr)).to("cuda")
+
+
+def classify(torch, eng, slots: np.ndarray, stride: int, n: int):
+    d_slots = to_dev(torch, slots.view(np.uint8))
+    port = torch.zeros(max(n, 1), dtype=torch.int32, device="cuda")
+    permit = torch.zeros(max((n + 63) // 64, 1), dtype=torch.int64, device="cuda")
+    eng.classify_device(d_slots, stride, n, port, permit)
+    torch.cuda.synchronize()
+    p = port.cpu().numpy().view(np.uint32)[:n]
+    b = permit.cpu().numpy().view(np.uint64)[:(n + 63) // 64]
+    return p, b
+
+
+def permit_bits(port: np.ndarray) -> np.ndarray:
+    n = len(port)
+    bits = np.zeros((n + 63) // 64 * 64, np.uint64)
+    bits[:n] = (port != 0).astype(np.uint64)
+    bits = bits.reshape(-1, 64) << np.arange(64, dtype=np.uint64)[None, :]
+    return np.bitwise_or.reduce(bits, axis=1)
+
+
+def slot_buffer(frames, stride):
+    buf = np.zeros((len(frames), stride), np.uint8)
+    for i, f in enumerate(frames):
+        f = f[:stride]
+        buf[i, :len(f)] = np.frombuffer(f, np.uint8)
+    return buf.reshape(-1)
+
+
+# ---- reference known answers on the GPU -------------------------------------------
+
+@pytest.mark.parametrize("algo", ALGOS)
+@pytest.mark.parametrize("stride", [64, 256])
+def test_match_kats_gpu(torch_cuda, golden, algo, stride):
+    """All 7369 cases of acl_internal_test.go:501-1141 through the HIP path."""
+    torch = torch_cuda
+    z = np.load(golden / "acl_match_kats.npz", allow_pickle=False)
+    pk = json.loads((golden / "kat_packets.json").read_text())
+    frames = [bytes.fromhex(pk[name]) for name in z["packet_names"]]
+    slots = slot_buffer(frames, stride)
+    d_slots = to_dev(torch, slots)
+    total = len(z["c4_want"]) + len(z["c6_want"])
+    out = torch.zeros((total, 8), dtype=torch.int32, device="cuda")
+    engines, wants, pkts = [], [], []
+    row = 0
+    for fam in (4, 6):
+        rules = z[f"c{fam}_rule"]
+        for i in range(len(rules)):
+            rs = nffacl.L3Rules.from_arrays(rules[i:i + 1], None) if fam == 4 else \
+                nffacl.L3Rules.from_arrays(None, rules[i:i + 1])
+            eng = nffacl.Engine(rs, algo=algo)
+            eng.classify_device(d_slots, stride, len(frames), out[row])
+            engines.append(eng)
+            wants.append(int(z[f"c{fam}_want"][i]))
+            pkts.append(int(z[f"c{fam}_packet"][i]))
+            row += 1
+            if len(engines) >= 256:  # keep device tables bounded
+                torch.cuda.synchronize()
+                for e in engines:
+                    e.close()
+                engines.clear()
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(np.uint32)
+    verdict = got[np.arange(total), np.array(pkts)]
+    bad = np.nonzero(verdict != np.array(wants, np.uint32))[0]
+    assert len(bad) == 0, [(int(i), int(verdict[i]), wants[i]) for i in bad[:10]]
+
+
+@pytest.mark.parametrize("algo", ALGOS)
+def test_header_parse_kat_gpu(torch_cuda, golden, algo):
+    """packet_test.go:22-338 frames: exact-match rule hits, each perturbed field misses."""
+    torch = torch_cuda
+    cases = json.loads((golden / "parse_l3_kat.json").read_text())
+    frames = [bytes.fromhex(c["hex"]) for c in cases]
+    slots = slot_buffer(frames, 64)
+    for k, c in enumerate(cases):
+        sp = ((c["src_port_le"] & 0xFF) << 8) | (c["src_port_le"] >> 8)
+        dp = ((c["dst_port_le"] & 0xFF) << 8) | (c["dst_port_le"] >> 8)
+        base = dict(output_number=7, src_addr=c["src_addr"], dst_addr=c["dst_addr"], src_mask=0xFFFFFFFF,
+                    dst_mask=0xFFFFFFFF, id=c["proto"], id_mask=0xFF, valid=1, src_port_min=sp,
+                    src_port_max=sp, dst_port_min=dp, dst_port_max=dp)
+        variants = [({}, 7), ({"src_addr": c["src_addr"] ^ 0x01000000}, 0),
+                    ({"dst_addr": c["dst_addr"] ^ 0x100}, 0), ({"id": c["proto"] ^ 0x10}, 0),
+                    ({"src_port_min": (sp + 1) & 0xFFFF, "src_port_max": (sp + 1) & 0xFFFF}, 0),
+                    ({"dst_port_min": (dp + 1) & 0xFFFF, "dst_port_max": (dp + 1) & 0xFFFF}, 0)]
+        for over, want in variants:
+            r = np.zeros(1, nffacl.RULE4)
+            for key, v in {**base, **over}.items():
+                r[key] = v
+            with nffacl.Engine(nffacl.L3Rules.from_arrays(r), algo=algo) as eng:
+                p, _ = classify(torch, eng, slots, 64, len(frames))
+            assert p[k] == want, (k, over)
+
+
+# ---- synthetic batches vs the oracle ---------------------------------------------
+
+def _rules_and_arrays(text: str):
+    return nffacl.L3Rules.parse_text(text), ro.parse_text_table(text.encode()).arrays()
+
+
+@pytest.mark.parametrize("algo", ALGOS)
+def test_firewall_conf_c1(torch_cuda, golden, algo):
+    text = (golden / "rules" / "firewall.conf").read_text()
+    rules, (a4, a6) = _rules_and_arrays(text)
+    g = synth.firewall_rules(text)
+    n = 1 << 18
+    slots = synth.gen_slots(g, n, synth.PACKET_SEEDS["c1"])
+    with nffacl.Engine(rules, algo=algo) as eng:
+        p, b = classify(torch_cuda, eng, slots, 64, n)
+    want = oracle.classify_slots(slots, 64, n, a4, a6, threads=THREADS)
+    np.testing.assert_array_equal(p, want)
+    np.testing.assert_array_equal(b, permit_bits(want))
+    assert 0 < (want != 0).mean() < 1
+
+
+@pytest.mark.parametrize("algo", ALGOS)
+def test_c2_1k_rules(torch_cuda, algo):
+    g = synth.gen_rules(synth.SPECS["c2"], synth.RULE_SEEDS["c2"])
+    rules, (a4, a6) = _rules_and_arrays(g.text)
+    n = (1 << 20) + 37  # ragged tail
+    slots = synth.gen_slots(g, n, synth.PACKET_SEEDS["c2"])
+    with nffacl.Engine(rules, algo=algo) as eng:
+        p, b = classify(torch_cuda, eng, slots, 64, n)
+    want = oracle.classify_slots(slots, 64, n, a4, a6, threads=THREADS)
+    np.testing.assert_array_equal(p, want)
+    np.testing.assert_array_equal(b, permit_bits(want))
+
+
+@pytest.mark.parametrize("algo", ALGOS)
+def test_c5_port_ranges(torch_cuda, algo):
+    spec = synth.RuleSpec(20000, sport=(0.0, 0.7, 0.3), dport=(0.5, 0.4, 0.1))
+    g = synth.gen_rules(spec, synth.RULE_SEEDS["c5"])
+    rules, (a4, a6) = _rules_and_arrays(g.text)
+    n = 1 << 16
+    slots = synth.gen_slots(g, n, synth.PACKET_SEEDS["c5"])
+    with nffacl.Engine(rules, algo=algo) as eng:
+        p, _ = classify(torch_cuda, eng, slots, 64, n)
+    np.testing.assert_array_equal(p, oracle.classify_slots(slots, 64, n, a4, a6, threads=THREADS))
+
+
+@pytest.mark.parametrize("algo", ALGOS)
+def test_c3_imix_frames(torch_cuda, algo):
+    torch = torch_cuda
+    spec = synth.RuleSpec(10000, sport=(0.0, 0.2, 0.8), dport=(0.5, 0.3, 0.2))
+    g = synth.gen_rules(spec, synth.RULE_SEEDS["c3"])
+    rules, (a4, a6) = _rules_and_arrays(g.text)
+    n = 1 << 16
+    frames, desc = synth.gen_imix(g, n, synth.PACKET_SEEDS["c3"])
+    with nffacl.Engine(rules, algo=algo) as eng:
+        port = torch.zeros(n, dtype=torch.int32, device="cuda")
+        permit = torch.zeros((n + 63) // 64, dtype=torch.int64, device="cuda")
+        eng.classify_frames_device(to_dev(torch, frames), to_dev(torch, desc.view(np.int64)), n, port, permit)
+        torch.cuda.synchronize()
+    want = oracle.classify_frames(frames, desc, a4, a6, threads=THREADS)
+    got = port.cpu().numpy().view(np.uint32)
+    np.testing.assert_array_equal(got, want)
+    np.testing.assert_array_equal(permit.cpu().numpy().view(np.uint64), permit_bits(want))
+
+
+@pytest.mark.parametrize("algo", ALGOS)
+def test_ip_options_and_wide_slots(torch_cuda, algo):
+    """IHL 0..15 with 128-byte slots: ports at bytes up to 77 are real bytes;
+    with 64-byte slots the same frames read zeros past byte 63."""
+    rng = np.random.default_rng(3)
+    n = 4096
+    frames = []
+    for i in range(n):
+        ihl = i % 16
+        f = bytearray(rng.integers(0, 256, 128, dtype=np.uint8).tobytes())
+        f[12:14] = b"\x08\x00"
+        f[14] = 0x40 | ihl
+        f[23] = [6, 17, 1][i % 3]
+        frames.append(bytes(f))
+    text = "\n".join(f"ANY ANY {p} {a}:{b} {c}:{d} {o}" for p, a, b, c, d, o in [
+        ("TCP", 0, 30000, 0, 65535, 2), ("UDP", 20000, 65535, 100, 40000, 3), ("ANY", 0, 0, 0, 65535, 4),
+        ("ANY", 0, 65535, 0, 0, 5), ("ANY", 1000, 50000, 1000, 50000, 6)]) + "\n"
+    rules, (a4, a6) = _rules_and_arrays(text)
+    for stride in (64, 128):
+        slots = slot_buffer(frames, stride)
+        with nffacl.Engine(rules, algo=algo) as eng:
+            p, _ = classify(torch_cuda, eng, slots, stride, n)
+        np.testing.assert_array_equal(p, oracle.classify_slots(slots, stride, n, a4, a6))
+
+
+@pytest.mark.parametrize("algo", ALGOS)
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 1000])
+def test_ragged_sizes(torch_cuda, algo, n):
+    g = synth.gen_rules(synth.RuleSpec(300), 11)
+    rules, (a4, a6) = _rules_and_arrays(g.text)
+    slots = synth.gen_slots(g, n, 12)
+    with nffacl.Engine(rules, algo=algo) as eng:
+        p, b = classify(torch_cuda, eng, slots, 64, n)
+    want = oracle.classify_slots(slots, 64, n, a4, a6)
+    np.testing.assert_array_equal(p, want)
+    np.testing.assert_array_equal(b, permit_bits(want))
+
+
+def test_empty_batch_and_empty_rules(torch_cuda):
+    torch = torch_cuda
+    empty = nffacl.L3Rules.from_arrays(None, None)
+    g = synth.gen_rules(synth.RuleSpec(10), 1)
+    slots = synth.gen_slots(g, 256, 2)
+    with nffacl.Engine(empty) as eng:
+        p, b = classify(torch, eng, slots, 64, 256)
+        assert not p.any() and not b.any()
+        eng.classify_device(to_dev(torch, slots), 64, 0, None, None)  # n == 0 is a no-op
+    only6 = nffacl.L3Rules.parse_text(b"::/0 ANY ANY ANY ANY 9\n")
+    with nffacl.Engine(only6) as eng:
+        p, _ = classify(torch, eng, slots, 64, 256)
+    want = oracle.classify_slots(slots, 64, 256, *ro.parse_text_table(b"::/0 ANY ANY ANY ANY 9\n").arrays())
+    np.testing.assert_array_equal(p, want)
+
+
+def test_invalid_arguments(torch_cuda):
+    torch = torch_cuda
+    rules = nffacl.L3Rules.parse_text(b"ANY ANY ANY ANY ANY Accept\n")
+    with nffacl.Engine(rules) as eng:
+        buf = torch.zeros(4096, dtype=torch.uint8, device="cuda")
+        out = torch.zeros(64, dtype=torch.int32, device="cuda")
+        for stride in (0, 48, 72):
+            with pytest.raises(nffacl.NFError):
+                eng.classify_device(buf, stride, 16, out)
+        with pytest.raises(nffacl.NFError):
+            eng.classify_device(buf.data_ptr() + 4, 64, 16, out)  # misaligned slots
+
+
+def test_swap_rules_between_batches(torch_cuda):
+    torch = torch_cuda
+    g = synth.gen_rules(synth.RuleSpec(500), 21)
+    n = 1 << 14
+    slots = synth.gen_slots(g, n, 22)
+    r1, (a4, a6) = _rules_and_arrays(g.text)
+    r2, (b4, b6) = _rules_and_arrays(synth.gen_rules(synth.RuleSpec(700), 23).text)
+    with nffacl.Engine(r1) as eng:
+        p1, _ = classify(torch, eng, slots, 64, n)
+        eng.swap_rules(r2)
+        p2, _ = classify(torch, eng, slots, 64, n)
+        eng.swap_rules(r1)
+        p3, _ = classify(torch, eng, slots, 64, n)
+    np.testing.assert_array_equal(p1, oracle.classify_slots(slots, 64, n, a4, a6))
+    np.testing.assert_array_equal(p2, oracle.classify_slots(slots, 64, n, b4, b6))
+    np.testing.assert_array_equal(p3, p1)
+
+
+def test_classify_host_matches_device(torch_cuda):
+    g = synth.gen_rules(synth.SPECS["c2"], synth.RULE_SEEDS["c2"])
+    rules, (a4, a6) = _rules_and_arrays(g.text)
+    n = (1 << 21) + 5  # > one pipeline chunk, ragged
+    slots = synth.gen_slots(g, n, 99)
+    with nffacl.Engine(rules) as eng:
+        port, permit = eng.classify_host(slots, 64, n)
+    want = oracle.classify_slots(slots, 64, n, a4, a6, threads=THREADS)
+    np.testing.assert_array_equal(port, want)
+    np.testing.assert_array_equal(permit, (want != 0).astype(np.uint8))
+
+
+def test_stability_separate_split_proportions(torch_cuda, golden):
+    """testSingleWorkingFF.go: separate -> exactly the dst-port-111 third is
+    permitted; split -> outputs 1/2 by dst port (test-*.conf)."""
+    n = 3 * 4000
+    frames = []
+    for i in range(n):
+        f = bytearray(bytes.fromhex(json.loads((golden / "kat_packets.json").read_text())["ipv4_udp"]))
+        dport = (111, 222, 333)[i % 3]
+        f[36:38] = dport.to_bytes(2, "big")
+        frames.append(bytes(f))
+    slots = slot_buffer(frames, 64)
+    sep = nffacl.L3Rules.from_text_file(golden / "rules" / "test-separate-l3rules.conf")
+    with nffacl.Engine(sep) as eng:
+        p, _ = classify(torch_cuda, eng, slots, 64, n)
+    assert (p != 0).sum() == n // 3 and (p[0::3] == 1).all() and not p[1::3].any() and not p[2::3].any()
+    split = nffacl.L3Rules.from_text_file(golden / "rules" / "test-split.conf")
+    with nffacl.Engine(split) as eng:
+        p, _ = classify(torch_cuda, eng, slots, 64, n)
+    assert (p[0::3] == 1).all() and (p[1::3] == 2).all() and (p[2::3] == 3).all()
+
+
+# ---- BASELINE-size properties (2^24 packets, C2) ------------------------------------
+
+def test_full_size_c2_properties(torch_cuda):
+    """At the bench size: linear == indexed on every packet, a 2^16 random
+    sample equals the oracle, and classifying two halves separately equals
+    classifying the whole batch (size independence)."""
+    torch = torch_cuda
+    g = synth.gen_rules(synth.SPECS["c2"], synth.RULE_SEEDS["c2"])
+    rules, (a4, a6) = _rules_and_arrays(g.text)
+    n = 1 << 24
+    slots = synth.gen_slots(g, n, synth.PACKET_SEEDS["c2"])
+    d_slots = to_dev(torch, slots)
+    del slots
+    outs = {}
+    for algo in ALGOS:
+        with nffacl.Engine(rules, algo=algo) as eng:
+            port = torch.zeros(n, dtype=torch.int32, device="cuda")
+            eng.classify_device(d_slots, 64, n, port)
+            half = torch.zeros(n, dtype=torch.int32, device="cuda")
+            h = n // 2 + 64 * 3 + 17
+            eng.classify_device(d_slots, 64, h, half)
+            eng.classify_device(d_slots.data_ptr() + h * 64, 64, n - h, half.data_ptr() + h * 4)
+            torch.cuda.synchronize()
+            assert torch.equal(port, half)
+            outs[algo] = port
+    assert torch.equal(outs[nffacl.ALGO_LINEAR], outs[nffacl.ALGO_INDEXED])
+    rng = np.random.default_rng(5)
+    idx = np.sort(rng.choice(n, 1 << 16, replace=False))
+    sample = d_slots.view(n, 64)[torch.from_numpy(idx).to("cuda")].cpu().numpy().reshape(-1)
+    want = oracle.classify_slots(sample, 64, len(idx), a4, a6, threads=THREADS)
+    got = outs[nffacl.ALGO_LINEAR].cpu().numpy().view(np.uint32)[idx]
+    np.testing.assert_array_equal(got, want)
