@@ -87,17 +87,24 @@ def cpu_baseline(slots: np.ndarray, n: int, a4, a6, budget_s: float):
     oracle.classify_slots(slots, 64, cal, a4, a6, threads=cores)
     rate = cal / max(time.perf_counter() - t, 1e-6)
     sample = int(min(n, max(cal, rate * budget_s)))
-    t = time.perf_counter()
-    ports, which = oracle.classify_slots_which(slots, 64, sample, a4, a6, threads=cores)
-    dt = time.perf_counter() - t
+    passes, done, dt = 0, 0, 0.0
+    while True:  # whole passes over the sample until ~budget_s of CPU work
+        t = time.perf_counter()
+        ports, which = oracle.classify_slots_which(slots, 64, sample, a4, a6, threads=cores)
+        dt += time.perf_counter() - t
+        passes += 1
+        done += sample
+        if dt >= budget_s or passes >= 50:
+            break
     t1 = time.perf_counter()
     one = min(sample, 1 << 16)
     oracle.classify_slots(slots, 64, one, a4, a6, threads=1)
     dt1 = time.perf_counter() - t1
     hit = which >= 0
     return {
-        "value": round(sample / dt / 1e6, 3), "unit": "Mpps", "cores": cores, "kind": "port",
-        "sample": f"first {sample} packets of rank 0's batch (oracle/acl_oracle.c, {cores} threads, {dt:.1f}s)",
+        "value": round(done / dt / 1e6, 3), "unit": "Mpps", "cores": cores, "kind": "port",
+        "sample": f"first {sample} packets of rank 0's batch x {passes} pass(es) "
+                  f"(oracle/acl_oracle.c = acl.go l3ACL restated in C, {cores} threads, {dt:.1f}s)",
         "single_core_mpps": round(one / dt1 / 1e6, 3),
         "mean_first_match_index": round(float(which[hit].mean()), 1) if hit.any() else None,
         "match_fraction": round(float(hit.mean()), 4),

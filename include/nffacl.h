@@ -166,6 +166,39 @@ NFFACL_API int nffacl_engine_algo(const nffacl_engine *eng);
 /* Bytes of the active device table (rule records + index), for reporting. */
 NFFACL_API int nffacl_engine_table_bytes(const nffacl_engine *eng, uint64_t *bytes);
 
+/* Host-side compilation of a rule set into the device table blob, without a
+ * device (tooling / inspection; the engine runs the same compiler).  Call with
+ * blob == NULL to learn info->blob_dwords, then again with a buffer of at
+ * least that many dwords. */
+typedef struct nffacl_dim_info {
+    uint32_t kind;       /* key: 0 src4, 1 dst4, 2 src6 (top 32 bits), 3 dst6, 4 sport, 5 dport */
+    uint32_t shift;      /* radix bucket = key >> shift */
+    uint32_t n_bounds;   /* elementary intervals */
+    uint32_t off_radix, off_bounds, off_lists, off_cands; /* dword offsets into the blob */
+    uint32_t n_rules;    /* rules indexed by this key */
+    uint64_t n_cands;    /* candidate-list entries (with replication) */
+    uint32_t max_list;   /* longest candidate list */
+    uint32_t reserved;
+} nffacl_dim_info;
+
+typedef struct nffacl_family_info {
+    uint32_t n_dims;
+    uint32_t off_rec;    /* dword offset of the rule records (8 dwords IPv4, 20 IPv6) */
+    uint32_t n_rec;      /* live records */
+    uint32_t off_resid, n_resid; /* records scanned linearly (no selective key) */
+    nffacl_dim_info dims[4];
+} nffacl_family_info;
+
+typedef struct nffacl_table_info {
+    int32_t algo;        /* NFFACL_ALGO_LINEAR or NFFACL_ALGO_INDEXED */
+    uint32_t reserved;
+    uint64_t blob_dwords;
+    nffacl_family_info fam[2]; /* [0] IPv4, [1] IPv6 */
+} nffacl_table_info;
+
+NFFACL_API int nffacl_table_compile(const nffacl_rules *rules, int algo, uint32_t *blob,
+                                    uint64_t cap_dwords, nffacl_table_info *info);
+
 /* ---- classification ------------------------------------------------------ */
 
 /* Device-resident dense slots: packet i occupies d_slots[i*stride, (i+1)*stride)

@@ -12,6 +12,7 @@
 
 #include "engine.hpp"
 #include "nffacl.h"
+#include "compile.hpp"
 #include "rules.hpp"
 
 using namespace nffacl;
@@ -182,6 +183,42 @@ int nffacl_rules_get6(const nffacl_rules *rules, size_t i, nffacl_rule6 *out) {
     return NFFACL_OK;
 }
 
+// ---- host-side table compilation ------------------------------------------
+
+int nffacl_table_compile(const nffacl_rules *rules, int algo, uint32_t *blob, uint64_t cap_dwords,
+                         nffacl_table_info *info) {
+    if (!rules || !info) return NFFACL_ERR_INVALID_ARG;
+    CompiledTable ct;
+    std::string err;
+    if (!compile_table(*rules, algo, ct, err)) {
+        set_last_error("compile: " + err);
+        return NFFACL_ERR_INVALID_ARG;
+    }
+    std::memset(info, 0, sizeof(*info));
+    info->algo = ct.algo;
+    info->blob_dwords = ct.blob.size();
+    const FamilyIndex *fi[2] = {&ct.idx4, &ct.idx6};
+    const uint32_t off_rec[2] = {ct.off_rec4, ct.off_rec6}, n_rec[2] = {ct.n4, ct.n6};
+    for (int f = 0; f < 2; ++f) {
+        nffacl_family_info &o = info->fam[f];
+        o.n_dims = fi[f]->n_dims;
+        o.off_rec = off_rec[f];
+        o.n_rec = n_rec[f];
+        o.off_resid = fi[f]->off_resid;
+        o.n_resid = fi[f]->n_resid;
+        for (int k = 0; k < 4; ++k) {
+            const DimInfo &d = fi[f]->dims[k];
+            o.dims[k] = nffacl_dim_info{d.kind, d.shift, d.n_bounds, d.off_radix, d.off_bounds, d.off_lists,
+                                        d.off_cands, d.n_rules, d.n_cands, d.max_list, 0};
+        }
+    }
+    if (blob) {
+        if (cap_dwords < ct.blob.size()) return NFFACL_ERR_INVALID_ARG;
+        std::memcpy(blob, ct.blob.data(), ct.blob.size() * sizeof(uint32_t));
+    }
+    return NFFACL_OK;
+}
+
 // ---- engine ----------------------------------------------------------------
 
 int nffacl_engine_create_ex(int hip_device, const nffacl_rules *rules, int algo, nffacl_engine **out) {
@@ -195,6 +232,8 @@ int nffacl_engine_create_ex(int hip_device, const nffacl_rules *rules, int algo,
     }
     if (hip_device < 0 || hip_device >= count) return NFFACL_ERR_INVALID_ARG;
     HIP_CHECK(hipSetDevice(hip_device));
+    int pst = prepare_kernels();
+    if (pst != NFFACL_OK) return pst;
     nffacl_engine *eng = new (std::nothrow) nffacl_engine();
     if (!eng) return NFFACL_ERR_NOMEM;
     eng->device = hip_device;

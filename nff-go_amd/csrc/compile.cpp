@@ -10,6 +10,9 @@
 //    directly, never from the parsers) can never match and is dropped here.
 #include "compile.hpp"
 
+#include <algorithm>
+#include <cmath>
+#include <array>
 #include <cstring>
 
 namespace nffacl {
@@ -59,6 +62,222 @@ bool emit_rec6(const nffacl_rule6 &r, std::vector<uint32_t> &out) {
 
 }  // namespace
 
+// ---------------------------------------------------------------------------
+// Indexed table
+// ---------------------------------------------------------------------------
+
+namespace {
+
+uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+
+uint32_t lead_ones(uint32_t m) { return m == 0xFFFFFFFFu ? 32u : static_cast<uint32_t>(__builtin_clz(~m)); }
+
+struct KeyRange {
+    uint32_t lo, hi;  // inclusive, in key space
+    double cover;     // fraction of the key domain
+};
+
+// Superset interval of an address constraint (addr ^ x) & mask == 0 on the
+// big-endian key: the leading-ones run of the mask is a prefix, so the
+// matching set is inside [a & p, (a & p) | ~p].
+KeyRange addr_range(uint32_t addr_le, uint32_t mask_le) {
+    const uint32_t a = bswap32(addr_le), m = bswap32(mask_le);
+    const uint32_t L = lead_ones(m);
+    const uint32_t p = L == 0 ? 0u : (0xFFFFFFFFu << (32 - L));
+    return KeyRange{a & p, (a & p) | ~p, std::ldexp(1.0, -static_cast<int>(L))};
+}
+
+KeyRange port_range(uint32_t mn, uint32_t mx) {
+    return KeyRange{mn, mx, (double(mx) - double(mn) + 1.0) / 65536.0};
+}
+
+// Key ranges of record r in dimension order [dst, src, dport, sport].
+void rec_ranges(const uint32_t *rec, bool v6, KeyRange out[4]) {
+    const uint32_t *m = v6 ? rec + 16 : rec + 4;  // meta, lo, hi
+    if (v6) {
+        out[0] = addr_range(rec[8], rec[12]);
+        out[1] = addr_range(rec[0], rec[4]);
+    } else {
+        out[0] = addr_range(rec[2], rec[3]);
+        out[1] = addr_range(rec[0], rec[1]);
+    }
+    const bool pc = (m[0] & kMetaPortCheck) != 0;
+    const uint32_t lo = pc ? m[1] : 0u, hi = pc ? m[2] : 0xFFFFFFFFu;
+    out[2] = port_range(lo >> 16, hi >> 16);
+    out[3] = port_range(lo & 0xFFFFu, hi & 0xFFFFu);
+}
+
+struct DimBuild {
+    uint32_t kind = 0;
+    uint32_t key_bits = 32;
+    std::vector<uint32_t> rules;  // record indices, ascending
+    std::vector<KeyRange> ranges; // parallel to rules
+    // built
+    std::vector<uint32_t> bounds, lists, cands, radix;
+    uint32_t shift = 0, max_list = 0;
+    std::vector<uint64_t> span;   // per rule: elementary intervals covered
+};
+
+uint64_t build_dim(DimBuild &d) {
+    d.bounds.clear();
+    d.bounds.push_back(0);
+    const uint64_t key_max = (d.key_bits == 32) ? 0xFFFFFFFFull : 0xFFFFull;
+    for (const KeyRange &r : d.ranges) {
+        d.bounds.push_back(r.lo);
+        if (uint64_t(r.hi) < key_max) d.bounds.push_back(r.hi + 1);
+    }
+    std::sort(d.bounds.begin(), d.bounds.end());
+    d.bounds.erase(std::unique(d.bounds.begin(), d.bounds.end()), d.bounds.end());
+    const size_t m = d.bounds.size();
+    // per rule: covered interval range [ja, jb]
+    std::vector<uint32_t> ja(d.rules.size()), jb(d.rules.size());
+    std::vector<uint64_t> count(m + 1, 0);
+    d.span.assign(d.rules.size(), 0);
+    uint64_t total = 0;
+    for (size_t i = 0; i < d.rules.size(); ++i) {
+        ja[i] = static_cast<uint32_t>(std::lower_bound(d.bounds.begin(), d.bounds.end(), d.ranges[i].lo) - d.bounds.begin());
+        jb[i] = static_cast<uint32_t>(std::upper_bound(d.bounds.begin(), d.bounds.end(), d.ranges[i].hi) - d.bounds.begin()) - 1;
+        count[ja[i]] += 1;
+        count[jb[i] + 1] -= 1;  // difference array (mod 2^64 wrap is fine)
+        d.span[i] = uint64_t(jb[i]) - ja[i] + 1;
+        total += d.span[i];
+    }
+    return total;
+}
+
+void finish_dim(DimBuild &d) {
+    const size_t m = d.bounds.size();
+    std::vector<uint32_t> len(m, 0);
+    for (size_t i = 0; i < d.rules.size(); ++i) {
+        const uint32_t a = static_cast<uint32_t>(std::lower_bound(d.bounds.begin(), d.bounds.end(), d.ranges[i].lo) - d.bounds.begin());
+        const uint32_t b = static_cast<uint32_t>(std::upper_bound(d.bounds.begin(), d.bounds.end(), d.ranges[i].hi) - d.bounds.begin()) - 1;
+        for (uint32_t j = a; j <= b; ++j) ++len[j];
+    }
+    d.lists.assign(m + 1, 0);
+    d.max_list = 0;
+    for (size_t j = 0; j < m; ++j) {
+        d.lists[j + 1] = d.lists[j] + len[j];
+        d.max_list = std::max(d.max_list, len[j]);
+    }
+    d.cands.assign(d.lists[m], 0);
+    std::vector<uint32_t> fill(d.lists.begin(), d.lists.end() - 1);
+    for (size_t i = 0; i < d.rules.size(); ++i) {  // ascending rule order -> sorted lists
+        const uint32_t a = static_cast<uint32_t>(std::lower_bound(d.bounds.begin(), d.bounds.end(), d.ranges[i].lo) - d.bounds.begin());
+        const uint32_t b = static_cast<uint32_t>(std::upper_bound(d.bounds.begin(), d.bounds.end(), d.ranges[i].hi) - d.bounds.begin()) - 1;
+        for (uint32_t j = a; j <= b; ++j) d.cands[fill[j]++] = d.rules[i];
+    }
+    // radix directory over the top RB key bits: answer for key k lies in
+    // [radix[k >> shift], radix[(k >> shift) + 1]]
+    uint32_t rb = 1;
+    while (rb < 14 && (size_t(1) << (rb + 1)) <= m) ++rb;
+    rb = std::min(rb, d.key_bits);
+    d.shift = d.key_bits - rb;
+    const size_t nb = size_t(1) << rb;
+    d.radix.assign(nb + 1, 0);
+    for (size_t t = 0; t < nb; ++t) {
+        const uint64_t start = uint64_t(t) << d.shift;
+        d.radix[t] = static_cast<uint32_t>(std::upper_bound(d.bounds.begin(), d.bounds.end(), start) - d.bounds.begin()) - 1;
+    }
+    d.radix[nb] = static_cast<uint32_t>(m - 1);
+}
+
+// Assign the live records of one family to key dimensions and build them.
+void build_family(const std::vector<uint32_t> &recs, uint32_t rw, bool v6, uint32_t n,
+                  std::vector<uint32_t> &blob, FamilyIndex &fi) {
+    static const uint32_t kinds4[4] = {kKeyDst4, kKeySrc4, kKeyDport, kKeySport};
+    static const uint32_t kinds6[4] = {kKeyDst6, kKeySrc6, kKeyDport, kKeySport};
+    DimBuild dims[4];
+    std::vector<uint32_t> resid;
+    std::vector<std::array<KeyRange, 4>> rr(n);
+    std::vector<uint32_t> order_dims(n * 4);
+    for (int k = 0; k < 4; ++k) {
+        dims[k].kind = v6 ? kinds6[k] : kinds4[k];
+        dims[k].key_bits = k < 2 ? 32 : 16;
+    }
+    // preference order per rule: dimensions by increasing coverage
+    std::vector<int> choice(n, -1);
+    std::vector<std::array<int, 4>> pref(n);
+    for (uint32_t r = 0; r < n; ++r) {
+        KeyRange kr[4];
+        rec_ranges(recs.data() + size_t(r) * rw, v6, kr);
+        for (int k = 0; k < 4; ++k) rr[r][k] = kr[k];
+        std::array<int, 4> o = {0, 1, 2, 3};
+        std::stable_sort(o.begin(), o.end(), [&](int a, int b) { return kr[a].cover < kr[b].cover; });
+        pref[r] = o;
+        choice[r] = kr[o[0]].cover < 1.0 ? o[0] : -1;
+    }
+    // Bound replication: a dimension may hold at most budget candidate entries;
+    // past it, the widest rules move to their next-best dimension (or the
+    // residual scan).
+    std::vector<int> rank(n, 0);
+    for (int round = 0; round < 8; ++round) {
+        for (int k = 0; k < 4; ++k) {
+            dims[k].rules.clear();
+            dims[k].ranges.clear();
+        }
+        for (uint32_t r = 0; r < n; ++r)
+            if (choice[r] >= 0) {
+                dims[choice[r]].rules.push_back(r);
+                dims[choice[r]].ranges.push_back(rr[r][choice[r]]);
+            }
+        bool moved = false;
+        for (int k = 0; k < 4; ++k) {
+            DimBuild &d = dims[k];
+            if (d.rules.empty()) continue;
+            const uint64_t total = build_dim(d);
+            const uint64_t budget = 16ull * d.rules.size() + 65536ull;
+            if (total <= budget) continue;
+            // move the widest rules out until the rest fits
+            std::vector<size_t> idx(d.rules.size());
+            for (size_t i = 0; i < idx.size(); ++i) idx[i] = i;
+            std::sort(idx.begin(), idx.end(), [&](size_t a, size_t b) { return d.span[a] > d.span[b]; });
+            uint64_t t = total;
+            for (size_t q = 0; q < idx.size() && t > budget; ++q) {
+                const uint32_t r = d.rules[idx[q]];
+                t -= d.span[idx[q]];
+                int next = -1;
+                while (++rank[r] < 4) {
+                    const int cand = pref[r][rank[r]];
+                    if (rr[r][cand].cover < 1.0) { next = cand; break; }
+                }
+                choice[r] = next;
+                moved = true;
+            }
+        }
+        if (!moved) break;
+    }
+    for (uint32_t r = 0; r < n; ++r)
+        if (choice[r] < 0) resid.push_back(r);
+    // emit: dims with rules (fixed order), then residual
+    fi.n_dims = 0;
+    for (int k = 0; k < 4; ++k) {
+        DimBuild &d = dims[k];
+        if (d.rules.empty()) continue;
+        finish_dim(d);
+        DimInfo &di = fi.dims[fi.n_dims++];
+        di.kind = d.kind;
+        di.shift = d.shift;
+        di.n_bounds = static_cast<uint32_t>(d.bounds.size());
+        di.n_rules = static_cast<uint32_t>(d.rules.size());
+        di.n_cands = d.cands.size();
+        di.max_list = d.max_list;
+        di.off_radix = static_cast<uint32_t>(blob.size());
+        blob.insert(blob.end(), d.radix.begin(), d.radix.end());
+        di.off_bounds = static_cast<uint32_t>(blob.size());
+        blob.insert(blob.end(), d.bounds.begin(), d.bounds.end());
+        di.off_lists = static_cast<uint32_t>(blob.size());
+        blob.insert(blob.end(), d.lists.begin(), d.lists.end());
+        di.off_cands = static_cast<uint32_t>(blob.size());
+        blob.insert(blob.end(), d.cands.begin(), d.cands.end());
+    }
+    fi.off_resid = static_cast<uint32_t>(blob.size());
+    fi.n_resid = static_cast<uint32_t>(resid.size());
+    blob.insert(blob.end(), resid.begin(), resid.end());
+    while (blob.size() % 4) blob.push_back(0);  // keep 16-byte alignment
+}
+
+}  // namespace
+
 bool compile_table(const nffacl_rules &rules, int algo, CompiledTable &out, std::string &err) {
     if (algo != NFFACL_ALGO_AUTO && algo != NFFACL_ALGO_LINEAR && algo != NFFACL_ALGO_INDEXED) {
         err = "unknown algorithm";
@@ -74,10 +293,15 @@ bool compile_table(const nffacl_rules &rules, int algo, CompiledTable &out, std:
         if (emit_rec6(r, rec6)) ++out.n6;
     out.off_rec4 = 0;
     out.off_rec6 = static_cast<uint32_t>(rec4.size());
-    out.blob = std::move(rec4);
+    out.blob = rec4;
     out.blob.insert(out.blob.end(), rec6.begin(), rec6.end());
-    out.algo = NFFACL_ALGO_LINEAR;
+    out.algo = (algo == NFFACL_ALGO_LINEAR) ? NFFACL_ALGO_LINEAR : NFFACL_ALGO_INDEXED;
+    if (out.algo == NFFACL_ALGO_INDEXED) {
+        build_family(rec4, kRec4Dwords, false, out.n4, out.blob, out.idx4);
+        build_family(rec6, kRec6Dwords, true, out.n6, out.blob, out.idx6);
+    }
     if (out.blob.empty()) out.blob.push_back(0);  // keep a valid allocation
+    while (out.blob.size() % 4) out.blob.push_back(0);
     return true;
 }
 

@@ -11,6 +11,24 @@
 
 namespace nffacl {
 
+// One key dimension of the indexed table (see table.hpp).
+struct DimInfo {
+    uint32_t kind = 0;       // KeyKind
+    uint32_t shift = 0;      // key >> shift = radix bucket
+    uint32_t n_bounds = 0;   // elementary intervals
+    uint32_t off_radix = 0, off_bounds = 0, off_lists = 0, off_cands = 0;  // dwords into blob
+    uint32_t n_rules = 0;    // rules assigned to this dimension
+    uint64_t n_cands = 0;    // total candidate entries (with replication)
+    uint32_t max_list = 0;   // longest candidate list
+};
+
+// Indexed view of one address family.
+struct FamilyIndex {
+    uint32_t n_dims = 0;
+    DimInfo dims[4];
+    uint32_t off_resid = 0, n_resid = 0;  // residual record indices (scanned linearly)
+};
+
 struct CompiledTable {
     int algo = NFFACL_ALGO_LINEAR;
     // One contiguous blob of dwords, uploaded as is.
@@ -18,15 +36,8 @@ struct CompiledTable {
     // Linear records (dword offsets into blob) and live record counts.
     uint32_t off_rec4 = 0, n4 = 0;
     uint32_t off_rec6 = 0, n6 = 0;
-    // Indexed: per family, dimension headers (dword offsets into blob),
-    // plus the residual list (records not covered by any dimension).
-    uint32_t n_dims4 = 0, off_dims4 = 0;
-    uint32_t n_dims6 = 0, off_dims6 = 0;
-    uint32_t off_resid4 = 0, n_resid4 = 0;
-    uint32_t off_resid6 = 0, n_resid6 = 0;
-    // Stats for reporting.
-    uint64_t max_list4 = 0, max_list6 = 0;
-    double mean_list4 = 0.0, mean_list6 = 0.0;
+    // Indexed: per family key dimensions + residual list.
+    FamilyIndex idx4, idx6;
 };
 
 // Compile `rules`.  algo: NFFACL_ALGO_LINEAR, NFFACL_ALGO_INDEXED or AUTO.

@@ -259,6 +259,181 @@ k_linear_frames(const uint8_t *__restrict__ frames, const uint64_t *__restrict__
     }
 }
 
+// ---------------------------------------------------------------------------
+// INDEXED: per-lane interval search + ordered candidate lists (table.hpp).
+// ---------------------------------------------------------------------------
+
+struct DimArgs {
+    uint32_t kind, shift, off_radix, off_bounds, off_lists, off_cands;
+};
+struct FamArgs {
+    uint32_t n_dims, off_rec, n_resid, off_resid;
+    DimArgs dim[4];
+};
+struct IndexedArgs {
+    const uint32_t *tab;  // device table (global memory)
+    uint32_t tab_dwords;  // multiple of 4
+    FamArgs f4, f6;
+};
+
+extern __shared__ __attribute__((aligned(16))) uint32_t lds_tab[];
+
+// Table accessors: the whole table staged in LDS, or read through L1/L2.
+struct LdsTab {
+    __device__ __forceinline__ uint32_t ld(uint32_t i) const { return lds_tab[i]; }
+    __device__ __forceinline__ u32x4 ld4(uint32_t i) const {
+        return *reinterpret_cast<const u32x4 *>(&lds_tab[i]);
+    }
+};
+struct GlobalTab {
+    const uint32_t *__restrict__ p;
+    __device__ __forceinline__ uint32_t ld(uint32_t i) const { return p[i]; }
+    __device__ __forceinline__ u32x4 ld4(uint32_t i) const {
+        return *reinterpret_cast<const u32x4 *>(p + i);
+    }
+};
+
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+
+// Full rule test of record r (acl.go:525-541 / 545-559 for one rule).
+template <bool V6, class T>
+__device__ __forceinline__ bool rule_matches(const T &tab, uint32_t off_rec, uint32_t r,
+                                             const Fields &f, uint32_t &out) {
+    if (!V6) {
+        const uint32_t b0 = off_rec + r * kRec4Dwords;
+        const u32x4 a = tab.ld4(b0), b = tab.ld4(b0 + 4);
+        const uint32_t m = ((f.s[0] ^ a.x) & a.y) | ((f.t[0] ^ a.z) & a.w) |
+                           ((f.proto ^ b.x) & ((b.x >> 8) & 0xFFu)) | port_miss(f.ports, b.y, b.z);
+        out = b.w;
+        return m == 0u;
+    } else {
+        const uint32_t b0 = off_rec + r * kRec6Dwords;
+        const u32x4 sa = tab.ld4(b0), sm = tab.ld4(b0 + 4), da = tab.ld4(b0 + 8), dm = tab.ld4(b0 + 12),
+                    b = tab.ld4(b0 + 16);
+        const uint32_t m = ((f.s[0] ^ sa.x) & sm.x) | ((f.s[1] ^ sa.y) & sm.y) | ((f.s[2] ^ sa.z) & sm.z) |
+                           ((f.s[3] ^ sa.w) & sm.w) | ((f.t[0] ^ da.x) & dm.x) | ((f.t[1] ^ da.y) & dm.y) |
+                           ((f.t[2] ^ da.z) & dm.z) | ((f.t[3] ^ da.w) & dm.w) |
+                           ((f.proto ^ b.x) & ((b.x >> 8) & 0xFFu)) | port_miss(f.ports, b.y, b.z);
+        out = b.w;
+        return m == 0u;
+    }
+}
+
+__device__ __forceinline__ uint32_t dim_key(uint32_t kind, const Fields &f) {
+    switch (kind) {
+    case kKeyDst4: case kKeyDst6: return __builtin_bswap32(f.t[0]);
+    case kKeySrc4: case kKeySrc6: return __builtin_bswap32(f.s[0]);
+    case kKeyDport: return f.ports >> 16;
+    default: return f.ports & 0xFFFFu;
+    }
+}
+
+// First match of one family for the lanes with `mine` set; best/out carry
+// the running minimum record index and its OutputNumber.
+template <bool V6, class T>
+__device__ __forceinline__ void classify_family(const T &tab, const FamArgs &fa, const Fields &f,
+                                                bool mine, uint32_t &best, uint32_t &out) {
+    if (mine) {
+        for (uint32_t d = 0; d < fa.n_dims; ++d) {
+            const DimArgs &da = fa.dim[d];
+            const uint32_t key = dim_key(da.kind, f);
+            const uint32_t t = key >> da.shift;
+            uint32_t lo = tab.ld(da.off_radix + t), hi = tab.ld(da.off_radix + t + 1);
+            while (lo < hi) {  // last interval start <= key
+                const uint32_t mid = (lo + hi + 1) >> 1;
+                if (tab.ld(da.off_bounds + mid) <= key) lo = mid; else hi = mid - 1;
+            }
+            uint32_t c = tab.ld(da.off_lists + lo);
+            const uint32_t e = tab.ld(da.off_lists + lo + 1);
+            for (; c < e; ++c) {
+                const uint32_t r = tab.ld(da.off_cands + c);
+                if (r >= best) break;  // lists ascend: nothing earlier left here
+                uint32_t o;
+                if (rule_matches<V6>(tab, fa.off_rec, r, f, o)) {
+                    best = r;
+                    out = o;
+                    break;
+                }
+            }
+        }
+    }
+    // rules with no selective key: wave-uniform scan in rule order
+    for (uint32_t i = 0; i < fa.n_resid; ++i) {
+        const uint32_t r = tab.ld(fa.off_resid + i);
+        const bool want = mine && r < best;
+        if (!ballot(want)) break;  // residual list ascends too
+        if (want) {
+            uint32_t o;
+            if (rule_matches<V6>(tab, fa.off_rec, r, f, o)) {
+                best = r;
+                out = o;
+            }
+        }
+    }
+}
+
+template <class T>
+__device__ __forceinline__ uint32_t classify_indexed(const T &tab, const IndexedArgs &a, const Fields &f) {
+    uint32_t best = kNone, out = 0;
+    if (ballot(f.is4)) classify_family<false>(tab, a.f4, f, f.is4, best, out);
+    if (ballot(f.is6)) classify_family<true>(tab, a.f6, f, f.is6, best, out);
+    return best != kNone ? out : 0u;
+}
+
+__device__ __forceinline__ void stage_table(const IndexedArgs &a) {
+    const u32x4 *src = reinterpret_cast<const u32x4 *>(a.tab);
+    u32x4 *dst = reinterpret_cast<u32x4 *>(lds_tab);
+    for (uint32_t i = threadIdx.x; i < a.tab_dwords / 4; i += blockDim.x) dst[i] = src[i];
+    __syncthreads();
+}
+
+template <bool LDS>
+__global__ void __launch_bounds__(1024)
+k_indexed_slots(const uint8_t *__restrict__ slots, uint32_t stride, uint64_t n, IndexedArgs a,
+                uint32_t *__restrict__ port_out, uint64_t *__restrict__ permit_out) {
+    if (LDS) stage_table(a);
+    NFFACL_WAVE_LOOP(n) {
+        const uint64_t idx = base + lane;
+        const bool live = idx < n;
+        const uint8_t *pkt = slots + (live ? idx : 0) * stride;
+        uint32_t d[16];
+        load16(pkt, d);
+        Fields f;
+        parse_fields(d, live, f, [&](uint32_t k, uint32_t &lo, uint32_t &hi) {
+            far_dwords(pkt, stride, k, lo, hi);
+        });
+        uint32_t res;
+        if (LDS) res = classify_indexed(LdsTab{}, a, f);
+        else res = classify_indexed(GlobalTab{a.tab}, a, f);
+        store_verdicts(base, lane, live, res, port_out, permit_out);
+    }
+}
+
+template <bool LDS>
+__global__ void __launch_bounds__(1024)
+k_indexed_frames(const uint8_t *__restrict__ frames, const uint64_t *__restrict__ desc, uint64_t n,
+                 IndexedArgs a, uint32_t *__restrict__ port_out, uint64_t *__restrict__ permit_out) {
+    if (LDS) stage_table(a);
+    NFFACL_WAVE_LOOP(n) {
+        const uint64_t idx = base + lane;
+        const bool live = idx < n;
+        const uint64_t ds = live ? desc[idx] : 0;
+        const uint32_t len = static_cast<uint32_t>(ds & 0xFFFFu);
+        const uint8_t *pkt = frames + (ds >> 16);
+        uint32_t d[16];
+        load16(pkt, d);
+        clip16(d, len);
+        Fields f;
+        parse_fields(d, live, f, [&](uint32_t k, uint32_t &lo, uint32_t &hi) {
+            far_dwords(pkt, len, k, lo, hi);
+        });
+        uint32_t res;
+        if (LDS) res = classify_indexed(LdsTab{}, a, f);
+        else res = classify_indexed(GlobalTab{a.tab}, a, f);
+        store_verdicts(base, lane, live, res, port_out, permit_out);
+    }
+}
+
 }  // namespace dev
 
 // ---------------------------------------------------------------------------
@@ -312,15 +487,81 @@ static uint32_t grid_for(const nffacl_engine *eng, uint64_t n, uint32_t block, u
     return static_cast<uint32_t>(std::max<uint64_t>(1, std::min(blocks_needed, cap)));
 }
 
+static dev::IndexedArgs indexed_args(const DevTable *t) {
+    dev::IndexedArgs a{};
+    a.tab = t->d_blob;
+    a.tab_dwords = static_cast<uint32_t>(t->meta.blob.size());
+    auto fam = [&](const FamilyIndex &fi, uint32_t off_rec, dev::FamArgs &fa) {
+        fa.n_dims = fi.n_dims;
+        fa.off_rec = off_rec;
+        fa.n_resid = fi.n_resid;
+        fa.off_resid = fi.off_resid;
+        for (uint32_t k = 0; k < 4; ++k) {
+            const DimInfo &d = fi.dims[k];
+            fa.dim[k] = dev::DimArgs{d.kind, d.shift, d.off_radix, d.off_bounds, d.off_lists, d.off_cands};
+        }
+    };
+    fam(t->meta.idx4, t->meta.off_rec4, a.f4);
+    fam(t->meta.idx6, t->meta.off_rec6, a.f6);
+    return a;
+}
+
+// LDS budget per workgroup for a staged table (gfx950: 160 KiB per CU).
+constexpr size_t kLdsBytes = 160 * 1024;
+
+struct IndexedLaunch {
+    bool lds;
+    uint32_t block, per_cu;
+    size_t lds_bytes;
+};
+
+static IndexedLaunch indexed_launch(const DevTable *t) {
+    const size_t bytes = t->meta.blob.size() * sizeof(uint32_t);
+    if (bytes <= kLdsBytes - 1024) {
+        const uint32_t per_cu = static_cast<uint32_t>(std::min<size_t>(2, kLdsBytes / bytes));
+        return IndexedLaunch{true, per_cu >= 2 ? 1024u : 1024u, per_cu, bytes};
+    }
+    return IndexedLaunch{false, 256u, 8u, 0};
+}
+
+int prepare_kernels() {
+    static std::once_flag once;
+    static hipError_t err = hipSuccess;
+    std::call_once(once, [] {
+        err = hipFuncSetAttribute(reinterpret_cast<const void *>(dev::k_indexed_slots<true>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kLdsBytes));
+        if (err == hipSuccess)
+            err = hipFuncSetAttribute(reinterpret_cast<const void *>(dev::k_indexed_frames<true>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kLdsBytes));
+    });
+    if (err != hipSuccess) {
+        set_last_error(std::string("hipFuncSetAttribute(LDS): ") + hipGetErrorString(err));
+        return NFFACL_ERR_HIP;
+    }
+    return NFFACL_OK;
+}
+
 int launch_slots(nffacl_engine *eng, const DevTable *t, const uint8_t *d_slots, uint32_t stride,
                  uint64_t n, uint32_t *d_port, uint64_t *d_permit, hipStream_t stream) {
     if (n == 0) return NFFACL_OK;
-    const uint32_t block = 256;
-    dev::LinearArgs a{t->d_blob + t->meta.off_rec4, t->meta.n4, t->d_blob + t->meta.off_rec6,
-                      t->meta.n6};
-    const uint32_t grid = grid_for(eng, n, block, 8);
-    hipLaunchKernelGGL(dev::k_linear_slots, dim3(grid), dim3(block), 0, stream, d_slots, stride,
-                       n, a, d_port, d_permit);
+    if (t->meta.algo == NFFACL_ALGO_INDEXED) {
+        const dev::IndexedArgs a = indexed_args(t);
+        const IndexedLaunch L = indexed_launch(t);
+        const uint32_t grid = grid_for(eng, n, L.block, L.per_cu);
+        if (L.lds)
+            hipLaunchKernelGGL(dev::k_indexed_slots<true>, dim3(grid), dim3(L.block), L.lds_bytes, stream,
+                               d_slots, stride, n, a, d_port, d_permit);
+        else
+            hipLaunchKernelGGL(dev::k_indexed_slots<false>, dim3(grid), dim3(L.block), 0, stream, d_slots,
+                               stride, n, a, d_port, d_permit);
+    } else {
+        const uint32_t block = 256;
+        dev::LinearArgs a{t->d_blob + t->meta.off_rec4, t->meta.n4, t->d_blob + t->meta.off_rec6,
+                          t->meta.n6};
+        const uint32_t grid = grid_for(eng, n, block, 8);
+        hipLaunchKernelGGL(dev::k_linear_slots, dim3(grid), dim3(block), 0, stream, d_slots, stride,
+                           n, a, d_port, d_permit);
+    }
     HIP_TRY(hipGetLastError());
     return NFFACL_OK;
 }
@@ -329,12 +570,24 @@ int launch_frames(nffacl_engine *eng, const DevTable *t, const uint8_t *d_frames
                   const uint64_t *d_desc, uint64_t n, uint32_t *d_port, uint64_t *d_permit,
                   hipStream_t stream) {
     if (n == 0) return NFFACL_OK;
-    const uint32_t block = 256;
-    dev::LinearArgs a{t->d_blob + t->meta.off_rec4, t->meta.n4, t->d_blob + t->meta.off_rec6,
-                      t->meta.n6};
-    const uint32_t grid = grid_for(eng, n, block, 8);
-    hipLaunchKernelGGL(dev::k_linear_frames, dim3(grid), dim3(block), 0, stream, d_frames, d_desc,
-                       n, a, d_port, d_permit);
+    if (t->meta.algo == NFFACL_ALGO_INDEXED) {
+        const dev::IndexedArgs a = indexed_args(t);
+        const IndexedLaunch L = indexed_launch(t);
+        const uint32_t grid = grid_for(eng, n, L.block, L.per_cu);
+        if (L.lds)
+            hipLaunchKernelGGL(dev::k_indexed_frames<true>, dim3(grid), dim3(L.block), L.lds_bytes, stream,
+                               d_frames, d_desc, n, a, d_port, d_permit);
+        else
+            hipLaunchKernelGGL(dev::k_indexed_frames<false>, dim3(grid), dim3(L.block), 0, stream,
+                               d_frames, d_desc, n, a, d_port, d_permit);
+    } else {
+        const uint32_t block = 256;
+        dev::LinearArgs a{t->d_blob + t->meta.off_rec4, t->meta.n4, t->d_blob + t->meta.off_rec6,
+                          t->meta.n6};
+        const uint32_t grid = grid_for(eng, n, block, 8);
+        hipLaunchKernelGGL(dev::k_linear_frames, dim3(grid), dim3(block), 0, stream, d_frames, d_desc,
+                           n, a, d_port, d_permit);
+    }
     HIP_TRY(hipGetLastError());
     return NFFACL_OK;
 }

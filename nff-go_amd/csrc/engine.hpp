@@ -49,6 +49,7 @@ struct nffacl_engine {
 };
 
 namespace nffacl {
+int prepare_kernels();
 int launch_slots(nffacl_engine *eng, const DevTable *t, const uint8_t *d_slots, uint32_t stride,
                  uint64_t n, uint32_t *d_port, uint64_t *d_permit, hipStream_t stream);
 int launch_frames(nffacl_engine *eng, const DevTable *t, const uint8_t *d_frames,

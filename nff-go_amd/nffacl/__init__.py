@@ -27,6 +27,16 @@ if not LIB_PATH.exists():
         f"libnffacl.so not found at {LIB_PATH}; build it with `make -C nff-go_amd` "
         "(or __graft_entry__.build()).  There is no CPU fallback.")
 
+# PyTorch-ROCm ships its own libamdhip64 / libhsa-runtime64 (same SONAME
+# libamdhip64.so.7 as /opt/rocm's).  If libnffacl were loaded first, torch
+# would later bring in a second HIP/HSA runtime and the two fight over the
+# device ("no HIP device").  Loading torch first makes libnffacl bind to the
+# runtime already in the process, so device pointers and streams are shared.
+try:  # pragma: no cover - import side effect only
+    import torch as _torch  # noqa: F401
+except ImportError:
+    _torch = None
+
 _lib = ctypes.CDLL(str(LIB_PATH))
 
 # ---- status codes (include/nffacl.h) -----------------------------------------
@@ -139,8 +149,11 @@ class L3Rules:
 
     def __del__(self):
         h, self._h = getattr(self, "_h", None), None
-        if h:
-            _rules_free(h)
+        if h and _rules_free is not None:
+            try:
+                _rules_free(h)
+            except Exception:  # interpreter teardown
+                pass
 
     @property
     def handle(self):
@@ -234,8 +247,11 @@ class Engine:
 
     def close(self):
         h, self._h = getattr(self, "_h", None), None
-        if h:
-            _engine_destroy(h)
+        if h and _engine_destroy is not None:
+            try:
+                _engine_destroy(h)
+            except Exception:  # interpreter teardown
+                pass
 
     def __del__(self):
         self.close()
