@@ -172,13 +172,14 @@ NFFACL_API int nffacl_engine_table_bytes(const nffacl_engine *eng, uint64_t *byt
  * least that many dwords. */
 typedef struct nffacl_dim_info {
     uint32_t kind;       /* key: 0 src4, 1 dst4, 2 src6 (top 32 bits), 3 dst6, 4 sport, 5 dport */
-    uint32_t shift;      /* radix bucket = key >> shift */
-    uint32_t n_bounds;   /* elementary intervals */
-    uint32_t off_radix, off_bounds, off_lists, off_cands; /* dword offsets into the blob */
+    uint32_t shift;      /* bucket = key >> shift */
+    uint32_t n_buckets;  /* radix buckets */
+    uint32_t off_dir;    /* dword offset of dir[n_buckets + 1] (bucket list bounds) */
+    uint32_t off_cands;  /* dword offset of the bucket lists (record indices, ascending per bucket) */
     uint32_t n_rules;    /* rules indexed by this key */
-    uint64_t n_cands;    /* candidate-list entries (with replication) */
-    uint32_t max_list;   /* longest candidate list */
+    uint32_t max_list;   /* longest bucket list */
     uint32_t reserved;
+    uint64_t n_cands;    /* bucket-list entries (with replication) */
 } nffacl_dim_info;
 
 typedef struct nffacl_family_info {

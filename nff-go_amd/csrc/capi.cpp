@@ -208,8 +208,8 @@ int nffacl_table_compile(const nffacl_rules *rules, int algo, uint32_t *blob, ui
         o.n_resid = fi[f]->n_resid;
         for (int k = 0; k < 4; ++k) {
             const DimInfo &d = fi[f]->dims[k];
-            o.dims[k] = nffacl_dim_info{d.kind, d.shift, d.n_bounds, d.off_radix, d.off_bounds, d.off_lists,
-                                        d.off_cands, d.n_rules, d.n_cands, d.max_list, 0};
+            o.dims[k] = nffacl_dim_info{d.kind, d.shift, d.n_buckets, d.off_dir, d.off_cands, d.n_rules,
+                                        d.max_list, 0, d.n_cands};
         }
     }
     if (blob) {

@@ -113,72 +113,59 @@ struct DimBuild {
     std::vector<uint32_t> rules;  // record indices, ascending
     std::vector<KeyRange> ranges; // parallel to rules
     // built
-    std::vector<uint32_t> bounds, lists, cands, radix;
-    uint32_t shift = 0, max_list = 0;
-    std::vector<uint64_t> span;   // per rule: elementary intervals covered
+    uint32_t rb = 0, shift = 0, max_list = 0;
+    std::vector<uint32_t> dir, cands;
+    std::vector<uint64_t> span;   // per rule: buckets covered
 };
 
-uint64_t build_dim(DimBuild &d) {
-    d.bounds.clear();
-    d.bounds.push_back(0);
-    const uint64_t key_max = (d.key_bits == 32) ? 0xFFFFFFFFull : 0xFFFFull;
-    for (const KeyRange &r : d.ranges) {
-        d.bounds.push_back(r.lo);
-        if (uint64_t(r.hi) < key_max) d.bounds.push_back(r.hi + 1);
-    }
-    std::sort(d.bounds.begin(), d.bounds.end());
-    d.bounds.erase(std::unique(d.bounds.begin(), d.bounds.end()), d.bounds.end());
-    const size_t m = d.bounds.size();
-    // per rule: covered interval range [ja, jb]
-    std::vector<uint32_t> ja(d.rules.size()), jb(d.rules.size());
-    std::vector<uint64_t> count(m + 1, 0);
-    d.span.assign(d.rules.size(), 0);
+// Radix bits for a dimension holding n rules: about 4 buckets per rule,
+// at most 2^20 buckets (addresses) / 2^16 (ports, i.e. one bucket per port).
+uint32_t pick_rb(size_t n, uint32_t key_bits) {
+    uint32_t rb = 4;
+    while (rb < 20 && (size_t(1) << rb) < 4 * n) ++rb;
+    return std::min(rb, key_bits);
+}
+
+uint64_t budget_for(size_t n) { return 8ull * n + 65536ull; }
+
+// Pick the radix width and count the replicated entries of the dimension's
+// bucket lists: start at ~4 buckets per rule and narrow the radix while wide
+// rules would replicate past the budget.
+uint64_t span_dim(DimBuild &d) {
     uint64_t total = 0;
-    for (size_t i = 0; i < d.rules.size(); ++i) {
-        ja[i] = static_cast<uint32_t>(std::lower_bound(d.bounds.begin(), d.bounds.end(), d.ranges[i].lo) - d.bounds.begin());
-        jb[i] = static_cast<uint32_t>(std::upper_bound(d.bounds.begin(), d.bounds.end(), d.ranges[i].hi) - d.bounds.begin()) - 1;
-        count[ja[i]] += 1;
-        count[jb[i] + 1] -= 1;  // difference array (mod 2^64 wrap is fine)
-        d.span[i] = uint64_t(jb[i]) - ja[i] + 1;
-        total += d.span[i];
+    for (uint32_t rb = pick_rb(d.rules.size(), d.key_bits);; --rb) {
+        d.rb = rb;
+        d.shift = d.key_bits - rb;
+        d.span.assign(d.rules.size(), 0);
+        total = 0;
+        for (size_t i = 0; i < d.rules.size(); ++i) {
+            d.span[i] = uint64_t(d.ranges[i].hi >> d.shift) - (d.ranges[i].lo >> d.shift) + 1;
+            total += d.span[i];
+        }
+        if (total <= budget_for(d.rules.size()) || rb <= 4) break;
     }
     return total;
 }
 
+// Bucket t holds, in ascending rule order, every rule whose key range meets
+// [t << shift, ((t + 1) << shift) - 1]; dir[t] .. dir[t+1] delimit it.
 void finish_dim(DimBuild &d) {
-    const size_t m = d.bounds.size();
-    std::vector<uint32_t> len(m, 0);
-    for (size_t i = 0; i < d.rules.size(); ++i) {
-        const uint32_t a = static_cast<uint32_t>(std::lower_bound(d.bounds.begin(), d.bounds.end(), d.ranges[i].lo) - d.bounds.begin());
-        const uint32_t b = static_cast<uint32_t>(std::upper_bound(d.bounds.begin(), d.bounds.end(), d.ranges[i].hi) - d.bounds.begin()) - 1;
-        for (uint32_t j = a; j <= b; ++j) ++len[j];
-    }
-    d.lists.assign(m + 1, 0);
+    span_dim(d);  // sets rb / shift
+    const size_t nb = size_t(1) << d.rb;
+    std::vector<uint32_t> len(nb + 1, 0);
+    for (const KeyRange &r : d.ranges)
+        for (uint64_t t = r.lo >> d.shift; t <= (r.hi >> d.shift); ++t) ++len[t];
+    d.dir.assign(nb + 1, 0);
     d.max_list = 0;
-    for (size_t j = 0; j < m; ++j) {
-        d.lists[j + 1] = d.lists[j] + len[j];
-        d.max_list = std::max(d.max_list, len[j]);
-    }
-    d.cands.assign(d.lists[m], 0);
-    std::vector<uint32_t> fill(d.lists.begin(), d.lists.end() - 1);
-    for (size_t i = 0; i < d.rules.size(); ++i) {  // ascending rule order -> sorted lists
-        const uint32_t a = static_cast<uint32_t>(std::lower_bound(d.bounds.begin(), d.bounds.end(), d.ranges[i].lo) - d.bounds.begin());
-        const uint32_t b = static_cast<uint32_t>(std::upper_bound(d.bounds.begin(), d.bounds.end(), d.ranges[i].hi) - d.bounds.begin()) - 1;
-        for (uint32_t j = a; j <= b; ++j) d.cands[fill[j]++] = d.rules[i];
-    }
-    // radix directory over the top RB key bits: answer for key k lies in
-    // [radix[k >> shift], radix[(k >> shift) + 1]]
-    uint32_t rb = 1;
-    while (rb < 14 && (size_t(1) << (rb + 1)) <= m) ++rb;
-    rb = std::min(rb, d.key_bits);
-    d.shift = d.key_bits - rb;
-    const size_t nb = size_t(1) << rb;
-    d.radix.assign(nb + 1, 0);
     for (size_t t = 0; t < nb; ++t) {
-        const uint64_t start = uint64_t(t) << d.shift;
-        d.radix[t] = static_cast<uint32_t>(std::upper_bound(d.bounds.begin(), d.bounds.end(), start) - d.bounds.begin()) - 1;
+        d.dir[t + 1] = d.dir[t] + len[t];
+        d.max_list = std::max(d.max_list, len[t]);
     }
-    d.radix[nb] = static_cast<uint32_t>(m - 1);
+    d.cands.assign(d.dir[nb], 0);
+    std::vector<uint32_t> fill(d.dir.begin(), d.dir.end() - 1);
+    for (size_t i = 0; i < d.rules.size(); ++i)  // ascending rule order -> sorted lists
+        for (uint64_t t = d.ranges[i].lo >> d.shift; t <= (d.ranges[i].hi >> d.shift); ++t)
+            d.cands[fill[t]++] = d.rules[i];
 }
 
 // Assign the live records of one family to key dimensions and build them.
@@ -189,7 +176,6 @@ void build_family(const std::vector<uint32_t> &recs, uint32_t rw, bool v6, uint3
     DimBuild dims[4];
     std::vector<uint32_t> resid;
     std::vector<std::array<KeyRange, 4>> rr(n);
-    std::vector<uint32_t> order_dims(n * 4);
     for (int k = 0; k < 4; ++k) {
         dims[k].kind = v6 ? kinds6[k] : kinds4[k];
         dims[k].key_bits = k < 2 ? 32 : 16;
@@ -206,8 +192,8 @@ void build_family(const std::vector<uint32_t> &recs, uint32_t rw, bool v6, uint3
         pref[r] = o;
         choice[r] = kr[o[0]].cover < 1.0 ? o[0] : -1;
     }
-    // Bound replication: a dimension may hold at most budget candidate entries;
-    // past it, the widest rules move to their next-best dimension (or the
+    // Bound replication: a dimension may hold at most `budget` list entries;
+    // past it, the widest rules move to their next-best dimension (or to the
     // residual scan).
     std::vector<int> rank(n, 0);
     for (int round = 0; round < 8; ++round) {
@@ -224,10 +210,9 @@ void build_family(const std::vector<uint32_t> &recs, uint32_t rw, bool v6, uint3
         for (int k = 0; k < 4; ++k) {
             DimBuild &d = dims[k];
             if (d.rules.empty()) continue;
-            const uint64_t total = build_dim(d);
-            const uint64_t budget = 16ull * d.rules.size() + 65536ull;
+            const uint64_t total = span_dim(d);
+            const uint64_t budget = budget_for(d.rules.size());
             if (total <= budget) continue;
-            // move the widest rules out until the rest fits
             std::vector<size_t> idx(d.rules.size());
             for (size_t i = 0; i < idx.size(); ++i) idx[i] = i;
             std::sort(idx.begin(), idx.end(), [&](size_t a, size_t b) { return d.span[a] > d.span[b]; });
@@ -248,7 +233,7 @@ void build_family(const std::vector<uint32_t> &recs, uint32_t rw, bool v6, uint3
     }
     for (uint32_t r = 0; r < n; ++r)
         if (choice[r] < 0) resid.push_back(r);
-    // emit: dims with rules (fixed order), then residual
+    // emit non-empty dimensions (fixed order), then the residual list
     fi.n_dims = 0;
     for (int k = 0; k < 4; ++k) {
         DimBuild &d = dims[k];
@@ -257,18 +242,15 @@ void build_family(const std::vector<uint32_t> &recs, uint32_t rw, bool v6, uint3
         DimInfo &di = fi.dims[fi.n_dims++];
         di.kind = d.kind;
         di.shift = d.shift;
-        di.n_bounds = static_cast<uint32_t>(d.bounds.size());
+        di.n_buckets = 1u << d.rb;
         di.n_rules = static_cast<uint32_t>(d.rules.size());
         di.n_cands = d.cands.size();
         di.max_list = d.max_list;
-        di.off_radix = static_cast<uint32_t>(blob.size());
-        blob.insert(blob.end(), d.radix.begin(), d.radix.end());
-        di.off_bounds = static_cast<uint32_t>(blob.size());
-        blob.insert(blob.end(), d.bounds.begin(), d.bounds.end());
-        di.off_lists = static_cast<uint32_t>(blob.size());
-        blob.insert(blob.end(), d.lists.begin(), d.lists.end());
+        di.off_dir = static_cast<uint32_t>(blob.size());
+        blob.insert(blob.end(), d.dir.begin(), d.dir.end());
         di.off_cands = static_cast<uint32_t>(blob.size());
         blob.insert(blob.end(), d.cands.begin(), d.cands.end());
+        if (d.cands.empty()) blob.push_back(0);  // keep cands[0] addressable
     }
     fi.off_resid = static_cast<uint32_t>(blob.size());
     fi.n_resid = static_cast<uint32_t>(resid.size());

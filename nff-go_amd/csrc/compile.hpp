@@ -14,12 +14,12 @@ namespace nffacl {
 // One key dimension of the indexed table (see table.hpp).
 struct DimInfo {
     uint32_t kind = 0;       // KeyKind
-    uint32_t shift = 0;      // key >> shift = radix bucket
-    uint32_t n_bounds = 0;   // elementary intervals
-    uint32_t off_radix = 0, off_bounds = 0, off_lists = 0, off_cands = 0;  // dwords into blob
+    uint32_t shift = 0;      // bucket = key >> shift
+    uint32_t n_buckets = 0;  // 2^(key bits - shift)
+    uint32_t off_dir = 0, off_cands = 0;  // dword offsets into blob
     uint32_t n_rules = 0;    // rules assigned to this dimension
     uint64_t n_cands = 0;    // total candidate entries (with replication)
-    uint32_t max_list = 0;   // longest candidate list
+    uint32_t max_list = 0;   // longest bucket list
 };
 
 // Indexed view of one address family.

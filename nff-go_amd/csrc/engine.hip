@@ -264,7 +264,7 @@ k_linear_frames(const uint8_t *__restrict__ frames, const uint64_t *__restrict__
 // ---------------------------------------------------------------------------
 
 struct DimArgs {
-    uint32_t kind, shift, off_radix, off_bounds, off_lists, off_cands;
+    uint32_t kind, shift, off_dir, off_cands;
 };
 struct FamArgs {
     uint32_t n_dims, off_rec, n_resid, off_resid;
@@ -329,32 +329,29 @@ __device__ __forceinline__ uint32_t dim_key(uint32_t kind, const Fields &f) {
 }
 
 // First match of one family for the lanes with `mine` set; best/out carry
-// the running minimum record index and its OutputNumber.
+// the running minimum record index and its OutputNumber.  All loops have a
+// wave-uniform trip count (a ballot), their bodies are predicated, so the
+// wave never splits its exec mask.
 template <bool V6, class T>
 __device__ __forceinline__ void classify_family(const T &tab, const FamArgs &fa, const Fields &f,
                                                 bool mine, uint32_t &best, uint32_t &out) {
-    if (mine) {
-        for (uint32_t d = 0; d < fa.n_dims; ++d) {
-            const DimArgs &da = fa.dim[d];
-            const uint32_t key = dim_key(da.kind, f);
-            const uint32_t t = key >> da.shift;
-            uint32_t lo = tab.ld(da.off_radix + t), hi = tab.ld(da.off_radix + t + 1);
-            while (lo < hi) {  // last interval start <= key
-                const uint32_t mid = (lo + hi + 1) >> 1;
-                if (tab.ld(da.off_bounds + mid) <= key) lo = mid; else hi = mid - 1;
-            }
-            uint32_t c = tab.ld(da.off_lists + lo);
-            const uint32_t e = tab.ld(da.off_lists + lo + 1);
-            for (; c < e; ++c) {
-                const uint32_t r = tab.ld(da.off_cands + c);
-                if (r >= best) break;  // lists ascend: nothing earlier left here
-                uint32_t o;
-                if (rule_matches<V6>(tab, fa.off_rec, r, f, o)) {
-                    best = r;
-                    out = o;
-                    break;
-                }
-            }
+    for (uint32_t d = 0; d < fa.n_dims; ++d) {
+        const DimArgs &da = fa.dim[d];
+        const uint32_t t = dim_key(da.kind, f) >> da.shift;
+        uint32_t c = tab.ld(da.off_dir + t);
+        uint32_t e = tab.ld(da.off_dir + t + 1);
+        if (!mine) e = c;
+        while (ballot(c < e)) {
+            const bool act = c < e;
+            const uint32_t r = tab.ld(da.off_cands + (act ? c : 0u));
+            uint32_t o;
+            const bool hit = rule_matches<V6>(tab, fa.off_rec, r, f, o);
+            const bool earlier = act && r < best;
+            const bool take = earlier && hit;
+            best = take ? r : best;
+            out = take ? o : out;
+            // stop at a hit, or once the ascending list has passed `best`
+            c = (earlier && !hit) ? c + 1 : e;
         }
     }
     // rules with no selective key: wave-uniform scan in rule order
@@ -362,13 +359,10 @@ __device__ __forceinline__ void classify_family(const T &tab, const FamArgs &fa,
         const uint32_t r = tab.ld(fa.off_resid + i);
         const bool want = mine && r < best;
         if (!ballot(want)) break;  // residual list ascends too
-        if (want) {
-            uint32_t o;
-            if (rule_matches<V6>(tab, fa.off_rec, r, f, o)) {
-                best = r;
-                out = o;
-            }
-        }
+        uint32_t o;
+        const bool take = want && rule_matches<V6>(tab, fa.off_rec, r, f, o);
+        best = take ? r : best;
+        out = take ? o : out;
     }
 }
 
@@ -387,19 +381,31 @@ __device__ __forceinline__ void stage_table(const IndexedArgs &a) {
     __syncthreads();
 }
 
+// Grid-stride over 64-packet batches with the next batch's packet loads in
+// flight while the current batch is classified (software pipelining).
 template <bool LDS>
 __global__ void __launch_bounds__(1024)
 k_indexed_slots(const uint8_t *__restrict__ slots, uint32_t stride, uint64_t n, IndexedArgs a,
                 uint32_t *__restrict__ port_out, uint64_t *__restrict__ permit_out) {
     if (LDS) stage_table(a);
-    NFFACL_WAVE_LOOP(n) {
+    const uint32_t lane = lane_id();
+    const uint32_t wpb = blockDim.x >> 6;
+    const uint64_t wave0 = uint64_t(blockIdx.x) * wpb + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t step = uint64_t(gridDim.x) * wpb * 64;
+    uint64_t base = wave0 * 64;
+    uint32_t d[16];
+    if (base < n) load16(slots + (base + lane < n ? base + lane : 0) * stride, d);
+    for (; base < n; base += step) {
         const uint64_t idx = base + lane;
         const bool live = idx < n;
         const uint8_t *pkt = slots + (live ? idx : 0) * stride;
-        uint32_t d[16];
-        load16(pkt, d);
+        uint32_t cur[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) cur[k] = d[k];
+        const uint64_t nb = base + step;
+        if (nb < n) load16(slots + (nb + lane < n ? nb + lane : 0) * stride, d);  // prefetch
         Fields f;
-        parse_fields(d, live, f, [&](uint32_t k, uint32_t &lo, uint32_t &hi) {
+        parse_fields(cur, live, f, [&](uint32_t k, uint32_t &lo, uint32_t &hi) {
             far_dwords(pkt, stride, k, lo, hi);
         });
         uint32_t res;
@@ -498,7 +504,7 @@ static dev::IndexedArgs indexed_args(const DevTable *t) {
         fa.off_resid = fi.off_resid;
         for (uint32_t k = 0; k < 4; ++k) {
             const DimInfo &d = fi.dims[k];
-            fa.dim[k] = dev::DimArgs{d.kind, d.shift, d.off_radix, d.off_bounds, d.off_lists, d.off_cands};
+            fa.dim[k] = dev::DimArgs{d.kind, d.shift, d.off_dir, d.off_cands};
         }
     };
     fam(t->meta.idx4, t->meta.off_rec4, a.f4);

@@ -32,26 +32,20 @@ constexpr uint32_t kMetaPortCheck = 1u << 16;
 
 // ---- indexed table -------------------------------------------------------
 //
-// The rules of one family are split into "key dimensions".  Each rule is
-// assigned to exactly one dimension d and is stored in d's interval index: the
-// sorted list of elementary-interval starts of the rules' key ranges on d, and
-// per interval the ordered (ascending rule index) candidate list of rules whose
-// key range covers that interval.  A packet's first match is the minimum over
-// dimensions of the first candidate (in rule order) that passes the full rule
-// test, so the index only has to return a superset of the matching rules —
-// projections (a non-prefix mask's leading-ones run, the top 32 bits of an
-// IPv6 address) keep the result exact.
-//
-// Dimension header (in the index blob, dwords):
-//   [0] key_kind   (kKey*)
-//   [1] n_bounds   number of interval starts (>= 1; bounds[0] == 0)
-//   [2] radix_bits number of leading key bits used by the radix directory
-//   [3] off_radix  dword offset of the radix directory (2^radix_bits + 1 entries)
-//   [4] off_bounds dword offset of bounds[n_bounds]   (sorted u32 interval starts)
-//   [5] off_lists  dword offset of list_start[n_bounds + 1]
-//   [6] off_cands  dword offset of candidates (u32 rule record indices)
-//   [7] reserved
-constexpr uint32_t kDimHeaderDwords = 8;
+// The rules of one family are split over "key dimensions" (destination
+// address, source address, destination port, source port).  Each rule is
+// assigned to exactly one dimension d — the one where its constraint is most
+// selective — and filed in d's radix-bucket index: bucket t covers keys
+// [t << shift, ((t+1) << shift) - 1] and lists, in ascending rule order, every
+// rule of d whose key range meets the bucket:
+//   dir[t] .. dir[t+1]   (u32, 2^(keybits - shift) + 1 entries)
+//   cands[...]           (u32 record indices)
+// A packet's first match is the minimum over dimensions of the first listed
+// rule (in rule order) that passes the full rule test, so a bucket only has to
+// list a superset of the rules that can match a key in it — the projection of
+// a non-prefix mask to its leading-ones run, or of an IPv6 address to its top
+// 32 bits, keeps the result exact.  Rules without any selective key go to the
+// family's residual list, scanned wave-uniformly in rule order.
 enum KeyKind : uint32_t {
     kKeySrc4 = 0,   // IPv4 source address (host-order value of the wire bytes)
     kKeyDst4 = 1,   // IPv4 destination address

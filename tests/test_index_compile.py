@@ -1,5 +1,5 @@
 """The INDEXED table compiler (host C++) checked on CPU: a numpy model of the
-kernel's lookup (radix directory -> interval -> ordered candidate list ->
+kernel's lookup (radix bucket -> ordered candidate list ->
 full rule test, min over key dimensions + residual scan) run over the blob
 nffacl_table_compile() produces must give the oracle's first match on every
 packet.  This validates the compiled structure without a device; the HIP
@@ -16,10 +16,9 @@ from oracle import oracle, rules_oracle as ro
 
 
 class DimInfo(ctypes.Structure):
-    _fields_ = [("kind", ctypes.c_uint32), ("shift", ctypes.c_uint32), ("n_bounds", ctypes.c_uint32),
-                ("off_radix", ctypes.c_uint32), ("off_bounds", ctypes.c_uint32), ("off_lists", ctypes.c_uint32),
-                ("off_cands", ctypes.c_uint32), ("n_rules", ctypes.c_uint32), ("n_cands", ctypes.c_uint64),
-                ("max_list", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+    _fields_ = [("kind", ctypes.c_uint32), ("shift", ctypes.c_uint32), ("n_buckets", ctypes.c_uint32),
+                ("off_dir", ctypes.c_uint32), ("off_cands", ctypes.c_uint32), ("n_rules", ctypes.c_uint32),
+                ("max_list", ctypes.c_uint32), ("reserved", ctypes.c_uint32), ("n_cands", ctypes.c_uint64)]
 
 
 class FamInfo(ctypes.Structure):
@@ -96,20 +95,16 @@ def emulate(blob, info, F, n):
             kind = di.kind
             key = {0: bswap(F["s"][0]), 1: bswap(F["t"][0]), 2: bswap(F["s"][0]), 3: bswap(F["t"][0]),
                    4: F["sp"], 5: F["dp"]}[kind].astype(np.uint64)
-            radix = blob[di.off_radix:di.off_radix + (1 << (32 - di.shift if kind < 4 else 16 - di.shift)) + 1]
-            bounds = blob[di.off_bounds:di.off_bounds + di.n_bounds].astype(np.uint64)
-            lists = blob[di.off_lists:di.off_lists + di.n_bounds + 1]
-            j = np.searchsorted(bounds, key, side="right") - 1
+            dirv = blob[di.off_dir:di.off_dir + di.n_buckets + 1].astype(np.int64)
             t = (key >> np.uint64(di.shift)).astype(np.int64)
-            assert (j >= radix[t]).all() and (j <= radix[t + 1]).all(), "radix directory bracket broken"
-            start, end = lists[j].astype(np.int64), lists[j + 1].astype(np.int64)
+            assert (t < di.n_buckets).all()
+            start, end = dirv[t], dirv[t + 1]
             for k in range(di.max_list):
                 live = mine & (start + k < end)
                 if not live.any():
                     break
                 sel = np.nonzero(live)[0]
                 r = blob[di.off_cands + start[sel] + k].astype(np.uint64)
-                assert (np.diff(blob[di.off_cands + start[sel] + k]) is not None)
                 keep = r < best[sel]
                 sel, r = sel[keep], r[keep]
                 ok, out = match(blob, fi.off_rec, v6, r.astype(np.int64), F, sel)
@@ -136,16 +131,17 @@ def check(text: str, slots: np.ndarray, n: int):
     sel = ~F["skip"]
     got = np.where(best != 0xFFFFFFFF, out, 0)
     np.testing.assert_array_equal(got[sel], want[sel])
-    # every candidate list ascends (first-match order is preserved)
+    # every bucket list ascends (first-match order is preserved)
     for fam in range(2):
         fi = info.fam[fam]
         for d in range(fi.n_dims):
             di = fi.dims[d]
-            lists = blob[di.off_lists:di.off_lists + di.n_bounds + 1]
+            dirv = blob[di.off_dir:di.off_dir + di.n_buckets + 1].astype(np.int64)
+            assert dirv[0] == 0 and dirv[-1] == di.n_cands and (np.diff(dirv) >= 0).all()
             c = blob[di.off_cands:di.off_cands + int(di.n_cands)].astype(np.int64)
-            inner = np.ones(len(c), bool)
-            inner[lists[:-1][lists[:-1] < len(c)]] = False
-            assert (np.diff(c)[inner[1:]] > 0).all()
+            first = np.zeros(len(c), bool)
+            first[dirv[:-1][dirv[:-1] < len(c)]] = True
+            assert (np.diff(c)[~first[1:]] > 0).all()
     return info
 
 
