@@ -174,20 +174,20 @@ typedef struct nffacl_dim_info {
     uint32_t kind;       /* key: 0 src4, 1 dst4, 2 src6 (top 32 bits), 3 dst6, 4 sport, 5 dport */
     uint32_t shift;      /* bucket = key >> shift */
     uint32_t n_buckets;  /* radix buckets */
-    uint32_t off_dir;    /* dword offset of dir[n_buckets + 1] (bucket list bounds) */
-    uint32_t off_cands;  /* dword offset of the bucket lists (record indices, ascending per bucket) */
+    uint32_t off_dir;    /* dword offset of dir[n_buckets + 1] (bucket bounds, in entries) */
+    uint32_t off_entries;/* dword offset of the bucket entries (inline rules, ascending per bucket) */
     uint32_t n_rules;    /* rules indexed by this key */
     uint32_t max_list;   /* longest bucket list */
     uint32_t reserved;
-    uint64_t n_cands;    /* bucket-list entries (with replication) */
+    uint64_t n_entries;  /* bucket entries (with replication) */
 } nffacl_dim_info;
 
 typedef struct nffacl_family_info {
-    uint32_t n_dims;
-    uint32_t off_rec;    /* dword offset of the rule records (8 dwords IPv4, 20 IPv6) */
-    uint32_t n_rec;      /* live records */
-    uint32_t off_resid, n_resid; /* records scanned linearly (no selective key) */
-    nffacl_dim_info dims[4];
+    uint32_t n_rec;        /* live rules of the family */
+    uint32_t off_rec;      /* LINEAR: dword offset of the rule records (8 dwords IPv4, 20 IPv6) */
+    uint32_t entry_dwords; /* INDEXED: dwords per entry (8 IPv4, 20 IPv6) */
+    uint32_t off_resid, n_resid; /* INDEXED: entries scanned linearly (no selective key) */
+    nffacl_dim_info dims[4];     /* INDEXED: [dst addr, src addr, dst port, src port] */
 } nffacl_family_info;
 
 typedef struct nffacl_table_info {

@@ -201,15 +201,15 @@ int nffacl_table_compile(const nffacl_rules *rules, int algo, uint32_t *blob, ui
     const uint32_t off_rec[2] = {ct.off_rec4, ct.off_rec6}, n_rec[2] = {ct.n4, ct.n6};
     for (int f = 0; f < 2; ++f) {
         nffacl_family_info &o = info->fam[f];
-        o.n_dims = fi[f]->n_dims;
-        o.off_rec = off_rec[f];
         o.n_rec = n_rec[f];
+        o.off_rec = off_rec[f];
+        o.entry_dwords = fi[f]->entry_dwords;
         o.off_resid = fi[f]->off_resid;
         o.n_resid = fi[f]->n_resid;
         for (int k = 0; k < 4; ++k) {
             const DimInfo &d = fi[f]->dims[k];
-            o.dims[k] = nffacl_dim_info{d.kind, d.shift, d.n_buckets, d.off_dir, d.off_cands, d.n_rules,
-                                        d.max_list, 0, d.n_cands};
+            o.dims[k] = nffacl_dim_info{d.kind, d.shift, d.n_buckets, d.off_dir, d.off_ent, d.n_rules,
+                                        d.max_list, 0, d.n_ent};
         }
     }
     if (blob) {

@@ -114,8 +114,8 @@ struct DimBuild {
     std::vector<KeyRange> ranges; // parallel to rules
     // built
     uint32_t rb = 0, shift = 0, max_list = 0;
-    std::vector<uint32_t> dir, cands;
-    std::vector<uint64_t> span;   // per rule: buckets covered
+    std::vector<uint32_t> dir, ents;  // ents: record indices per bucket entry
+    std::vector<uint64_t> span;       // per rule: buckets covered
 };
 
 // Radix bits for a dimension holding n rules: about 4 buckets per rule,
@@ -148,9 +148,17 @@ uint64_t span_dim(DimBuild &d) {
 }
 
 // Bucket t holds, in ascending rule order, every rule whose key range meets
-// [t << shift, ((t + 1) << shift) - 1]; dir[t] .. dir[t+1] delimit it.
+// [t << shift, ((t+1) << shift) - 1]; dir[t] .. dir[t+1] delimit it.
 void finish_dim(DimBuild &d) {
-    span_dim(d);  // sets rb / shift
+    if (d.rules.empty()) {  // empty slot: 2 empty buckets
+        d.rb = 1;
+        d.shift = d.key_bits - 1;
+        d.dir.assign(3, 0);
+        d.ents.clear();
+        d.max_list = 0;
+        return;
+    }
+    span_dim(d);
     const size_t nb = size_t(1) << d.rb;
     std::vector<uint32_t> len(nb + 1, 0);
     for (const KeyRange &r : d.ranges)
@@ -161,14 +169,32 @@ void finish_dim(DimBuild &d) {
         d.dir[t + 1] = d.dir[t] + len[t];
         d.max_list = std::max(d.max_list, len[t]);
     }
-    d.cands.assign(d.dir[nb], 0);
+    d.ents.assign(d.dir[nb], 0);
     std::vector<uint32_t> fill(d.dir.begin(), d.dir.end() - 1);
     for (size_t i = 0; i < d.rules.size(); ++i)  // ascending rule order -> sorted lists
         for (uint64_t t = d.ranges[i].lo >> d.shift; t <= (d.ranges[i].hi >> d.shift); ++t)
-            d.cands[fill[t]++] = d.rules[i];
+            d.ents[fill[t]++] = d.rules[i];
 }
 
-// Assign the live records of one family to key dimensions and build them.
+// Inline entry of record r (table.hpp) appended to blob.
+void emit_entry(const uint32_t *rec, bool v6, uint32_t r, std::vector<uint32_t> &blob) {
+    if (!v6) {
+        const uint32_t meta = rec[4];
+        const uint32_t exact = ((meta >> 8) & 0xFFu) ? kEntExact : 0u;
+        blob.insert(blob.end(), {rec[0], rec[1], rec[2], rec[3],
+                                 (meta & 0xFFu) | exact | (r << kEntIndexShift), rec[5], rec[6], rec[7]});
+    } else {
+        const uint32_t meta = rec[16];
+        const uint32_t exact = ((meta >> 8) & 0xFFu) ? kEntExact : 0u;
+        blob.insert(blob.end(), {rec[0], rec[4], rec[8], rec[12],
+                                 (meta & 0xFFu) | exact | (r << kEntIndexShift), rec[17], rec[18], rec[19],
+                                 rec[1], rec[2], rec[3], rec[5], rec[6], rec[7],
+                                 rec[9], rec[10], rec[11], rec[13], rec[14], rec[15]});
+    }
+}
+
+// Assign the live records of one family to key slots and emit the slots'
+// directories + inline entries and the residual entries.
 void build_family(const std::vector<uint32_t> &recs, uint32_t rw, bool v6, uint32_t n,
                   std::vector<uint32_t> &blob, FamilyIndex &fi) {
     static const uint32_t kinds4[4] = {kKeyDst4, kKeySrc4, kKeyDport, kKeySport};
@@ -180,7 +206,7 @@ void build_family(const std::vector<uint32_t> &recs, uint32_t rw, bool v6, uint3
         dims[k].kind = v6 ? kinds6[k] : kinds4[k];
         dims[k].key_bits = k < 2 ? 32 : 16;
     }
-    // preference order per rule: dimensions by increasing coverage
+    // preference order per rule: slots by increasing coverage
     std::vector<int> choice(n, -1);
     std::vector<std::array<int, 4>> pref(n);
     for (uint32_t r = 0; r < n; ++r) {
@@ -192,9 +218,8 @@ void build_family(const std::vector<uint32_t> &recs, uint32_t rw, bool v6, uint3
         pref[r] = o;
         choice[r] = kr[o[0]].cover < 1.0 ? o[0] : -1;
     }
-    // Bound replication: a dimension may hold at most `budget` list entries;
-    // past it, the widest rules move to their next-best dimension (or to the
-    // residual scan).
+    // Bound replication: a slot may hold at most `budget` entries; past it,
+    // the widest rules move to their next-best slot (or to the residual scan).
     std::vector<int> rank(n, 0);
     for (int round = 0; round < 8; ++round) {
         for (int k = 0; k < 4; ++k) {
@@ -233,29 +258,40 @@ void build_family(const std::vector<uint32_t> &recs, uint32_t rw, bool v6, uint3
     }
     for (uint32_t r = 0; r < n; ++r)
         if (choice[r] < 0) resid.push_back(r);
-    // emit non-empty dimensions (fixed order), then the residual list
-    fi.n_dims = 0;
+    const uint32_t ew = v6 ? kEnt6Dwords : kEnt4Dwords;
+    fi.entry_dwords = ew;
     for (int k = 0; k < 4; ++k) {
         DimBuild &d = dims[k];
-        if (d.rules.empty()) continue;
         finish_dim(d);
-        DimInfo &di = fi.dims[fi.n_dims++];
+        DimInfo &di = fi.dims[k];
         di.kind = d.kind;
         di.shift = d.shift;
         di.n_buckets = 1u << d.rb;
         di.n_rules = static_cast<uint32_t>(d.rules.size());
-        di.n_cands = d.cands.size();
+        di.n_ent = d.ents.size();
         di.max_list = d.max_list;
         di.off_dir = static_cast<uint32_t>(blob.size());
         blob.insert(blob.end(), d.dir.begin(), d.dir.end());
-        di.off_cands = static_cast<uint32_t>(blob.size());
-        blob.insert(blob.end(), d.cands.begin(), d.cands.end());
-        if (d.cands.empty()) blob.push_back(0);  // keep cands[0] addressable
+        while (blob.size() % 4) blob.push_back(0);  // entries 16-byte aligned
+        di.off_ent = static_cast<uint32_t>(blob.size());
+        for (uint32_t r : d.ents) emit_entry(recs.data() + size_t(r) * rw, v6, r, blob);
+        if (d.ents.empty()) blob.insert(blob.end(), ew, 0u);  // keep entry 0 addressable
+        if (k >= 2 && !d.rules.empty()) fi.port_dims = true;
     }
     fi.off_resid = static_cast<uint32_t>(blob.size());
     fi.n_resid = static_cast<uint32_t>(resid.size());
-    blob.insert(blob.end(), resid.begin(), resid.end());
-    while (blob.size() % 4) blob.push_back(0);  // keep 16-byte alignment
+    for (uint32_t r : resid) emit_entry(recs.data() + size_t(r) * rw, v6, r, blob);
+    while (blob.size() % 4) blob.push_back(0);
+}
+
+// Indexed tables encode id_mask as one bit and the rule index in 23 bits.
+bool indexable(const nffacl_rules &rules) {
+    if (rules.ip4.size() >= kMaxIndexedRules || rules.ip6.size() >= kMaxIndexedRules) return false;
+    for (const auto &r : rules.ip4)
+        if (r.l4.id_mask != 0 && r.l4.id_mask != 0xFF) return false;
+    for (const auto &r : rules.ip6)
+        if (r.l4.id_mask != 0 && r.l4.id_mask != 0xFF) return false;
+    return true;
 }
 
 }  // namespace
@@ -273,12 +309,14 @@ bool compile_table(const nffacl_rules &rules, int algo, CompiledTable &out, std:
         if (emit_rec4(r, rec4)) ++out.n4;
     for (const auto &r : rules.ip6)
         if (emit_rec6(r, rec6)) ++out.n6;
-    out.off_rec4 = 0;
-    out.off_rec6 = static_cast<uint32_t>(rec4.size());
-    out.blob = rec4;
-    out.blob.insert(out.blob.end(), rec6.begin(), rec6.end());
-    out.algo = (algo == NFFACL_ALGO_LINEAR) ? NFFACL_ALGO_LINEAR : NFFACL_ALGO_INDEXED;
-    if (out.algo == NFFACL_ALGO_INDEXED) {
+    const bool indexed = algo != NFFACL_ALGO_LINEAR && indexable(rules);
+    out.algo = indexed ? NFFACL_ALGO_INDEXED : NFFACL_ALGO_LINEAR;
+    if (!indexed) {
+        out.off_rec4 = 0;
+        out.off_rec6 = static_cast<uint32_t>(rec4.size());
+        out.blob = rec4;
+        out.blob.insert(out.blob.end(), rec6.begin(), rec6.end());
+    } else {
         build_family(rec4, kRec4Dwords, false, out.n4, out.blob, out.idx4);
         build_family(rec6, kRec6Dwords, true, out.n6, out.blob, out.idx6);
     }

@@ -11,32 +11,35 @@
 
 namespace nffacl {
 
-// One key dimension of the indexed table (see table.hpp).
+// One key dimension ("slot") of the indexed table of a family (table.hpp).
 struct DimInfo {
     uint32_t kind = 0;       // KeyKind
     uint32_t shift = 0;      // bucket = key >> shift
     uint32_t n_buckets = 0;  // 2^(key bits - shift)
-    uint32_t off_dir = 0, off_cands = 0;  // dword offsets into blob
+    uint32_t off_dir = 0;    // dword offset of dir[n_buckets + 1]
+    uint32_t off_ent = 0;    // dword offset of the bucket entries (inline rule entries)
     uint32_t n_rules = 0;    // rules assigned to this dimension
-    uint64_t n_cands = 0;    // total candidate entries (with replication)
+    uint64_t n_ent = 0;      // bucket entries (with replication)
     uint32_t max_list = 0;   // longest bucket list
 };
 
-// Indexed view of one address family.
+// Indexed view of one address family: always 4 slots in the order
+// [dst address, src address, dst port, src port] (empty slots allowed).
 struct FamilyIndex {
-    uint32_t n_dims = 0;
+    uint32_t entry_dwords = 0;  // 8 (IPv4) or 20 (IPv6)
     DimInfo dims[4];
-    uint32_t off_resid = 0, n_resid = 0;  // residual record indices (scanned linearly)
+    uint32_t off_resid = 0, n_resid = 0;  // residual entries (scanned linearly)
+    bool port_dims = false;               // slot 2 or 3 non-empty
 };
 
 struct CompiledTable {
     int algo = NFFACL_ALGO_LINEAR;
     // One contiguous blob of dwords, uploaded as is.
     std::vector<uint32_t> blob;
-    // Linear records (dword offsets into blob) and live record counts.
+    // LINEAR: rule records (dword offsets into blob) and live record counts.
     uint32_t off_rec4 = 0, n4 = 0;
     uint32_t off_rec6 = 0, n6 = 0;
-    // Indexed: per family key dimensions + residual list.
+    // INDEXED: per family key slots + residual entries.
     FamilyIndex idx4, idx6;
 };
 

@@ -263,12 +263,12 @@ k_linear_frames(const uint8_t *__restrict__ frames, const uint64_t *__restrict__
 // INDEXED: per-lane interval search + ordered candidate lists (table.hpp).
 // ---------------------------------------------------------------------------
 
-struct DimArgs {
-    uint32_t kind, shift, off_dir, off_cands;
+struct SlotArgs {
+    uint32_t shift, off_dir, off_ent, pad;
 };
 struct FamArgs {
-    uint32_t n_dims, off_rec, n_resid, off_resid;
-    DimArgs dim[4];
+    SlotArgs slot[4];  // [dst addr, src addr, dst port, src port]
+    uint32_t off_resid, n_resid;
 };
 struct IndexedArgs {
     const uint32_t *tab;  // device table (global memory)
@@ -295,82 +295,90 @@ struct GlobalTab {
 
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 
-// Full rule test of record r (acl.go:525-541 / 545-559 for one rule).
-template <bool V6, class T>
-__device__ __forceinline__ bool rule_matches(const T &tab, uint32_t off_rec, uint32_t r,
-                                             const Fields &f, uint32_t &out) {
-    if (!V6) {
-        const uint32_t b0 = off_rec + r * kRec4Dwords;
-        const u32x4 a = tab.ld4(b0), b = tab.ld4(b0 + 4);
-        const uint32_t m = ((f.s[0] ^ a.x) & a.y) | ((f.t[0] ^ a.z) & a.w) |
-                           ((f.proto ^ b.x) & ((b.x >> 8) & 0xFFu)) | port_miss(f.ports, b.y, b.z);
-        out = b.w;
-        return m == 0u;
-    } else {
-        const uint32_t b0 = off_rec + r * kRec6Dwords;
-        const u32x4 sa = tab.ld4(b0), sm = tab.ld4(b0 + 4), da = tab.ld4(b0 + 8), dm = tab.ld4(b0 + 12),
-                    b = tab.ld4(b0 + 16);
-        const uint32_t m = ((f.s[0] ^ sa.x) & sm.x) | ((f.s[1] ^ sa.y) & sm.y) | ((f.s[2] ^ sa.z) & sm.z) |
-                           ((f.s[3] ^ sa.w) & sm.w) | ((f.t[0] ^ da.x) & dm.x) | ((f.t[1] ^ da.y) & dm.y) |
-                           ((f.t[2] ^ da.z) & dm.z) | ((f.t[3] ^ da.w) & dm.w) |
-                           ((f.proto ^ b.x) & ((b.x >> 8) & 0xFFu)) | port_miss(f.ports, b.y, b.z);
-        out = b.w;
-        return m == 0u;
-    }
+// Mismatch bits of an entry's first 8 dwords (A = words 0..3, B = 4..7):
+// address words, protocol (exact flag) and ports — acl.go:526-539 / 546-557
+// with IPv6 restricted to the top 32 bits of each address.
+__device__ __forceinline__ uint32_t entry_miss(const u32x4 &A, const u32x4 &B, const Fields &f) {
+    const uint32_t proto = ((f.proto ^ B.x) & 0xFFu) & (0u - ((B.x >> 8) & 1u));
+    return ((f.s[0] ^ A.x) & A.y) | ((f.t[0] ^ A.z) & A.w) | proto | port_miss(f.ports, B.y, B.z);
 }
 
-__device__ __forceinline__ uint32_t dim_key(uint32_t kind, const Fields &f) {
-    switch (kind) {
-    case kKeyDst4: case kKeyDst6: return __builtin_bswap32(f.t[0]);
-    case kKeySrc4: case kKeySrc6: return __builtin_bswap32(f.s[0]);
-    case kKeyDport: return f.ports >> 16;
-    default: return f.ports & 0xFFFFu;
-    }
+// Mismatch bits of the IPv6 extension words 8..19 (address words 1..3).
+template <class T>
+__device__ __forceinline__ uint32_t entry_miss_ext(const T &tab, uint32_t off, const Fields &f) {
+    const u32x4 x = tab.ld4(off), y = tab.ld4(off + 4), z = tab.ld4(off + 8);
+    // x = s1 s2 s3 sm1 | y = sm2 sm3 t1 t2 | z = t3 tm1 tm2 tm3
+    return ((f.s[1] ^ x.x) & x.w) | ((f.s[2] ^ x.y) & y.x) | ((f.s[3] ^ x.z) & y.y) |
+           ((f.t[1] ^ y.z) & z.y) | ((f.t[2] ^ y.w) & z.z) | ((f.t[3] ^ z.x) & z.w);
 }
 
-// First match of one family for the lanes with `mine` set; best/out carry
-// the running minimum record index and its OutputNumber.  All loops have a
-// wave-uniform trip count (a ballot), their bodies are predicated, so the
-// wave never splits its exec mask.
-template <bool V6, class T>
-__device__ __forceinline__ void classify_family(const T &tab, const FamArgs &fa, const Fields &f,
-                                                bool mine, uint32_t &best, uint32_t &out) {
-    for (uint32_t d = 0; d < fa.n_dims; ++d) {
-        const DimArgs &da = fa.dim[d];
-        const uint32_t t = dim_key(da.kind, f) >> da.shift;
-        uint32_t c = tab.ld(da.off_dir + t);
-        uint32_t e = tab.ld(da.off_dir + t + 1);
-        if (!mine) e = c;
-        while (ballot(c < e)) {
-            const bool act = c < e;
-            const uint32_t r = tab.ld(da.off_cands + (act ? c : 0u));
-            uint32_t o;
-            const bool hit = rule_matches<V6>(tab, fa.off_rec, r, f, o);
-            const bool earlier = act && r < best;
-            const bool take = earlier && hit;
-            best = take ? r : best;
-            out = take ? o : out;
+// First match over the four key slots of the lane's family, walked together:
+// every iteration tests the next entry of every slot list, so the wave pays
+// max(list lengths) table round trips, not their sum.  Loops have
+// wave-uniform trip counts (ballots) and predicated bodies.
+template <int NS, class T>
+__device__ __forceinline__ uint32_t classify_indexed(const T &tab, const IndexedArgs &a, const Fields &f) {
+    const bool v6 = f.is6;
+    const bool mine = f.is4 || f.is6;
+    const uint32_t ew = v6 ? kEnt6Dwords : kEnt4Dwords;
+    const uint32_t key[4] = {__builtin_bswap32(f.t[0]), __builtin_bswap32(f.s[0]), f.ports >> 16,
+                             f.ports & 0xFFFFu};
+    uint32_t c[NS], e[NS], base[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        const SlotArgs &s4 = a.f4.slot[s], &s6 = a.f6.slot[s];
+        const uint32_t shift = v6 ? s6.shift : s4.shift;
+        const uint32_t dir = v6 ? s6.off_dir : s4.off_dir;
+        base[s] = v6 ? s6.off_ent : s4.off_ent;
+        const uint32_t t = key[s] >> shift;
+        c[s] = tab.ld(dir + t);
+        e[s] = mine ? tab.ld(dir + t + 1) : c[s];
+    }
+    uint32_t best = kNone, out = 0;
+    while (true) {
+        bool any = false;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) any |= c[s] < e[s];
+        if (!ballot(any)) break;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            const bool act = c[s] < e[s];
+            const uint32_t off = base[s] + (act ? c[s] : 0u) * ew;
+            const u32x4 A = tab.ld4(off), B = tab.ld4(off + 4);
+            const uint32_t idx = B.x >> kEntIndexShift;
+            const bool earlier = act && idx < best;
+            bool pass = entry_miss(A, B, f) == 0u;
+            const bool ext = v6 && earlier && pass;
+            if (ballot(ext)) {
+                if (ext) pass = entry_miss_ext(tab, off + 8, f) == 0u;
+            }
+            const bool take = earlier && pass;
+            best = take ? idx : best;
+            out = take ? B.w : out;
             // stop at a hit, or once the ascending list has passed `best`
-            c = (earlier && !hit) ? c + 1 : e;
+            c[s] = (earlier && !pass) ? c[s] + 1 : e[s];
         }
     }
-    // rules with no selective key: wave-uniform scan in rule order
-    for (uint32_t i = 0; i < fa.n_resid; ++i) {
-        const uint32_t r = tab.ld(fa.off_resid + i);
-        const bool want = mine && r < best;
-        if (!ballot(want)) break;  // residual list ascends too
-        uint32_t o;
-        const bool take = want && rule_matches<V6>(tab, fa.off_rec, r, f, o);
-        best = take ? r : best;
-        out = take ? o : out;
+    // rules with no selective key: wave-uniform scan in rule order per family
+#pragma unroll
+    for (int fam = 0; fam < 2; ++fam) {
+        const FamArgs &fa = fam ? a.f6 : a.f4;
+        const bool in_fam = fam ? f.is6 : f.is4;
+        const uint32_t w = fam ? kEnt6Dwords : kEnt4Dwords;
+        for (uint32_t i = 0; i < fa.n_resid; ++i) {
+            const uint32_t off = fa.off_resid + i * w;
+            const u32x4 A = tab.ld4(off), B = tab.ld4(off + 4);
+            const uint32_t idx = B.x >> kEntIndexShift;
+            const bool want = in_fam && idx < best;
+            if (!ballot(want)) break;  // residual list ascends too
+            bool pass = want && entry_miss(A, B, f) == 0u;
+            if (fam && ballot(pass)) {
+                if (pass) pass = entry_miss_ext(tab, off + 8, f) == 0u;
+            }
+            best = pass ? idx : best;
+            out = pass ? B.w : out;
+        }
     }
-}
-
-template <class T>
-__device__ __forceinline__ uint32_t classify_indexed(const T &tab, const IndexedArgs &a, const Fields &f) {
-    uint32_t best = kNone, out = 0;
-    if (ballot(f.is4)) classify_family<false>(tab, a.f4, f, f.is4, best, out);
-    if (ballot(f.is6)) classify_family<true>(tab, a.f6, f, f.is6, best, out);
     return best != kNone ? out : 0u;
 }
 
@@ -381,9 +389,15 @@ __device__ __forceinline__ void stage_table(const IndexedArgs &a) {
     __syncthreads();
 }
 
+template <int NS, bool LDS>
+__device__ __forceinline__ uint32_t classify_any(const IndexedArgs &a, const Fields &f) {
+    if (LDS) return classify_indexed<NS>(LdsTab{}, a, f);
+    return classify_indexed<NS>(GlobalTab{a.tab}, a, f);
+}
+
 // Grid-stride over 64-packet batches with the next batch's packet loads in
 // flight while the current batch is classified (software pipelining).
-template <bool LDS>
+template <int NS, bool LDS>
 __global__ void __launch_bounds__(1024)
 k_indexed_slots(const uint8_t *__restrict__ slots, uint32_t stride, uint64_t n, IndexedArgs a,
                 uint32_t *__restrict__ port_out, uint64_t *__restrict__ permit_out) {
@@ -408,14 +422,12 @@ k_indexed_slots(const uint8_t *__restrict__ slots, uint32_t stride, uint64_t n, 
         parse_fields(cur, live, f, [&](uint32_t k, uint32_t &lo, uint32_t &hi) {
             far_dwords(pkt, stride, k, lo, hi);
         });
-        uint32_t res;
-        if (LDS) res = classify_indexed(LdsTab{}, a, f);
-        else res = classify_indexed(GlobalTab{a.tab}, a, f);
+        const uint32_t res = classify_any<NS, LDS>(a, f);
         store_verdicts(base, lane, live, res, port_out, permit_out);
     }
 }
 
-template <bool LDS>
+template <int NS, bool LDS>
 __global__ void __launch_bounds__(1024)
 k_indexed_frames(const uint8_t *__restrict__ frames, const uint64_t *__restrict__ desc, uint64_t n,
                  IndexedArgs a, uint32_t *__restrict__ port_out, uint64_t *__restrict__ permit_out) {
@@ -433,9 +445,7 @@ k_indexed_frames(const uint8_t *__restrict__ frames, const uint64_t *__restrict_
         parse_fields(d, live, f, [&](uint32_t k, uint32_t &lo, uint32_t &hi) {
             far_dwords(pkt, len, k, lo, hi);
         });
-        uint32_t res;
-        if (LDS) res = classify_indexed(LdsTab{}, a, f);
-        else res = classify_indexed(GlobalTab{a.tab}, a, f);
+        const uint32_t res = classify_any<NS, LDS>(a, f);
         store_verdicts(base, lane, live, res, port_out, permit_out);
     }
 }
@@ -497,18 +507,16 @@ static dev::IndexedArgs indexed_args(const DevTable *t) {
     dev::IndexedArgs a{};
     a.tab = t->d_blob;
     a.tab_dwords = static_cast<uint32_t>(t->meta.blob.size());
-    auto fam = [&](const FamilyIndex &fi, uint32_t off_rec, dev::FamArgs &fa) {
-        fa.n_dims = fi.n_dims;
-        fa.off_rec = off_rec;
-        fa.n_resid = fi.n_resid;
-        fa.off_resid = fi.off_resid;
+    auto fam = [&](const FamilyIndex &fi, dev::FamArgs &fa) {
         for (uint32_t k = 0; k < 4; ++k) {
             const DimInfo &d = fi.dims[k];
-            fa.dim[k] = dev::DimArgs{d.kind, d.shift, d.off_dir, d.off_cands};
+            fa.slot[k] = dev::SlotArgs{d.shift, d.off_dir, d.off_ent, 0};
         }
+        fa.off_resid = fi.off_resid;
+        fa.n_resid = fi.n_resid;
     };
-    fam(t->meta.idx4, t->meta.off_rec4, a.f4);
-    fam(t->meta.idx6, t->meta.off_rec6, a.f6);
+    fam(t->meta.idx4, a.f4);
+    fam(t->meta.idx6, a.f6);
     return a;
 }
 
@@ -517,28 +525,35 @@ constexpr size_t kLdsBytes = 160 * 1024;
 
 struct IndexedLaunch {
     bool lds;
+    int ns;
     uint32_t block, per_cu;
     size_t lds_bytes;
 };
 
 static IndexedLaunch indexed_launch(const DevTable *t) {
     const size_t bytes = t->meta.blob.size() * sizeof(uint32_t);
+    const int ns = (t->meta.idx4.port_dims || t->meta.idx6.port_dims) ? 4 : 2;
     if (bytes <= kLdsBytes - 1024) {
         const uint32_t per_cu = static_cast<uint32_t>(std::min<size_t>(2, kLdsBytes / bytes));
-        return IndexedLaunch{true, per_cu >= 2 ? 1024u : 1024u, per_cu, bytes};
+        return IndexedLaunch{true, ns, 1024u, per_cu, bytes};
     }
-    return IndexedLaunch{false, 256u, 8u, 0};
+    return IndexedLaunch{false, ns, 256u, 8u, 0};
+}
+
+template <class K>
+static hipError_t allow_lds(K kernel) {
+    return hipFuncSetAttribute(reinterpret_cast<const void *>(kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kLdsBytes));
 }
 
 int prepare_kernels() {
     static std::once_flag once;
     static hipError_t err = hipSuccess;
     std::call_once(once, [] {
-        err = hipFuncSetAttribute(reinterpret_cast<const void *>(dev::k_indexed_slots<true>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kLdsBytes));
-        if (err == hipSuccess)
-            err = hipFuncSetAttribute(reinterpret_cast<const void *>(dev::k_indexed_frames<true>),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kLdsBytes));
+        const hipError_t e[4] = {allow_lds(dev::k_indexed_slots<2, true>), allow_lds(dev::k_indexed_slots<4, true>),
+                                 allow_lds(dev::k_indexed_frames<2, true>), allow_lds(dev::k_indexed_frames<4, true>)};
+        for (hipError_t x : e)
+            if (x != hipSuccess) err = x;
     });
     if (err != hipSuccess) {
         set_last_error(std::string("hipFuncSetAttribute(LDS): ") + hipGetErrorString(err));
@@ -554,12 +569,15 @@ int launch_slots(nffacl_engine *eng, const DevTable *t, const uint8_t *d_slots, 
         const dev::IndexedArgs a = indexed_args(t);
         const IndexedLaunch L = indexed_launch(t);
         const uint32_t grid = grid_for(eng, n, L.block, L.per_cu);
-        if (L.lds)
-            hipLaunchKernelGGL(dev::k_indexed_slots<true>, dim3(grid), dim3(L.block), L.lds_bytes, stream,
-                               d_slots, stride, n, a, d_port, d_permit);
+        const dim3 g(grid), b(L.block);
+        if (L.lds && L.ns == 2)
+            hipLaunchKernelGGL((dev::k_indexed_slots<2, true>), g, b, L.lds_bytes, stream, d_slots, stride, n, a, d_port, d_permit);
+        else if (L.lds)
+            hipLaunchKernelGGL((dev::k_indexed_slots<4, true>), g, b, L.lds_bytes, stream, d_slots, stride, n, a, d_port, d_permit);
+        else if (L.ns == 2)
+            hipLaunchKernelGGL((dev::k_indexed_slots<2, false>), g, b, 0, stream, d_slots, stride, n, a, d_port, d_permit);
         else
-            hipLaunchKernelGGL(dev::k_indexed_slots<false>, dim3(grid), dim3(L.block), 0, stream, d_slots,
-                               stride, n, a, d_port, d_permit);
+            hipLaunchKernelGGL((dev::k_indexed_slots<4, false>), g, b, 0, stream, d_slots, stride, n, a, d_port, d_permit);
     } else {
         const uint32_t block = 256;
         dev::LinearArgs a{t->d_blob + t->meta.off_rec4, t->meta.n4, t->d_blob + t->meta.off_rec6,
@@ -580,12 +598,15 @@ int launch_frames(nffacl_engine *eng, const DevTable *t, const uint8_t *d_frames
         const dev::IndexedArgs a = indexed_args(t);
         const IndexedLaunch L = indexed_launch(t);
         const uint32_t grid = grid_for(eng, n, L.block, L.per_cu);
-        if (L.lds)
-            hipLaunchKernelGGL(dev::k_indexed_frames<true>, dim3(grid), dim3(L.block), L.lds_bytes, stream,
-                               d_frames, d_desc, n, a, d_port, d_permit);
+        const dim3 g(grid), b(L.block);
+        if (L.lds && L.ns == 2)
+            hipLaunchKernelGGL((dev::k_indexed_frames<2, true>), g, b, L.lds_bytes, stream, d_frames, d_desc, n, a, d_port, d_permit);
+        else if (L.lds)
+            hipLaunchKernelGGL((dev::k_indexed_frames<4, true>), g, b, L.lds_bytes, stream, d_frames, d_desc, n, a, d_port, d_permit);
+        else if (L.ns == 2)
+            hipLaunchKernelGGL((dev::k_indexed_frames<2, false>), g, b, 0, stream, d_frames, d_desc, n, a, d_port, d_permit);
         else
-            hipLaunchKernelGGL(dev::k_indexed_frames<false>, dim3(grid), dim3(L.block), 0, stream,
-                               d_frames, d_desc, n, a, d_port, d_permit);
+            hipLaunchKernelGGL((dev::k_indexed_frames<4, false>), g, b, 0, stream, d_frames, d_desc, n, a, d_port, d_permit);
     } else {
         const uint32_t block = 256;
         dev::LinearArgs a{t->d_blob + t->meta.off_rec4, t->meta.n4, t->d_blob + t->meta.off_rec6,

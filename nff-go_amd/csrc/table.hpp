@@ -32,20 +32,36 @@ constexpr uint32_t kMetaPortCheck = 1u << 16;
 
 // ---- indexed table -------------------------------------------------------
 //
-// The rules of one family are split over "key dimensions" (destination
+// The rules of one family are split over four key "slots" (destination
 // address, source address, destination port, source port).  Each rule is
-// assigned to exactly one dimension d — the one where its constraint is most
+// assigned to exactly one slot d — the one where its constraint is most
 // selective — and filed in d's radix-bucket index: bucket t covers keys
 // [t << shift, ((t+1) << shift) - 1] and lists, in ascending rule order, every
-// rule of d whose key range meets the bucket:
-//   dir[t] .. dir[t+1]   (u32, 2^(keybits - shift) + 1 entries)
-//   cands[...]           (u32 record indices)
-// A packet's first match is the minimum over dimensions of the first listed
-// rule (in rule order) that passes the full rule test, so a bucket only has to
+// rule of d whose key range meets the bucket, as an inline entry (the full
+// rule, so a candidate costs one table read):
+//   dir[t] .. dir[t+1]      (u32, 2^(keybits - shift) + 1 entries)
+//   entries[...]            (kEnt4Dwords / kEnt6Dwords each)
+// A packet's first match is the minimum over slots of the first listed rule
+// (in rule order) that passes the full rule test, so a bucket only has to
 // list a superset of the rules that can match a key in it — the projection of
 // a non-prefix mask to its leading-ones run, or of an IPv6 address to its top
 // 32 bits, keeps the result exact.  Rules without any selective key go to the
-// family's residual list, scanned wave-uniformly in rule order.
+// family's residual entry list, scanned wave-uniformly in rule order.
+//
+// Entry (IPv4, 8 dwords = 2 x 16 B; IPv6 adds 12 extension dwords):
+//   [0] src word  [1] src mask  [2] dst word  [3] dst mask     (IPv6: top 32 bits)
+//   [4] meta = id | exact << 8 | rule_index << 9   (exact: id_mask == 0xff)
+//   [5] lo = sport_min | dport_min << 16   [6] hi = sport_max | dport_max << 16
+//   [7] output_number
+//   IPv6 [8..19]: src[1..3], src_mask[1..3], dst[1..3], dst_mask[1..3]
+// Indexed tables therefore need id_mask in {0, 0xff} (what the parsers
+// produce) and < 2^23 rules per family; other rule sets compile LINEAR.
+constexpr uint32_t kEnt4Dwords = 8;
+constexpr uint32_t kEnt6Dwords = 20;
+constexpr uint32_t kEntIndexShift = 9;
+constexpr uint32_t kEntExact = 1u << 8;
+constexpr uint32_t kMaxIndexedRules = 1u << 23;
+
 enum KeyKind : uint32_t {
     kKeySrc4 = 0,   // IPv4 source address (host-order value of the wire bytes)
     kKeyDst4 = 1,   // IPv4 destination address

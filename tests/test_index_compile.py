@@ -17,12 +17,12 @@ from oracle import oracle, rules_oracle as ro
 
 class DimInfo(ctypes.Structure):
     _fields_ = [("kind", ctypes.c_uint32), ("shift", ctypes.c_uint32), ("n_buckets", ctypes.c_uint32),
-                ("off_dir", ctypes.c_uint32), ("off_cands", ctypes.c_uint32), ("n_rules", ctypes.c_uint32),
-                ("max_list", ctypes.c_uint32), ("reserved", ctypes.c_uint32), ("n_cands", ctypes.c_uint64)]
+                ("off_dir", ctypes.c_uint32), ("off_entries", ctypes.c_uint32), ("n_rules", ctypes.c_uint32),
+                ("max_list", ctypes.c_uint32), ("reserved", ctypes.c_uint32), ("n_entries", ctypes.c_uint64)]
 
 
 class FamInfo(ctypes.Structure):
-    _fields_ = [("n_dims", ctypes.c_uint32), ("off_rec", ctypes.c_uint32), ("n_rec", ctypes.c_uint32),
+    _fields_ = [("n_rec", ctypes.c_uint32), ("off_rec", ctypes.c_uint32), ("entry_dwords", ctypes.c_uint32),
                 ("off_resid", ctypes.c_uint32), ("n_resid", ctypes.c_uint32), ("dims", DimInfo * 4)]
 
 
@@ -64,24 +64,27 @@ def fields(slots: np.ndarray, n: int):
     return dict(is4=is4 & ihl5, is6=is6, s=s, t=t, proto=proto, sp=sp, dp=dp, skip=is4 & ~ihl5)
 
 
-def match(blob, off_rec, v6, r, F, sel):
-    """Full rule test of record r[i] against packet sel[i] (vectorised)."""
-    rw = 20 if v6 else 8
-    rec = blob[off_rec + r[:, None] * rw + np.arange(rw)[None, :]]
-    m = np.zeros(len(r), np.uint32)
-    if v6:
-        for k in range(4):
-            m |= (F["s"][k][sel] ^ rec[:, k]) & rec[:, 4 + k]
-            m |= (F["t"][k][sel] ^ rec[:, 8 + k]) & rec[:, 12 + k]
-        meta, lo, hi, out = rec[:, 16], rec[:, 17], rec[:, 18], rec[:, 19]
-    else:
-        m |= (F["s"][0][sel] ^ rec[:, 0]) & rec[:, 1]
-        m |= (F["t"][0][sel] ^ rec[:, 2]) & rec[:, 3]
-        meta, lo, hi, out = rec[:, 4], rec[:, 5], rec[:, 6], rec[:, 7]
-    m |= (F["proto"][sel] ^ meta) & ((meta >> 8) & 0xFF)
+def match(blob, offs, v6, F, sel):
+    """Full rule test of the entries at dword offsets offs[i] against packet
+    sel[i] (vectorised); returns (ok, rule index, output number)."""
+    ew = 20 if v6 else 8
+    e = blob[offs[:, None] + np.arange(ew)[None, :]]
+    m = (F["s"][0][sel] ^ e[:, 0]) & e[:, 1]
+    m |= (F["t"][0][sel] ^ e[:, 2]) & e[:, 3]
+    meta, lo, hi, out = e[:, 4], e[:, 5], e[:, 6], e[:, 7]
+    if v6:  # extension: s1 s2 s3 sm1 sm2 sm3 t1 t2 t3 tm1 tm2 tm3
+        for k in range(3):
+            m |= (F["s"][k + 1][sel] ^ e[:, 8 + k]) & e[:, 11 + k]
+            m |= (F["t"][k + 1][sel] ^ e[:, 14 + k]) & e[:, 17 + k]
+    exact = (meta >> 8) & 1
+    m |= np.where(exact == 1, (F["proto"][sel] ^ meta) & 0xFF, 0)
     sp, dp = F["sp"][sel], F["dp"][sel]
     ok = (m == 0) & (sp >= (lo & 0xFFFF)) & (sp <= (hi & 0xFFFF)) & (dp >= (lo >> 16)) & (dp <= (hi >> 16))
-    return ok, out
+    return ok, (meta >> 9).astype(np.uint64), out
+
+
+KEYS = {0: lambda F: bswap(F["s"][0]), 1: lambda F: bswap(F["t"][0]), 2: lambda F: bswap(F["s"][0]),
+        3: lambda F: bswap(F["t"][0]), 4: lambda F: F["sp"], 5: lambda F: F["dp"]}
 
 
 def emulate(blob, info, F, n):
@@ -89,12 +92,13 @@ def emulate(blob, info, F, n):
     outv = np.zeros(n, np.uint32)
     for fam, v6 in ((0, False), (1, True)):
         fi = info.fam[fam]
+        ew = fi.entry_dwords
         mine = F["is6"] if v6 else F["is4"]
-        for d in range(fi.n_dims):
+        for d in range(4):
             di = fi.dims[d]
-            kind = di.kind
-            key = {0: bswap(F["s"][0]), 1: bswap(F["t"][0]), 2: bswap(F["s"][0]), 3: bswap(F["t"][0]),
-                   4: F["sp"], 5: F["dp"]}[kind].astype(np.uint64)
+            if di.n_rules == 0:
+                continue
+            key = KEYS[di.kind](F).astype(np.uint64)
             dirv = blob[di.off_dir:di.off_dir + di.n_buckets + 1].astype(np.int64)
             t = (key >> np.uint64(di.shift)).astype(np.int64)
             assert (t < di.n_buckets).all()
@@ -104,18 +108,18 @@ def emulate(blob, info, F, n):
                 if not live.any():
                     break
                 sel = np.nonzero(live)[0]
-                r = blob[di.off_cands + start[sel] + k].astype(np.uint64)
-                keep = r < best[sel]
-                sel, r = sel[keep], r[keep]
-                ok, out = match(blob, fi.off_rec, v6, r.astype(np.int64), F, sel)
-                best[sel[ok]] = r[ok]
+                ok, idx, out = match(blob, di.off_entries + (start[sel] + k) * ew, v6, F, sel)
+                keep = idx < best[sel]
+                ok &= keep
+                best[sel[ok]] = idx[ok]
                 outv[sel[ok]] = out[ok]
-                start[sel[ok]] = end[sel[ok]]  # stop scanning this list
+                stop = ok | ~keep
+                start[sel[stop]] = end[sel[stop]]  # hit, or list passed best
         for i in range(fi.n_resid):
-            r = int(blob[fi.off_resid + i])
-            sel = np.nonzero(mine & (best > r))[0]
-            ok, out = match(blob, fi.off_rec, v6, np.full(len(sel), r), F, sel)
-            best[sel[ok]] = r
+            sel = np.nonzero(mine)[0]
+            ok, idx, out = match(blob, np.full(len(sel), fi.off_resid + i * ew), v6, F, sel)
+            ok &= idx < best[sel]
+            best[sel[ok]] = idx[ok]
             outv[sel[ok]] = out[ok]
     return best, outv
 
@@ -131,14 +135,15 @@ def check(text: str, slots: np.ndarray, n: int):
     sel = ~F["skip"]
     got = np.where(best != 0xFFFFFFFF, out, 0)
     np.testing.assert_array_equal(got[sel], want[sel])
-    # every bucket list ascends (first-match order is preserved)
+    # every bucket list ascends in rule index (first-match order is preserved)
     for fam in range(2):
         fi = info.fam[fam]
-        for d in range(fi.n_dims):
+        ew = fi.entry_dwords
+        for d in range(4):
             di = fi.dims[d]
             dirv = blob[di.off_dir:di.off_dir + di.n_buckets + 1].astype(np.int64)
-            assert dirv[0] == 0 and dirv[-1] == di.n_cands and (np.diff(dirv) >= 0).all()
-            c = blob[di.off_cands:di.off_cands + int(di.n_cands)].astype(np.int64)
+            assert dirv[0] == 0 and dirv[-1] == di.n_entries and (np.diff(dirv) >= 0).all()
+            c = blob[di.off_entries + 4 + ew * np.arange(int(di.n_entries))].astype(np.int64) >> 9
             first = np.zeros(len(c), bool)
             first[dirv[:-1][dirv[:-1] < len(c)]] = True
             assert (np.diff(c)[~first[1:]] > 0).all()
@@ -152,7 +157,7 @@ def test_index_matches_oracle_synthetic(cfg):
     slots = synth.gen_slots(g, n, synth.PACKET_SEEDS[cfg])
     info = check(g.text, slots, n)
     fi = info.fam[0]
-    assert fi.n_dims >= 2 and fi.n_resid < 10
+    assert fi.dims[0].n_rules > 0 and fi.dims[1].n_rules > 0 and fi.n_resid < 10
 
 
 def test_index_firewall(golden):
@@ -186,4 +191,12 @@ def test_index_nested_and_overlapping_rules():
 def test_linear_table_has_no_index():
     rules = nffacl.L3Rules.parse_text(b"10.0.0.0/8 ANY ANY ANY ANY 1\n")
     _, info = compile_table(rules, nffacl.ALGO_LINEAR)
-    assert info.algo == nffacl.ALGO_LINEAR and info.fam[0].n_dims == 0
+    assert info.algo == nffacl.ALGO_LINEAR and info.fam[0].entry_dwords == 0
+
+
+def test_non_indexable_rules_compile_linear():
+    """id_mask outside {0, 0xff} (only reachable through from_arrays) -> LINEAR."""
+    r = np.zeros(1, nffacl.RULE4)
+    r["id_mask"] = 0x0F
+    _, info = compile_table(nffacl.L3Rules.from_arrays(r), nffacl.ALGO_INDEXED)
+    assert info.algo == nffacl.ALGO_LINEAR
