@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <atomic>
 #include <cstdio>
 #include <cstring>
@@ -172,12 +173,15 @@ __device__ __forceinline__ uint32_t lane_id() {
 }
 
 // Dense slots: packet i at slots + i*stride; the first 64 bytes are loaded
-// with four 16-byte non-temporal loads (read once, never re-used).
+// with four 16-byte loads.  Plain loads, not non-temporal: with one lane per
+// 64-byte row every cache line is consumed by four successive instructions,
+// and the nt policy cost 30% of stream bandwidth on this pattern
+// (profiles/r1_sol/sol.out: rows 5.26 TB/s vs rows_nt 3.66 TB/s).
 __device__ __forceinline__ void load16(const uint8_t *__restrict__ p, uint32_t (&d)[16]) {
     const u32x4 *q = reinterpret_cast<const u32x4 *>(p);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        const u32x4 v = __builtin_nontemporal_load(q + j);
+        const u32x4 v = q[j];
         d[4 * j + 0] = v.x;
         d[4 * j + 1] = v.y;
         d[4 * j + 2] = v.z;
@@ -530,14 +534,25 @@ struct IndexedLaunch {
     size_t lds_bytes;
 };
 
+// Launch-shape overrides for tuning experiments (tools/sol.py); unset in production.
+static int tune_env(const char *name, int dflt) {
+    const char *v = std::getenv(name);
+    return v && *v ? std::atoi(v) : dflt;
+}
+
 static IndexedLaunch indexed_launch(const DevTable *t) {
     const size_t bytes = t->meta.blob.size() * sizeof(uint32_t);
     const int ns = (t->meta.idx4.port_dims || t->meta.idx6.port_dims) ? 4 : 2;
-    if (bytes <= kLdsBytes - 1024) {
-        const uint32_t per_cu = static_cast<uint32_t>(std::min<size_t>(2, kLdsBytes / bytes));
-        return IndexedLaunch{true, ns, 1024u, per_cu, bytes};
+    const bool lds = bytes <= kLdsBytes - 1024 && tune_env("NFFACL_TUNE_LDS", 1) != 0;
+    IndexedLaunch L{lds, ns, 256u, 8u, 0};
+    if (lds) {
+        L.block = 1024u;
+        L.per_cu = static_cast<uint32_t>(std::min<size_t>(2, kLdsBytes / bytes));
+        L.lds_bytes = bytes;
     }
-    return IndexedLaunch{false, ns, 256u, 8u, 0};
+    L.block = static_cast<uint32_t>(tune_env("NFFACL_TUNE_BLOCK", static_cast<int>(L.block)));
+    L.per_cu = static_cast<uint32_t>(tune_env("NFFACL_TUNE_PER_CU", static_cast<int>(L.per_cu)));
+    return L;
 }
 
 template <class K>

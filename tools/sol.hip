@@ -1,0 +1,121 @@
+// sol.hip — speed-of-light microbenchmarks for the classify access pattern
+// (measurement tool, not part of libnffacl).  Every kernel reads n 64-byte
+// slots and writes one u32 per slot + one u64 per 64 slots, like
+// nffacl_classify_device, but computes only a trivial function of the bytes.
+//
+//   rows     : lane = packet, 4 x 16 B loads at stride 64 (the classify pattern)
+//   rows_pf  : rows + next-batch prefetch (classify's software pipeline)
+//   coal     : lane-contiguous 16 B loads (1 KiB per wave instruction), then
+//              each packet's dword 3 gathered with ds_bpermute
+//   copy     : plain float4 copy n*64 bytes -> n*64 bytes (HBM reference)
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t lane_id() {
+    return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
+
+template <bool NT>
+__device__ __forceinline__ void ld16(const uint8_t *p, uint32_t (&d)[16]) {
+    const u32x4 *q = reinterpret_cast<const u32x4 *>(p);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const u32x4 v = NT ? __builtin_nontemporal_load(q + j) : q[j];
+        d[4 * j] = v.x; d[4 * j + 1] = v.y; d[4 * j + 2] = v.z; d[4 * j + 3] = v.w;
+    }
+}
+
+__device__ __forceinline__ uint32_t fold(const uint32_t (&d)[16]) {
+    uint32_t x = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) x ^= d[k] * (2 * k + 1);
+    return x;
+}
+
+template <bool NT>
+__global__ void __launch_bounds__(1024) k_rows(const uint8_t *s, uint64_t n, uint32_t *port, uint64_t *bits) {
+    const uint32_t lane = lane_id();
+    const uint64_t wave0 = uint64_t(blockIdx.x) * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t step = uint64_t(gridDim.x) * (blockDim.x >> 6) * 64;
+    for (uint64_t base = wave0 * 64; base < n; base += step) {
+        const uint64_t i = base + lane;
+        uint32_t d[16];
+        ld16<NT>(s + (i < n ? i : 0) * 64, d);
+        const uint32_t r = fold(d);
+        if (i < n) port[i] = r;
+        const uint64_t b = __builtin_amdgcn_ballot_w64(i < n && (r & 1));
+        if (lane == 0) bits[base >> 6] = b;
+    }
+}
+
+template <bool NT>
+__global__ void __launch_bounds__(1024) k_rows_pf(const uint8_t *s, uint64_t n, uint32_t *port, uint64_t *bits) {
+    const uint32_t lane = lane_id();
+    const uint64_t wave0 = uint64_t(blockIdx.x) * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t step = uint64_t(gridDim.x) * (blockDim.x >> 6) * 64;
+    uint64_t base = wave0 * 64;
+    uint32_t d[16];
+    if (base < n) ld16<NT>(s + (base + lane < n ? base + lane : 0) * 64, d);
+    for (; base < n; base += step) {
+        const uint64_t i = base + lane;
+        uint32_t cur[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) cur[k] = d[k];
+        const uint64_t nb = base + step;
+        if (nb < n) ld16<NT>(s + (nb + lane < n ? nb + lane : 0) * 64, d);
+        const uint32_t r = fold(cur);
+        if (i < n) port[i] = r;
+        const uint64_t b = __builtin_amdgcn_ballot_w64(i < n && (r & 1));
+        if (lane == 0) bits[base >> 6] = b;
+    }
+}
+
+__global__ void __launch_bounds__(1024) k_coal(const uint8_t *s, uint64_t n, uint32_t *port, uint64_t *bits) {
+    const uint32_t lane = lane_id();
+    const uint64_t wave0 = uint64_t(blockIdx.x) * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t step = uint64_t(gridDim.x) * (blockDim.x >> 6) * 64;
+    for (uint64_t base = wave0 * 64; base < n; base += step) {
+        // wave's 4 KiB = 4 instructions x 1 KiB contiguous
+        const u32x4 *q = reinterpret_cast<const u32x4 *>(s + base * 64);
+        uint32_t acc = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const u32x4 v = __builtin_nontemporal_load(q + j * 64 + lane);
+            acc ^= v.x * 3 + v.y * 5 + v.z * 7 + v.w * 11;
+        }
+        // lane l holds chunk (l % 4) of packets (j*16 + l/4): gather one dword per packet
+        const uint32_t r = __builtin_amdgcn_ds_bpermute(static_cast<int>((lane & 15) * 4 * 4), static_cast<int>(acc));
+        const uint64_t i = base + lane;
+        if (i < n) port[i] = r;
+        const uint64_t b = __builtin_amdgcn_ballot_w64(i < n && (r & 1));
+        if (lane == 0) bits[base >> 6] = b;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_copy(const u32x4 *a, u32x4 *b, uint64_t n16) {
+    for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n16; i += uint64_t(gridDim.x) * blockDim.x)
+        b[i] = __builtin_nontemporal_load(a + i);
+}
+
+extern "C" int sol_run(int which, const void *slots, uint64_t n, void *port, void *bits, void *scratch,
+                       int blocks_per_cu, int block, void *stream) {
+    int cus = 256;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const dim3 g(cus * blocks_per_cu), b(block);
+    const uint8_t *s = static_cast<const uint8_t *>(slots);
+    uint32_t *p = static_cast<uint32_t *>(port);
+    uint64_t *bb = static_cast<uint64_t *>(bits);
+    switch (which) {
+    case 0: hipLaunchKernelGGL(k_rows<true>, g, b, 0, st, s, n, p, bb); break;
+    case 1: hipLaunchKernelGGL(k_rows<false>, g, b, 0, st, s, n, p, bb); break;
+    case 2: hipLaunchKernelGGL(k_rows_pf<true>, g, b, 0, st, s, n, p, bb); break;
+    case 3: hipLaunchKernelGGL(k_coal, g, b, 0, st, s, n, p, bb); break;
+    case 4: hipLaunchKernelGGL(k_copy, g, b, 0, st, reinterpret_cast<const u32x4 *>(slots),
+                               static_cast<u32x4 *>(scratch), n * 4); break;
+    default: return -1;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
