@@ -8,7 +8,7 @@ import sys
 from pathlib import Path
 
 d = Path(sys.argv[1])
-key = sys.argv[2] if len(sys.argv) > 2 else "k_indexed_slots"
+key = sys.argv[2] if len(sys.argv) > 2 and not sys.argv[2].startswith("--") else "k_indexed_slots"
 out = {}
 for sub in ("fetch", "write", "sq", "sq2"):
     f = d / sub / "run_counter_collection.csv"
@@ -35,3 +35,12 @@ if waves and "SQ_INSTS_VALU" in out:
     batches = None
     res["per_wave"] = {k: out[k] / waves for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD") if k in out}
 print(json.dumps(res, indent=1))
+# --traffic-key cfg:algo:n  -> record HBM bytes/launch for bench.py's roofline.traffic
+if "--traffic-key" in sys.argv and "hbm_bytes_per_launch" in res:
+    k = sys.argv[sys.argv.index("--traffic-key") + 1]
+    root = Path(__file__).resolve().parent.parent
+    dst = root / "profiles" / "pmc_traffic.json"
+    db = json.loads(dst.read_text()) if dst.exists() else {}
+    db[k] = {"bytes_per_launch": res["hbm_bytes_per_launch"], "source": str(d), "kernel_avg_ns": stats.get("avg_ns"),
+             "fetch_size_kb": out.get("FETCH_SIZE"), "write_size_kb": out.get("WRITE_SIZE")}
+    dst.write_text(json.dumps(db, indent=1) + "\n")
