@@ -44,8 +44,12 @@ HBM_PEAK_GBPS = 8000.0
 WORKLOADS = {
     "c1": "C1 firewall.conf (4 text rules -> 4 ip4 + 1 ip6), 64B packets, device-resident",
     "c2": "C2 1k-rule L3 ACL, 64B packets, device-resident",
+    "c3": "C3 10k-rule L3+L4 ACL, IMIX 64/570/1518 (7:4:1) packed frames, device-resident",
+    "c4": "C4 1k-rule L3 ACL, 64B packets, packet batch sharded across GPUs",
     "c5": "C5 100k-rule L3+L4 ACL with port ranges, 64B packets, device-resident",
 }
+# C3 reads each frame's first 64-byte line + its 8-byte descriptor and writes 4 B
+BYTES_PER_PACKET_FRAMES = 76
 
 
 def log(*a):
@@ -116,7 +120,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c4", "c5"])
+    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5"])
     ap.add_argument("--algo", default="auto", choices=["auto", "linear", "indexed"])
     ap.add_argument("--packets", type=int, default=1 << 24, help="packets per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -163,15 +167,28 @@ def main():
     # ---- packets: per-rank shard, resident in HBM before timing ----
     from nffacl import synth
     t0 = time.perf_counter()
-    slots = synth.gen_slots(gen, n, synth.PACKET_SEEDS[cfg] + 7919 * rank)
+    frames_mode = cfg == "c3"
+    if frames_mode:
+        frames, desc = synth.gen_imix(gen, n, synth.PACKET_SEEDS[cfg] + 7919 * rank)
+        d_frames = torch.from_numpy(frames).to(dev)
+        d_desc = torch.from_numpy(desc.view(np.int64)).to(dev)
+        slots = None
+    else:
+        slots = synth.gen_slots(gen, n, synth.PACKET_SEEDS[cfg] + 7919 * rank)
+        d_slots = torch.from_numpy(slots).to(dev)
     log(f"[rank {rank}] generated {n} packets in {time.perf_counter() - t0:.1f}s; rules ip4={n4} ip6={n6}; algo={algo_name}")
-    d_slots = torch.from_numpy(slots).to(dev)
     port = torch.empty(n, dtype=torch.int32, device=dev)
     permit = torch.empty((n + 63) // 64, dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream(dev)
 
+    def launch():
+        if frames_mode:
+            eng.classify_frames_device(d_frames, d_desc, n, port, permit, stream)
+        else:
+            eng.classify_device(d_slots, 64, n, port, permit, stream)
+
     for _ in range(args.warmup):
-        eng.classify_device(d_slots, 64, n, port, permit, stream)
+        launch()
     torch.cuda.synchronize(dev)
 
     # ---- timed region ----
@@ -182,7 +199,7 @@ def main():
     t_start = time.perf_counter()
     for s in range(args.steps):
         evs[s][0].record(stream)
-        eng.classify_device(d_slots, 64, n, port, permit, stream)
+        launch()
         evs[s][1].record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -200,13 +217,17 @@ def main():
     got = port.cpu().numpy().view(np.uint32)
     rng = np.random.default_rng(rank)
     idx = np.sort(rng.choice(n, min(n, 4096), replace=False))
-    want = oracle.classify_slots(slots.reshape(n, 64)[idx].reshape(-1), 64, len(idx), a4, a6, threads=4)
+    if frames_mode:
+        want = oracle.classify_frames(frames, desc[idx], a4, a6, threads=4)
+    else:
+        want = oracle.classify_slots(slots.reshape(n, 64)[idx].reshape(-1), 64, len(idx), a4, a6, threads=4)
     bit_exact = bool((got[idx] == want).all())
 
     total = n * world * args.steps
     value = total / elapsed / 1e6
     mean_k = float(kms.mean()) / 1e3
-    achieved = BYTES_PER_PACKET * n / mean_k / 1e9
+    bpp = BYTES_PER_PACKET_FRAMES if frames_mode else BYTES_PER_PACKET
+    achieved = bpp * n / mean_k / 1e9
     out = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -222,7 +243,8 @@ def main():
         "data": "synthetic (deterministic seeds; SURVEY.md §8d mix)",
         "config": {
             "workload": WORKLOADS.get(cfg, cfg), "rules_ip4": n4, "rules_ip6": n6,
-            "packets_per_gpu": n, "slot_bytes": 64, "algo": algo_name, "parallelism": f"dp{world}",
+            "packets_per_gpu": n, "slot_bytes": None if frames_mode else 64,
+            "algorithmic_bytes_per_packet": bpp, "algo": algo_name, "parallelism": f"dp{world}",
             "table_bytes": eng.table_bytes,
         },
         "roofline": {
@@ -236,7 +258,7 @@ def main():
     }
 
     # ---- PCIe-inclusive rate (not `value`) ----
-    if rank == 0 and not args.no_host:
+    if rank == 0 and not args.no_host and not frames_mode:
         m = min(n, 1 << 22)
         pinned = torch.from_numpy(slots[: m * 64]).pin_memory().numpy()
         eng.classify_host(pinned, 64, m)
@@ -246,7 +268,7 @@ def main():
         out["host_inclusive_mpps"] = round(m / dt / 1e6, 1)
         out["host_inclusive_bit_exact_sample"] = bool((hp[idx[idx < m]] == got[idx[idx < m]]).all())
 
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not frames_mode:
         cb, cports = cpu_baseline(slots, n, a4, a6, args.cpu_seconds)
         cb["bit_exact_vs_gpu"] = bool((cports == got[: len(cports)]).all())
         out["cpu_baseline"] = cb
