@@ -126,22 +126,22 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host", action="store_true", help="skip the PCIe-inclusive measurement")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend for N>1 (nccl = RCCL on ROCm)")
     args = ap.parse_args()
 
     import torch
     import torch.distributed as dist
     import nffacl
+    from nffacl import dist as nd
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    rank, world, local = nd.world()
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        nd.init(args.backend, dev)
 
     cfg = args.config
     n = args.packets
@@ -149,16 +149,7 @@ def main():
 
     # ---- rules: rank 0 generates, RCCL broadcast of the rule file bytes ----
     text, gen = build_rules(cfg)
-    if world > 1:
-        blob = torch.zeros(1, dtype=torch.int64, device=dev)
-        if rank == 0:
-            raw = torch.frombuffer(bytearray(text.encode()), dtype=torch.uint8).to(dev)
-            blob[0] = raw.numel()
-        dist.broadcast(blob, 0)
-        if rank != 0:
-            raw = torch.empty(int(blob[0]), dtype=torch.uint8, device=dev)
-        dist.broadcast(raw, 0)
-        text = bytes(raw.cpu().numpy()).decode()
+    text = nd.broadcast_rules(text if rank == 0 else None, dev)
     rules = nffacl.L3Rules.parse_text(text)
     n4, n6 = rules.counts()
     eng = nffacl.Engine(rules, device=local, algo=algo_id)
@@ -206,10 +197,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t_start
     kms = np.array([a.elapsed_time(b) for a, b in evs])  # per-launch kernel time (ms)
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = nd.max_over_ranks(elapsed, dev)
 
     # ---- spot parity check (outside timing): GPU verdicts vs oracle sample ----
     from oracle import oracle, rules_oracle as ro
