@@ -4,6 +4,7 @@
 // status and records details retrievable with nffacl_last_error().
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <new>
@@ -337,18 +338,26 @@ int nffacl_classify_frames_device(nffacl_engine *eng, const uint8_t *d_frames, c
                          static_cast<hipStream_t>(stream));
 }
 
-static int ensure_host_pipeline(nffacl_engine *eng, uint32_t stride) {
-    const size_t chunk = size_t(1) << 20;  // packets per pipeline stage
-    if (eng->chunk == chunk && eng->staged_stride >= stride) return NFFACL_OK;
+// Staging sized to the request: small bursts get small pinned buffers, large
+// batches stream through two 1 M-packet stages.
+static int ensure_host_pipeline(nffacl_engine *eng, uint32_t stride, uint64_t n) {
+    size_t chunk = size_t(1) << 12;
+    while (chunk < n && chunk < (size_t(1) << 20)) chunk <<= 1;
+    if (eng->chunk >= chunk && eng->staged_stride >= stride) return NFFACL_OK;
+    chunk = std::max(chunk, eng->chunk);
+    stride = std::max(stride, eng->staged_stride);
     for (int b = 0; b < 2; ++b) {
         if (eng->h_stage[b]) { (void)hipHostFree(eng->h_stage[b]); eng->h_stage[b] = nullptr; }
         if (eng->d_slots[b]) { (void)hipFree(eng->d_slots[b]); eng->d_slots[b] = nullptr; }
+        if (eng->h_port[b]) { (void)hipHostFree(eng->h_port[b]); eng->h_port[b] = nullptr; }
+        if (eng->d_port[b]) { (void)hipFree(eng->d_port[b]); eng->d_port[b] = nullptr; }
     }
+    eng->chunk = 0;
     for (int b = 0; b < 2; ++b) {
         HIP_CHECK(hipHostMalloc(reinterpret_cast<void **>(&eng->h_stage[b]), chunk * stride, hipHostMallocDefault));
         HIP_CHECK(hipMalloc(reinterpret_cast<void **>(&eng->d_slots[b]), chunk * stride));
-        if (!eng->h_port[b]) HIP_CHECK(hipHostMalloc(reinterpret_cast<void **>(&eng->h_port[b]), chunk * 4, hipHostMallocDefault));
-        if (!eng->d_port[b]) HIP_CHECK(hipMalloc(reinterpret_cast<void **>(&eng->d_port[b]), chunk * 4));
+        HIP_CHECK(hipHostMalloc(reinterpret_cast<void **>(&eng->h_port[b]), chunk * 4, hipHostMallocDefault));
+        HIP_CHECK(hipMalloc(reinterpret_cast<void **>(&eng->d_port[b]), chunk * 4));
         if (!eng->streams[b]) HIP_CHECK(hipStreamCreateWithFlags(&eng->streams[b], hipStreamNonBlocking));
         if (!eng->done[b]) HIP_CHECK(hipEventCreateWithFlags(&eng->done[b], hipEventDisableTiming));
     }
@@ -364,7 +373,7 @@ int nffacl_classify_host(nffacl_engine *eng, const uint8_t *h_slots, uint32_t st
     if (!h_slots || stride < 64 || (stride % 16) != 0) return NFFACL_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> g(eng->host_mu);
     HIP_CHECK(hipSetDevice(eng->device));
-    int st = ensure_host_pipeline(eng, stride);
+    int st = ensure_host_pipeline(eng, stride, n);
     if (st != NFFACL_OK) return st;
     DevTable *t = acquire_table(eng);
     const bool direct = pointer_is_pinned(h_slots);

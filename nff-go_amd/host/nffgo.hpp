@@ -1,0 +1,286 @@
+// nffgo.hpp — C++ host mirror of the nff-go API surface this path replaces,
+// layered on the libnffacl C-ABI (include/nffacl.h).  Header-only.
+//
+// The reference host code is Go; with no Go toolchain in this image the host
+// side above the C-ABI is C++ and mirrors the reference's names, argument
+// meaning and error behaviour, so code written against nff-go reads the same:
+//
+//   nffgo::common::NFError / ErrorCode          common/error.go:18-66
+//   nffgo::packet::GetL3ACLFromTextTable         packet/acl.go:148-178
+//   nffgo::packet::GetL3ACLFromJSON              packet/acl.go:121-134
+//   nffgo::packet::L3Rules                       packet/acl.go:451-455
+//   nffgo::packet::Packet::L3ACLPermit / Port    packet/acl.go:495-506
+//   nffgo::flow::VectorSeparateFunction          flow/flow.go:131
+//   nffgo::flow::ACLVectorSeparator              the vector separator body of
+//                                                testSingleWorkingFF.go:538-546
+//   nffgo::flow::Aggregator                      burst aggregation for GPU-size batches
+//
+// Every verdict is computed by the HIP kernels of libnffacl; there is no CPU
+// path.  Per-packet calls are one-packet GPU batches (latency-bound); batch
+// through ACLVectorSeparator / Aggregator for throughput.
+#pragma once
+
+#include <array>
+#include <cstdint>
+#include <cstring>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <optional>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "nffacl.h"
+
+namespace nffgo {
+
+namespace common {
+
+// common/error.go:18-50 (values identical).
+enum class ErrorCode : int {
+    Fail = 1,
+    ParseRuleJSONErr = 11,
+    FileErr = 12,
+    ParseRuleErr = 13,
+    IncorrectArgInRules = 14,
+    IncorrectRule = 15,
+};
+
+// common/error.go:54-66: Error() formats "<message> (<code>)".
+struct NFError {
+    ErrorCode Code = ErrorCode::Fail;
+    std::string Message;
+    std::string Error() const { return Message; }
+};
+
+inline NFError from_status(int st, const std::string &msg) {
+    NFError e;
+    e.Code = (st <= -11 && st >= -15) ? static_cast<ErrorCode>(-st) : ErrorCode::Fail;
+    e.Message = msg;
+    return e;
+}
+
+}  // namespace common
+
+namespace types {
+// types/const.go:22-45, 66-78 — the constants the ACL path depends on.
+constexpr uint16_t IPV4Number = 0x0800, IPV6Number = 0x86dd, ARPNumber = 0x0806;
+constexpr uint8_t ICMPNumber = 0x01, TCPNumber = 0x06, UDPNumber = 0x11, ICMPv6Number = 0x3a;
+constexpr uint32_t EtherLen = 14, IPv4MinLen = 20, IPv6Len = 40, TCPMinLen = 20, UDPLen = 8, ICMPLen = 8;
+using IPv4Address = uint32_t;                  // types/ipv4.go:13 (LE of wire bytes)
+using IPv6Address = std::array<uint8_t, 16>;   // types/ipv6.go:13
+}  // namespace types
+
+namespace packet {
+
+// Owner of an nffacl_rules handle plus, lazily, its compiled device table.
+class L3Rules {
+public:
+    explicit L3Rules(nffacl_rules *h) : h_(h) {}
+    L3Rules(const L3Rules &) = delete;
+    L3Rules &operator=(const L3Rules &) = delete;
+    ~L3Rules() {
+        if (eng_) nffacl_engine_destroy(eng_);
+        if (h_) nffacl_rules_free(h_);
+    }
+    const nffacl_rules *handle() const { return h_; }
+
+    // The reference's unexported ip4/ip6 slices, as the records libnffacl holds.
+    std::vector<nffacl_rule4> ip4() const {
+        size_t n4 = 0, n6 = 0;
+        nffacl_rules_counts(h_, &n4, &n6);
+        std::vector<nffacl_rule4> v(n4);
+        for (size_t i = 0; i < n4; ++i) nffacl_rules_get4(h_, i, &v[i]);
+        return v;
+    }
+    std::vector<nffacl_rule6> ip6() const {
+        size_t n4 = 0, n6 = 0;
+        nffacl_rules_counts(h_, &n4, &n6);
+        std::vector<nffacl_rule6> v(n6);
+        for (size_t i = 0; i < n6; ++i) nffacl_rules_get6(h_, i, &v[i]);
+        return v;
+    }
+
+    // Compiled table on HIP device 0 (first use compiles + uploads).
+    nffacl_engine *engine(int algo = NFFACL_ALGO_AUTO) const {
+        std::call_once(once_, [&] {
+            st_ = nffacl_engine_create_ex(0, h_, algo, &eng_);
+            if (st_ != NFFACL_OK) err_ = nffacl_last_error();
+        });
+        if (st_ != NFFACL_OK)
+            throw std::runtime_error(std::string("nffacl_engine_create: ") + nffacl_strerror(st_) + " " + err_);
+        return eng_;
+    }
+
+    // L3Rules{ip4: ..., ip6: ...} literal, as the reference tests build them.
+    static std::shared_ptr<L3Rules> FromRecords(const std::vector<nffacl_rule4> &ip4,
+                                                const std::vector<nffacl_rule6> &ip6) {
+        nffacl_rules *h = nullptr;
+        const int st = nffacl_rules_from_arrays(ip4.data(), ip4.size(), ip6.data(), ip6.size(), &h);
+        if (st != NFFACL_OK) throw std::runtime_error("nffacl_rules_from_arrays failed");
+        return std::make_shared<L3Rules>(h);
+    }
+
+private:
+    nffacl_rules *h_ = nullptr;
+    mutable std::once_flag once_;
+    mutable nffacl_engine *eng_ = nullptr;
+    mutable int st_ = NFFACL_OK;
+    mutable std::string err_;
+};
+
+using RulesOrError = std::pair<std::shared_ptr<L3Rules>, std::optional<common::NFError>>;
+
+namespace detail {
+template <class F>
+RulesOrError load(F fn, const std::string &filename) {
+    nffacl_rules *h = nullptr;
+    char err[512] = {0};
+    const int st = fn(filename.c_str(), &h, err, sizeof err);
+    if (st != NFFACL_OK) return {nullptr, common::from_status(st, err)};
+    return {std::make_shared<L3Rules>(h), std::nullopt};
+}
+}  // namespace detail
+
+// acl.go:148.  On error the rules pointer is null (the reference also hands
+// back a partly filled *L3Rules, acl.go:177, that no caller uses).
+inline RulesOrError GetL3ACLFromTextTable(const std::string &filename) {
+    return detail::load(nffacl_rules_load_text, filename);
+}
+
+// acl.go:121.
+inline RulesOrError GetL3ACLFromJSON(const std::string &filename) {
+    return detail::load(nffacl_rules_load_json, filename);
+}
+
+// Slot width handed to the GPU: the verdict reads wire bytes 12..77, so 80
+// bytes keep IPv4 headers with IHL up to 15 exact.
+constexpr uint32_t kSlot = 80;
+
+// A packet as the ACL sees it: the frame bytes starting at the Ethernet
+// header (packet.go:207-218 Ether pointer + data length).
+struct Packet {
+    const uint8_t *Ether = nullptr;
+    uint32_t Len = 0;
+
+    uint32_t L3ACLPort(const L3Rules &rules) const;   // acl.go:504
+    bool L3ACLPermit(const L3Rules &rules) const {    // acl.go:495
+        return L3ACLPort(rules) > 0;
+    }
+};
+
+// Classify n packets in one GPU call (host staging inside libnffacl).
+inline void L3ACLPortBatch(const Packet *const *pkts, size_t n, uint32_t *ports, const L3Rules &rules) {
+    if (n == 0) return;
+    std::vector<uint8_t> slots(n * kSlot, 0);
+    for (size_t i = 0; i < n; ++i) {
+        const uint32_t len = pkts[i]->Len < kSlot ? pkts[i]->Len : kSlot;
+        if (len) std::memcpy(&slots[i * kSlot], pkts[i]->Ether, len);
+    }
+    const int st = nffacl_classify_host(rules.engine(), slots.data(), kSlot, n, ports, nullptr);
+    if (st != NFFACL_OK)
+        throw std::runtime_error(std::string("nffacl_classify_host: ") + nffacl_strerror(st) + " " +
+                                 nffacl_last_error());
+}
+
+inline uint32_t Packet::L3ACLPort(const L3Rules &rules) const {
+    const Packet *p = this;
+    uint32_t port = 0;
+    L3ACLPortBatch(&p, 1, &port, rules);
+    return port;
+}
+
+}  // namespace packet
+
+namespace flow {
+
+constexpr int vBurstSize = 32;  // flow/flow.go:465-469
+
+// flow.go:131: VectorSeparateFunction(pkts, mask, answers, ctx)
+using VectorSeparateFunction =
+    std::function<void(packet::Packet *const *pkts, const bool *mask, bool *answers)>;
+using VectorSplitFunction =  // flow.go:139
+    std::function<void(packet::Packet *const *pkts, const bool *mask, uint8_t *answers)>;
+
+// The reference's vector separator over L3ACLPermit
+// (testSingleWorkingFF.go:538-546) as one GPU call per burst.
+inline VectorSeparateFunction ACLVectorSeparator(std::shared_ptr<const packet::L3Rules> rules) {
+    return [rules](packet::Packet *const *pkts, const bool *mask, bool *answers) {
+        const packet::Packet *sel[vBurstSize];
+        int idx[vBurstSize];
+        size_t n = 0;
+        for (int i = 0; i < vBurstSize; ++i)
+            if (mask[i] && pkts[i]) { sel[n] = pkts[i]; idx[n++] = i; }
+        uint32_t ports[vBurstSize] = {0};
+        packet::L3ACLPortBatch(sel, n, ports, *rules);
+        for (size_t k = 0; k < n; ++k) answers[idx[k]] = ports[k] > 0;
+    };
+}
+
+// vectorL3Splitter (testSingleWorkingFF.go:553-560): answers[i] = uint8(L3ACLPort).
+inline VectorSplitFunction ACLVectorSplitter(std::shared_ptr<const packet::L3Rules> rules) {
+    return [rules](packet::Packet *const *pkts, const bool *mask, uint8_t *answers) {
+        const packet::Packet *sel[vBurstSize];
+        int idx[vBurstSize];
+        size_t n = 0;
+        for (int i = 0; i < vBurstSize; ++i)
+            if (mask[i] && pkts[i]) { sel[n] = pkts[i]; idx[n++] = i; }
+        uint32_t ports[vBurstSize] = {0};
+        packet::L3ACLPortBatch(sel, n, ports, *rules);
+        for (size_t k = 0; k < n; ++k) answers[idx[k]] = static_cast<uint8_t>(ports[k]);
+    };
+}
+
+// Burst aggregator: bursts are appended into one slot buffer and classified
+// in a single GPU call per Flush() (or automatically once `capacity` packets
+// are queued); each burst's callback receives its verdicts in order.
+class Aggregator {
+public:
+    using Done = std::function<void(const uint32_t *ports, size_t n)>;
+    Aggregator(std::shared_ptr<const packet::L3Rules> rules, size_t capacity = 1 << 20)
+        : rules_(std::move(rules)), capacity_(capacity) {
+        slots_.reserve(capacity_ * packet::kSlot);
+    }
+    ~Aggregator() { Flush(); }
+
+    void Push(const packet::Packet *const *pkts, size_t n, Done done) {
+        if (queued_ + n > capacity_) Flush();
+        slots_.resize((queued_ + n) * packet::kSlot, 0);
+        for (size_t i = 0; i < n; ++i) {
+            uint8_t *dst = &slots_[(queued_ + i) * packet::kSlot];
+            std::memset(dst, 0, packet::kSlot);
+            const uint32_t len = pkts[i]->Len < packet::kSlot ? pkts[i]->Len : packet::kSlot;
+            if (len) std::memcpy(dst, pkts[i]->Ether, len);
+        }
+        bursts_.push_back({queued_, n, std::move(done)});
+        queued_ += n;
+    }
+
+    void Flush() {
+        if (queued_ == 0) return;
+        std::vector<uint32_t> ports(queued_);
+        const int st = nffacl_classify_host(rules_->engine(), slots_.data(), packet::kSlot, queued_,
+                                            ports.data(), nullptr);
+        if (st != NFFACL_OK) throw std::runtime_error("nffacl_classify_host failed");
+        for (auto &b : bursts_) b.done(ports.data() + b.first, b.n);
+        bursts_.clear();
+        slots_.clear();
+        queued_ = 0;
+    }
+
+private:
+    struct Burst {
+        size_t first, n;
+        Done done;
+    };
+    std::shared_ptr<const packet::L3Rules> rules_;
+    size_t capacity_;
+    size_t queued_ = 0;
+    std::vector<uint8_t> slots_;
+    std::vector<Burst> bursts_;
+};
+
+}  // namespace flow
+}  // namespace nffgo
