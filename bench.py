@@ -7,7 +7,10 @@ roofline.  One step = one classify launch (nffacl_classify_device, the HIP
 path) over the whole per-GPU batch of synthetic 64-byte slots already
 resident in HBM.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c1|c5] [--algo auto|linear|indexed]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c1|c3|c4|c5|l2] [--algo auto|linear|indexed]
+
+(`--config l2` measures the L2 ACL kernel, SURVEY.md §8f row 4 — not a
+BASELINE.json config: 256 GetL2ACLFromTextTable rules over 64 B slots.)
 
 N > 1 runs under torch.distributed.run (one rank per GPU, RCCL): rank 0
 generates the rule file and broadcasts its bytes over RCCL (the path's one real
@@ -39,6 +42,7 @@ sys.path.insert(0, str(ROOT))
 import numpy as np  # noqa: E402
 
 METRIC = "Mpackets/s device-resident L3 ACL classify, 64B pkts @1k rules; % HBM roofline"
+METRIC_L2 = "Mpackets/s device-resident L2 ACL classify, 64B pkts @256 rules (SURVEY.md §8f, not a BASELINE metric)"
 BYTES_PER_PACKET = 68  # 64 B slot read + 4 B verdict write
 HBM_PEAK_GBPS = 8000.0
 WORKLOADS = {
@@ -47,7 +51,11 @@ WORKLOADS = {
     "c3": "C3 10k-rule L3+L4 ACL, IMIX 64/570/1518 (7:4:1) packed frames, device-resident",
     "c4": "C4 1k-rule L3 ACL, 64B packets, packet batch sharded across GPUs",
     "c5": "C5 100k-rule L3+L4 ACL with port ranges, 64B packets, device-resident",
+    "l2": "L2 ACL (acl.go l2ACL), 256 MAC/EtherType rules, 64B packets, device-resident",
 }
+L2_RULES = 256
+# L2 reads the 16-byte line holding the Ethernet header and writes 4 B
+BYTES_PER_PACKET_L2 = 20
 # C3 reads each frame's first 64-byte line + its 8-byte descriptor and writes 4 B
 BYTES_PER_PACKET_FRAMES = 76
 
@@ -58,6 +66,9 @@ def log(*a):
 
 def build_rules(cfg: str):
     from nffacl import synth
+    if cfg == "l2":
+        g = synth.gen_l2_rules(L2_RULES)
+        return g.text, g
     if cfg == "c1":
         text = (ROOT / "tests" / "golden" / "rules" / "firewall.conf").read_text()
         return text, synth.firewall_rules(text)
@@ -78,8 +89,10 @@ def pmc_traffic(cfg: str, algo: str, n: int):
         return None
 
 
-def cpu_baseline(slots: np.ndarray, n: int, a4, a6, budget_s: float):
+def cpu_baseline(slots: np.ndarray, n: int, a4, a6, budget_s: float, eth=None):
     from oracle import oracle
+    if eth is not None:
+        return cpu_baseline_l2(slots, n, eth, budget_s)
     try:
         cores = len(os.sched_getaffinity(0))
     except AttributeError:
@@ -115,12 +128,45 @@ def cpu_baseline(slots: np.ndarray, n: int, a4, a6, budget_s: float):
     }, ports[:sample]
 
 
+def cpu_baseline_l2(slots: np.ndarray, n: int, eth, budget_s: float):
+    from oracle import oracle
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    cores = max(1, min(cores, 16))
+    cal = min(n, 1 << 16)
+    t = time.perf_counter()
+    oracle.l2_classify_slots(slots, 64, cal, eth, threads=cores)
+    rate = cal / max(time.perf_counter() - t, 1e-6)
+    sample = int(min(n, max(cal, rate * budget_s)))
+    passes, done, dt = 0, 0, 0.0
+    while True:
+        t = time.perf_counter()
+        ports = oracle.l2_classify_slots(slots, 64, sample, eth, threads=cores)
+        dt += time.perf_counter() - t
+        passes += 1
+        done += sample
+        if dt >= budget_s or passes >= 50:
+            break
+    one = min(sample, 1 << 16)
+    t1 = time.perf_counter()
+    oracle.l2_classify_slots(slots, 64, one, eth, threads=1)
+    dt1 = time.perf_counter() - t1
+    return {
+        "value": round(done / dt / 1e6, 3), "unit": "Mpps", "cores": cores, "kind": "port",
+        "sample": f"first {sample} packets x {passes} pass(es) (oracle/acl_oracle.c = acl.go l2ACL "
+                  f"restated in C, {cores} threads, {dt:.1f}s)",
+        "single_core_mpps": round(one / dt1 / 1e6, 3),
+    }, ports[:sample]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5"])
+    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "l2"])
     ap.add_argument("--algo", default="auto", choices=["auto", "linear", "indexed"])
     ap.add_argument("--packets", type=int, default=1 << 24, help="packets per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -150,10 +196,17 @@ def main():
     # ---- rules: rank 0 generates, RCCL broadcast of the rule file bytes ----
     text, gen = build_rules(cfg)
     text = nd.broadcast_rules(text if rank == 0 else None, dev)
-    rules = nffacl.L3Rules.parse_text(text)
-    n4, n6 = rules.counts()
-    eng = nffacl.Engine(rules, device=local, algo=algo_id)
-    algo_name = {nffacl.ALGO_LINEAR: "linear", nffacl.ALGO_INDEXED: "indexed"}[eng.algo]
+    l2_mode = cfg == "l2"
+    if l2_mode:
+        rules = nffacl.L2Rules.parse_text(text)
+        n4, n6 = rules.count(), 0
+        eng = nffacl.L2Engine(rules, device=local)
+        algo_name = "linear"
+    else:
+        rules = nffacl.L3Rules.parse_text(text)
+        n4, n6 = rules.counts()
+        eng = nffacl.Engine(rules, device=local, algo=algo_id)
+        algo_name = {nffacl.ALGO_LINEAR: "linear", nffacl.ALGO_INDEXED: "indexed"}[eng.algo]
 
     # ---- packets: per-rank shard, resident in HBM before timing ----
     from nffacl import synth
@@ -164,6 +217,9 @@ def main():
         d_frames = torch.from_numpy(frames).to(dev)
         d_desc = torch.from_numpy(desc.view(np.int64)).to(dev)
         slots = None
+    elif l2_mode:
+        slots = synth.gen_l2_slots(gen, n, synth.L2_PACKET_SEED + 7919 * rank)
+        d_slots = torch.from_numpy(slots).to(dev)
     else:
         slots = synth.gen_slots(gen, n, synth.PACKET_SEEDS[cfg] + 7919 * rank)
         d_slots = torch.from_numpy(slots).to(dev)
@@ -201,11 +257,18 @@ def main():
 
     # ---- spot parity check (outside timing): GPU verdicts vs oracle sample ----
     from oracle import oracle, rules_oracle as ro
-    a4, a6 = ro.parse_text_table(text.encode()).arrays()
     got = port.cpu().numpy().view(np.uint32)
     rng = np.random.default_rng(rank)
     idx = np.sort(rng.choice(n, min(n, 4096), replace=False))
-    if frames_mode:
+    eth = a4 = a6 = None
+    if l2_mode:
+        eth = ro.parse_l2_text_table(text.encode()).array()
+        want = oracle.l2_classify_slots(slots.reshape(n, 64)[idx].reshape(-1), 64, len(idx), eth, threads=4)
+    else:
+        a4, a6 = ro.parse_text_table(text.encode()).arrays()
+    if l2_mode:
+        pass
+    elif frames_mode:
         want = oracle.classify_frames(frames, desc[idx], a4, a6, threads=4)
     else:
         want = oracle.classify_slots(slots.reshape(n, 64)[idx].reshape(-1), 64, len(idx), a4, a6, threads=4)
@@ -214,10 +277,10 @@ def main():
     total = n * world * args.steps
     value = total / elapsed / 1e6
     mean_k = float(kms.mean()) / 1e3
-    bpp = BYTES_PER_PACKET_FRAMES if frames_mode else BYTES_PER_PACKET
+    bpp = BYTES_PER_PACKET_FRAMES if frames_mode else BYTES_PER_PACKET_L2 if l2_mode else BYTES_PER_PACKET
     achieved = bpp * n / mean_k / 1e9
     out = {
-        "metric": METRIC,
+        "metric": METRIC_L2 if l2_mode else METRIC,
         "value": round(value, 1),
         "unit": "Mpps",
         "n_gpus": world,
@@ -233,7 +296,7 @@ def main():
             "workload": WORKLOADS.get(cfg, cfg), "rules_ip4": n4, "rules_ip6": n6,
             "packets_per_gpu": n, "slot_bytes": None if frames_mode else 64,
             "algorithmic_bytes_per_packet": bpp, "algo": algo_name, "parallelism": f"dp{world}",
-            "table_bytes": eng.table_bytes,
+            "table_bytes": None if l2_mode else eng.table_bytes,
         },
         "roofline": {
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
@@ -257,7 +320,7 @@ def main():
         out["host_inclusive_bit_exact_sample"] = bool((hp[idx[idx < m]] == got[idx[idx < m]]).all())
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not frames_mode:
-        cb, cports = cpu_baseline(slots, n, a4, a6, args.cpu_seconds)
+        cb, cports = cpu_baseline(slots, n, a4, a6, args.cpu_seconds, eth)
         cb["bit_exact_vs_gpu"] = bool((cports == got[: len(cports)]).all())
         out["cpu_baseline"] = cb
     elif rank == 0:

@@ -27,6 +27,13 @@
  *                                  — host slots in, verdicts out, PCIe staging inside
  *   nffacl_engine_swap_rules    <- the atomic *L3Rules pointer swap user code performs
  *                                  on rule reload (examples/tutorial/step08.go:33-44)
+ *   nffacl_batcher_*            <- the per-burst VectorSeparateFunction calls of every
+ *                                  flow-function clone (flow/flow.go:131, 1487-1520),
+ *                                  aggregated across threads into shared GPU batches
+ *   nffacl_l2rules_load_text    <- packet.GetL2ACLFromTextTable   packet/acl.go:88-117
+ *   nffacl_l2rules_load_json    <- packet.GetL2ACLFromJSON        packet/acl.go:70-84
+ *   nffacl_l2_classify_device   <- (*Packet).L2ACLPort / L2ACLPermit  acl.go:462-491
+ *                                  (l2ACL acl.go:478-491) over a batch in HBM
  *
  * Verdict semantics (bit-exact with acl.go):
  *   port  = OutputNumber of the FIRST rule (file order, per address family) that
@@ -55,7 +62,7 @@
 extern "C" {
 #endif
 
-#define NFFACL_ABI_VERSION 1
+#define NFFACL_ABI_VERSION 2
 
 /* Only the entry points below are exported from libnffacl.so (built with
  * -fvisibility=hidden). */
@@ -225,6 +232,101 @@ NFFACL_API int nffacl_classify_frames_device(nffacl_engine *eng, const uint8_t *
  * (h_permit gets one byte per packet, 0 or 1). */
 NFFACL_API int nffacl_classify_host(nffacl_engine *eng, const uint8_t *h_slots, uint32_t stride,
                          uint64_t n, uint32_t *h_port, uint8_t *h_permit);
+
+/* ---- burst aggregator (host ingest) ----------------
+ *
+ * Many threads (the reference's flow-function clones, each with a burst of
+ * <= 32 packets) submit bursts; the library copies each packet's first
+ * `stride` bytes into a shared pinned slot ring, ships a batch to the GPU when
+ * `max_batch` packets are queued or the oldest queued burst has waited
+ * `max_delay_us`, and wakes every submitter of that batch when its verdicts
+ * are back.  Thread-safe: any number of concurrent submitters per batcher.
+ */
+typedef struct nffacl_batcher nffacl_batcher;
+
+typedef struct nffacl_ticket {
+    uint64_t seq;
+    uint32_t buf, off, n, reserved;
+} nffacl_ticket;
+
+typedef struct nffacl_batcher_stats {
+    uint64_t batches;  /* GPU launches */
+    uint64_t packets;  /* packets classified */
+    uint64_t bursts;   /* submit calls */
+    uint64_t timeouts; /* batches shipped by max_delay_us rather than full */
+} nffacl_batcher_stats;
+
+/* stride: slot bytes per packet (multiple of 16, >= 64; 80 keeps IPv4 with IHL
+ * 15 exact); max_batch: packets per GPU launch (>= 64); nbuf: batch buffers in
+ * rotation (>= 2).  The engine must outlive the batcher. */
+NFFACL_API int nffacl_batcher_create(nffacl_engine *eng, uint32_t stride, uint32_t max_batch,
+                                     uint32_t max_delay_us, uint32_t nbuf, nffacl_batcher **out);
+/* Queue a burst: frames[i] points at packet i's Ether header, lens[i] its
+ * bytes (NULL lens: `stride` bytes each; bytes past a length read as 0).
+ * n <= max_batch.  Returns without waiting; *ticket identifies the burst. */
+NFFACL_API int nffacl_batcher_submit(nffacl_batcher *b, const uint8_t *const *frames, const uint32_t *lens,
+                                     uint32_t n, nffacl_ticket *ticket);
+/* Block until the burst's batch is classified; ports[i] <- L3ACLPort of packet i. */
+NFFACL_API int nffacl_batcher_wait(nffacl_batcher *b, const nffacl_ticket *ticket, uint32_t *ports);
+/* submit + wait: the body of a VectorSeparateFunction. */
+NFFACL_API int nffacl_batcher_classify(nffacl_batcher *b, const uint8_t *const *frames, const uint32_t *lens,
+                                       uint32_t n, uint32_t *ports);
+/* Ship the currently open batch now (do not wait for max_batch / max_delay_us). */
+NFFACL_API int nffacl_batcher_flush(nffacl_batcher *b);
+NFFACL_API int nffacl_batcher_get_stats(nffacl_batcher *b, nffacl_batcher_stats *out);
+/* Drains queued bursts, then frees; no submit/wait may be running. */
+NFFACL_API void nffacl_batcher_destroy(nffacl_batcher *b);
+
+/* ---- L2 ACL (packet/acl.go:68-117, 356-383, 413-421, 457-491) ----------- */
+
+/* l2Rules, acl.go:413-421.  MAC addresses in wire order; `id` is the EtherType
+ * as a host-order number (types.IPV4Number = 0x0800 ...), compared with the
+ * frame's big-endian EtherType under `id_mask` (0 = ANY, 0xffff = exact). */
+typedef struct nffacl_l2_rule {
+    uint32_t output_number;
+    uint8_t daddr_not_any; /* 1: daddr must equal Ether.DAddr (frame bytes 0..5) */
+    uint8_t saddr_not_any; /* 1: saddr must equal Ether.SAddr (frame bytes 6..11) */
+    uint8_t daddr[6];
+    uint8_t saddr[6];
+    uint16_t id_mask;
+    uint16_t id;
+    uint16_t reserved; /* must be 0 */
+} nffacl_l2_rule; /* 24 bytes */
+
+typedef struct nffacl_l2rules nffacl_l2rules;
+typedef struct nffacl_l2engine nffacl_l2engine;
+
+/* GetL2ACLFromTextTable (acl.go:88): "SrcMAC DstMAC ID [Rule]" per line. */
+NFFACL_API int nffacl_l2rules_load_text(const char *path, nffacl_l2rules **out, char *err, size_t errlen);
+NFFACL_API int nffacl_l2rules_parse_text(const char *text, size_t len, nffacl_l2rules **out, char *err,
+                                         size_t errlen);
+/* GetL2ACLFromJSON (acl.go:70): {"L2Rules": [{"Source", "Destination", "ID", "Rule"}]}. */
+NFFACL_API int nffacl_l2rules_load_json(const char *path, nffacl_l2rules **out, char *err, size_t errlen);
+NFFACL_API int nffacl_l2rules_parse_json(const char *text, size_t len, nffacl_l2rules **out, char *err,
+                                         size_t errlen);
+/* L2Rules{eth: ...} literal (acl_internal_test.go:1186-1193); copied. */
+NFFACL_API int nffacl_l2rules_from_array(const nffacl_l2_rule *r, size_t n, nffacl_l2rules **out);
+NFFACL_API void nffacl_l2rules_free(nffacl_l2rules *rules);
+NFFACL_API int nffacl_l2rules_count(const nffacl_l2rules *rules, size_t *n);
+NFFACL_API int nffacl_l2rules_get(const nffacl_l2rules *rules, size_t i, nffacl_l2_rule *out);
+
+NFFACL_API int nffacl_l2_engine_create(int hip_device, const nffacl_l2rules *rules, nffacl_l2engine **out);
+NFFACL_API int nffacl_l2_engine_swap_rules(nffacl_l2engine *eng, const nffacl_l2rules *rules);
+NFFACL_API void nffacl_l2_engine_destroy(nffacl_l2engine *eng);
+
+/* L2ACLPort / L2ACLPermit over device-resident slots / packed frames; same
+ * buffer conventions as nffacl_classify_device / _frames_device (only frame
+ * bytes 0..13 are read; bytes past a frame's length read as 0). */
+NFFACL_API int nffacl_l2_classify_device(nffacl_l2engine *eng, const uint8_t *d_slots, uint32_t stride,
+                                         uint64_t n, uint32_t *d_port, uint64_t *d_permit_bits,
+                                         void *stream);
+NFFACL_API int nffacl_l2_classify_frames_device(nffacl_l2engine *eng, const uint8_t *d_frames,
+                                                const uint64_t *d_desc, uint64_t n, uint32_t *d_port,
+                                                uint64_t *d_permit_bits, void *stream);
+/* Host slots in, host verdicts out (synchronous; staging inside, sized to the
+ * request).  h_port / h_permit (one byte per packet) may be NULL. */
+NFFACL_API int nffacl_l2_classify_host(nffacl_l2engine *eng, const uint8_t *h_slots, uint32_t stride,
+                                       uint64_t n, uint32_t *h_port, uint8_t *h_permit);
 
 /* ---- misc ------------------------------------------------------------- */
 NFFACL_API const char *nffacl_strerror(int status);

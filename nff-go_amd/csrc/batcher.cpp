@@ -1,0 +1,268 @@
+// batcher.cpp — nffacl_batcher: multi-producer burst aggregation onto the GPU
+// (see batcher.hpp).  One launcher thread seals and ships batches in ring
+// order; one completer thread waits on their events in launch order and wakes
+// the bursts' submitters.
+#include "batcher.hpp"
+
+#include <algorithm>
+#include <cstring>
+#include <new>
+#include <string>
+
+#include "devutil.hpp"
+
+using namespace nffacl;
+using Clock = std::chrono::steady_clock;
+
+namespace {
+
+void release_buffers(nffacl_batcher *b) {
+    if (!b->bufs) return;
+    for (uint32_t i = 0; i < b->nbuf; ++i) {
+        BatchBuf &x = b->bufs[i];
+        if (x.h_slots) (void)hipHostFree(x.h_slots);
+        if (x.h_port) (void)hipHostFree(x.h_port);
+        if (x.d_slots) (void)hipFree(x.d_slots);
+        if (x.d_port) (void)hipFree(x.d_port);
+        if (x.stream) (void)hipStreamDestroy(x.stream);
+        if (x.done) (void)hipEventDestroy(x.done);
+    }
+}
+
+// Under b->mu.  Seal the open buffer and move producers to the next one.
+void seal_open(nffacl_batcher *b) {
+    b->bufs[b->open_idx].state = BatchBuf::SEALED;
+    b->open_idx = (b->open_idx + 1) % b->nbuf;
+    b->cv_work.notify_one();
+    b->cv_free.notify_all();  // producers parked on the old open_idx re-check
+}
+
+// Under b->mu: ship bufs[launch_idx] (SEALED).  Drops the lock while copying.
+void launch_one(nffacl_batcher *b, std::unique_lock<std::mutex> &lk) {
+    const uint32_t i = b->launch_idx;
+    BatchBuf &x = b->bufs[i];
+    const uint32_t n = x.count;
+    b->launch_idx = (i + 1) % b->nbuf;
+    lk.unlock();
+    while (x.written.load(std::memory_order_acquire) < n) std::this_thread::yield();  // copies in progress
+    int st = NFFACL_OK;
+    hipError_t e = hipMemcpyAsync(x.d_slots, x.h_slots, size_t(n) * b->stride, hipMemcpyHostToDevice, x.stream);
+    if (e == hipSuccess) {
+        st = launch_slots(b->eng, acquire_table(b->eng), x.d_slots, b->stride, n, x.d_port, nullptr, x.stream);
+        if (st == NFFACL_OK) e = hipMemcpyAsync(x.h_port, x.d_port, size_t(n) * 4, hipMemcpyDeviceToHost, x.stream);
+        if (st == NFFACL_OK && e == hipSuccess) e = hipEventRecord(x.done, x.stream);
+    }
+    lk.lock();
+    if (e != hipSuccess || st != NFFACL_OK) {
+        if (e != hipSuccess) set_last_error(std::string("batcher launch: ") + hipGetErrorString(e));
+        b->error = st != NFFACL_OK ? st : NFFACL_ERR_HIP;
+        x.state = BatchBuf::DONE;  // wake the waiters with the error
+        b->cv_done.notify_all();
+        return;
+    }
+    x.state = BatchBuf::LAUNCHED;
+    ++b->batches;
+    b->packets += n;
+    b->inflight.push_back(i);
+    b->cv_inflight.notify_one();
+}
+
+void launcher_main(nffacl_batcher *b) {
+    (void)hipSetDevice(b->eng->device);
+    std::unique_lock<std::mutex> lk(b->mu);
+    while (true) {
+        BatchBuf &x = b->bufs[b->launch_idx];
+        if (x.state == BatchBuf::SEALED) {
+            launch_one(b, lk);
+            continue;
+        }
+        if (x.state == BatchBuf::OPEN && x.count > 0) {
+            const auto deadline = x.opened + b->max_delay;
+            if (b->stop || Clock::now() >= deadline) {
+                if (!b->stop) ++b->timeouts;
+                seal_open(b);  // open_idx == launch_idx here
+                continue;
+            }
+            b->cv_work.wait_until(lk, deadline);
+            continue;
+        }
+        if (b->stop) break;
+        b->cv_work.wait(lk);
+    }
+    b->launcher_done = true;
+    b->cv_inflight.notify_all();
+}
+
+void completer_main(nffacl_batcher *b) {
+    (void)hipSetDevice(b->eng->device);
+    std::unique_lock<std::mutex> lk(b->mu);
+    while (true) {
+        b->cv_inflight.wait(lk, [&] { return !b->inflight.empty() || b->launcher_done; });
+        if (b->inflight.empty()) break;
+        const uint32_t i = b->inflight.front();
+        lk.unlock();
+        const hipError_t e = hipEventSynchronize(b->bufs[i].done);
+        lk.lock();
+        b->inflight.pop_front();
+        if (e != hipSuccess) {
+            set_last_error(std::string("batcher completion: ") + hipGetErrorString(e));
+            b->error = NFFACL_ERR_HIP;
+        }
+        BatchBuf &x = b->bufs[i];
+        x.state = BatchBuf::DONE;
+        if (x.readers == 0) {
+            x.state = BatchBuf::FREE;
+            b->cv_free.notify_all();
+        }
+        b->cv_done.notify_all();
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int nffacl_batcher_create(nffacl_engine *eng, uint32_t stride, uint32_t max_batch, uint32_t max_delay_us,
+                          uint32_t nbuf, nffacl_batcher **out) {
+    if (!eng || !out || stride < 64 || stride % 16 != 0 || max_batch < 64 || nbuf < 2) return NFFACL_ERR_INVALID_ARG;
+    *out = nullptr;
+    HIP_TRY(hipSetDevice(eng->device));
+    nffacl_batcher *b = new (std::nothrow) nffacl_batcher();
+    if (!b) return NFFACL_ERR_NOMEM;
+    b->eng = eng;
+    b->stride = stride;
+    b->max_batch = max_batch;
+    b->max_delay = std::chrono::microseconds(max_delay_us);
+    b->nbuf = nbuf;
+    b->bufs.reset(new (std::nothrow) BatchBuf[nbuf]);
+    if (!b->bufs) {
+        delete b;
+        return NFFACL_ERR_NOMEM;
+    }
+    for (uint32_t i = 0; i < nbuf; ++i) {
+        BatchBuf &x = b->bufs[i];
+        hipError_t e = hipHostMalloc(reinterpret_cast<void **>(&x.h_slots), size_t(max_batch) * stride, hipHostMallocDefault);
+        if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&x.h_port), size_t(max_batch) * 4, hipHostMallocDefault);
+        if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&x.d_slots), size_t(max_batch) * stride);
+        if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&x.d_port), size_t(max_batch) * 4);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&x.stream, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&x.done, hipEventDisableTiming);
+        if (e != hipSuccess) {
+            set_last_error(std::string("batcher buffers: ") + hipGetErrorString(e));
+            release_buffers(b);
+            delete b;
+            return NFFACL_ERR_HIP;
+        }
+    }
+    b->launcher = std::thread(launcher_main, b);
+    b->completer = std::thread(completer_main, b);
+    *out = b;
+    return NFFACL_OK;
+}
+
+int nffacl_batcher_submit(nffacl_batcher *b, const uint8_t *const *frames, const uint32_t *lens, uint32_t n,
+                          nffacl_ticket *ticket) {
+    if (!b || !ticket || (n && !frames) || n > b->max_batch) return NFFACL_ERR_INVALID_ARG;
+    *ticket = nffacl_ticket{0, 0, 0, 0, 0};
+    if (n == 0) return NFFACL_OK;
+    std::unique_lock<std::mutex> lk(b->mu);
+    BatchBuf *x = nullptr;
+    uint32_t off = 0;
+    while (true) {
+        if (b->error != NFFACL_OK) return b->error;
+        if (b->stop) return NFFACL_ERR_INVALID_ARG;
+        BatchBuf &cur = b->bufs[b->open_idx];
+        if (cur.state == BatchBuf::FREE) {
+            cur.state = BatchBuf::OPEN;
+            cur.seq = b->next_seq++;
+            cur.count = 0;
+            cur.readers = 0;
+            cur.written.store(0, std::memory_order_relaxed);
+        } else if (cur.state != BatchBuf::OPEN) {
+            b->cv_free.wait(lk);  // every buffer in flight: back-pressure
+            continue;
+        }
+        if (cur.count + n > b->max_batch) {
+            seal_open(b);
+            continue;
+        }
+        x = &cur;
+        off = cur.count;
+        if (off == 0) cur.opened = Clock::now();
+        cur.count += n;
+        ++cur.readers;
+        ++b->bursts;
+        *ticket = nffacl_ticket{cur.seq, b->open_idx, off, n, 0};
+        if (cur.count == b->max_batch) seal_open(b);
+        else if (off == 0) b->cv_work.notify_one();  // start the max_delay clock
+        break;
+    }
+    lk.unlock();
+    uint8_t *dst = x->h_slots + size_t(off) * b->stride;
+    for (uint32_t i = 0; i < n; ++i, dst += b->stride) {
+        const uint32_t len = lens ? std::min(lens[i], b->stride) : b->stride;
+        if (len) std::memcpy(dst, frames[i], len);
+        if (len < b->stride) std::memset(dst + len, 0, b->stride - len);
+    }
+    x->written.fetch_add(n, std::memory_order_release);
+    return NFFACL_OK;
+}
+
+int nffacl_batcher_wait(nffacl_batcher *b, const nffacl_ticket *t, uint32_t *ports) {
+    if (!b || !t) return NFFACL_ERR_INVALID_ARG;
+    if (t->n == 0) return NFFACL_OK;
+    if (t->buf >= b->nbuf) return NFFACL_ERR_INVALID_ARG;
+    std::unique_lock<std::mutex> lk(b->mu);
+    BatchBuf &x = b->bufs[t->buf];
+    if (x.seq != t->seq || x.state == BatchBuf::FREE) return NFFACL_ERR_INVALID_ARG;
+    b->cv_done.wait(lk, [&] { return x.state == BatchBuf::DONE; });
+    const int st = b->error;
+    lk.unlock();
+    if (ports && st == NFFACL_OK) std::memcpy(ports, x.h_port + t->off, size_t(t->n) * 4);
+    lk.lock();
+    if (--x.readers == 0) {
+        x.state = BatchBuf::FREE;
+        b->cv_free.notify_all();
+    }
+    return st;
+}
+
+int nffacl_batcher_classify(nffacl_batcher *b, const uint8_t *const *frames, const uint32_t *lens, uint32_t n,
+                            uint32_t *ports) {
+    nffacl_ticket t;
+    const int st = nffacl_batcher_submit(b, frames, lens, n, &t);
+    if (st != NFFACL_OK) return st;
+    return nffacl_batcher_wait(b, &t, ports);
+}
+
+int nffacl_batcher_flush(nffacl_batcher *b) {
+    if (!b) return NFFACL_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> g(b->mu);
+    BatchBuf &cur = b->bufs[b->open_idx];
+    if (cur.state == BatchBuf::OPEN && cur.count > 0) seal_open(b);
+    return b->error;
+}
+
+int nffacl_batcher_get_stats(nffacl_batcher *b, nffacl_batcher_stats *out) {
+    if (!b || !out) return NFFACL_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> g(b->mu);
+    *out = nffacl_batcher_stats{b->batches, b->packets, b->bursts, b->timeouts};
+    return NFFACL_OK;
+}
+
+void nffacl_batcher_destroy(nffacl_batcher *b) {
+    if (!b) return;
+    {
+        std::lock_guard<std::mutex> g(b->mu);
+        b->stop = true;
+        b->cv_work.notify_all();
+        b->cv_free.notify_all();
+    }
+    if (b->launcher.joinable()) b->launcher.join();
+    if (b->completer.joinable()) b->completer.join();
+    (void)hipSetDevice(b->eng->device);
+    release_buffers(b);
+    delete b;
+}
+
+}  // extern "C"

@@ -1,0 +1,77 @@
+// batcher.hpp — multi-producer burst aggregator behind nffacl_batcher (internal).
+//
+// The reference classifies inside each flow-function clone, one burst of <= 32
+// packets at a time (segmentProcess, flow/flow.go:1487-1520, calling the
+// VectorSeparateFunction of flow.go:131).  A GPU launch per burst is latency
+// bound, so the batcher lets every clone (thread) submit its burst into a
+// shared pinned slot ring; one launcher thread ships a batch to the GPU when it
+// is full or its oldest burst has waited `max_delay_us`, and each clone blocks
+// only until its own batch's verdicts are back.
+//
+// Buffers: `nbuf` batch buffers, each = pinned slots + pinned ports on the host,
+// slots + ports in HBM, a stream and an event.  States cycle
+//   FREE -> OPEN (accepting bursts) -> SEALED -> LAUNCHED -> DONE -> FREE
+// (DONE -> FREE once every burst of the batch has collected its verdicts).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdint>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "engine.hpp"
+#include "nffacl.h"
+
+namespace nffacl {
+
+struct BatchBuf {
+    enum State { FREE, OPEN, SEALED, LAUNCHED, DONE };
+    State state = FREE;
+    uint64_t seq = 0;       // batch sequence number while not FREE
+    uint32_t count = 0;     // packets reserved
+    uint32_t readers = 0;   // bursts that have not collected their verdicts yet
+    std::atomic<uint32_t> written{0};  // packets whose bytes are in h_slots
+    std::chrono::steady_clock::time_point opened;
+    uint8_t *h_slots = nullptr;
+    uint32_t *h_port = nullptr;
+    uint8_t *d_slots = nullptr;
+    uint32_t *d_port = nullptr;
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;
+};
+
+}  // namespace nffacl
+
+struct nffacl_batcher {
+    nffacl_engine *eng = nullptr;
+    uint32_t stride = 64;
+    uint32_t max_batch = 0;
+    std::chrono::microseconds max_delay{100};
+    uint32_t nbuf = 0;
+    std::unique_ptr<nffacl::BatchBuf[]> bufs;
+
+    std::mutex mu;
+    std::condition_variable cv_work;  // launcher: a batch sealed / opened
+    std::condition_variable cv_free;  // producers: a buffer became FREE
+    std::condition_variable cv_done;  // waiters: a batch finished
+    uint32_t open_idx = 0;            // buffer producers append to
+    uint32_t launch_idx = 0;          // next buffer the launcher ships
+    uint64_t next_seq = 1;
+    bool stop = false;
+    bool launcher_done = false;
+    int error = NFFACL_OK;            // sticky launch error
+
+    std::deque<uint32_t> inflight;    // launched buffers, FIFO
+    std::condition_variable cv_inflight;
+    std::thread launcher, completer;
+
+    // stats
+    uint64_t batches = 0, packets = 0, bursts = 0, timeouts = 0;
+};

@@ -11,7 +11,9 @@
 #include <string>
 #include <vector>
 
+#include "devutil.hpp"
 #include "engine.hpp"
+#include "l2.hpp"
 #include "nffacl.h"
 #include "compile.hpp"
 #include "rules.hpp"
@@ -27,8 +29,8 @@ void copy_err(char *dst, size_t len, const std::string &msg) {
     dst[n] = '\0';
 }
 
-int finish_parse(bool ok, nffacl_rules *r, const ParseError &pe, nffacl_rules **out, char *err,
-                 size_t errlen) {
+template <class R>
+int finish_parse(bool ok, R *r, const ParseError &pe, R **out, char *err, size_t errlen) {
     if (!ok) {
         delete r;
         *out = nullptr;
@@ -60,8 +62,8 @@ bool read_file(const char *path, std::vector<char> &buf, std::string &msg) {
     return true;
 }
 
-template <class Parser>
-int load_with(const char *path, nffacl_rules **out, char *err, size_t errlen, Parser parser) {
+template <class R, class Parser>
+int load_with(const char *path, R **out, char *err, size_t errlen, Parser parser) {
     if (!path || !out) return NFFACL_ERR_INVALID_ARG;
     *out = nullptr;
     std::vector<char> buf;
@@ -72,10 +74,20 @@ int load_with(const char *path, nffacl_rules **out, char *err, size_t errlen, Pa
         set_last_error(msg);
         return NFFACL_ERR_FILE;
     }
-    nffacl_rules *r = new (std::nothrow) nffacl_rules();
+    R *r = new (std::nothrow) R();
     if (!r) return NFFACL_ERR_NOMEM;
     ParseError pe;
     bool ok = parser(buf.data(), buf.size(), *r, pe);
+    return finish_parse(ok, r, pe, out, err, errlen);
+}
+
+template <class R, class Parser>
+int parse_with(const char *text, size_t len, R **out, char *err, size_t errlen, Parser parser) {
+    if (!out || (!text && len)) return NFFACL_ERR_INVALID_ARG;
+    R *r = new (std::nothrow) R();
+    if (!r) return NFFACL_ERR_NOMEM;
+    ParseError pe;
+    bool ok = parser(text ? text : "", len, *r, pe);
     return finish_parse(ok, r, pe, out, err, errlen);
 }
 
@@ -90,14 +102,7 @@ bool pointer_is_pinned(const void *p) {
 
 }  // namespace
 
-#define HIP_CHECK(expr)                                                                  \
-    do {                                                                                 \
-        hipError_t e_ = (expr);                                                          \
-        if (e_ != hipSuccess) {                                                          \
-            set_last_error(std::string(#expr) + ": " + hipGetErrorString(e_));            \
-            return NFFACL_ERR_HIP;                                                       \
-        }                                                                                \
-    } while (0)
+#define HIP_CHECK HIP_TRY
 
 extern "C" {
 
@@ -130,12 +135,7 @@ int nffacl_rules_load_text(const char *path, nffacl_rules **out, char *err, size
 
 int nffacl_rules_parse_text(const char *text, size_t len, nffacl_rules **out, char *err,
                             size_t errlen) {
-    if (!out || (!text && len)) return NFFACL_ERR_INVALID_ARG;
-    nffacl_rules *r = new (std::nothrow) nffacl_rules();
-    if (!r) return NFFACL_ERR_NOMEM;
-    ParseError pe;
-    bool ok = parse_text_table(text ? text : "", len, *r, pe);
-    return finish_parse(ok, r, pe, out, err, errlen);
+    return parse_with(text, len, out, err, errlen, parse_text_table);
 }
 
 int nffacl_rules_load_json(const char *path, nffacl_rules **out, char *err, size_t errlen) {
@@ -144,12 +144,7 @@ int nffacl_rules_load_json(const char *path, nffacl_rules **out, char *err, size
 
 int nffacl_rules_parse_json(const char *text, size_t len, nffacl_rules **out, char *err,
                             size_t errlen) {
-    if (!out || (!text && len)) return NFFACL_ERR_INVALID_ARG;
-    nffacl_rules *r = new (std::nothrow) nffacl_rules();
-    if (!r) return NFFACL_ERR_NOMEM;
-    ParseError pe;
-    bool ok = parse_json(text ? text : "", len, *r, pe);
-    return finish_parse(ok, r, pe, out, err, errlen);
+    return parse_with(text, len, out, err, errlen, parse_json);
 }
 
 int nffacl_rules_from_arrays(const nffacl_rule4 *r4, size_t n4, const nffacl_rule6 *r6, size_t n6,
@@ -308,11 +303,6 @@ int nffacl_engine_table_bytes(const nffacl_engine *eng, uint64_t *bytes) {
 
 // ---- classification ---------------------------------------------------------
 
-static DevTable *acquire_table(nffacl_engine *eng) {
-    std::lock_guard<std::mutex> g(eng->table_mu);
-    return eng->active;
-}
-
 int nffacl_classify_device(nffacl_engine *eng, const uint8_t *d_slots, uint32_t stride, uint64_t n,
                            uint32_t *d_port, uint64_t *d_permit_bits, void *stream) {
     if (!eng) return NFFACL_ERR_INVALID_ARG;
@@ -411,6 +401,174 @@ int nffacl_classify_host(nffacl_engine *eng, const uint8_t *h_slots, uint32_t st
     }
     for (int b = 0; b < 2; ++b)
         if ((st = drain(b)) != NFFACL_OK) return st;
+    return NFFACL_OK;
+}
+
+// ---- L2 ACL -------------------------------------------------------------------
+
+int nffacl_l2rules_load_text(const char *path, nffacl_l2rules **out, char *err, size_t errlen) {
+    return load_with(path, out, err, errlen, parse_l2_text_table);
+}
+
+int nffacl_l2rules_parse_text(const char *text, size_t len, nffacl_l2rules **out, char *err, size_t errlen) {
+    return parse_with(text, len, out, err, errlen, parse_l2_text_table);
+}
+
+int nffacl_l2rules_load_json(const char *path, nffacl_l2rules **out, char *err, size_t errlen) {
+    return load_with(path, out, err, errlen, parse_l2_json);
+}
+
+int nffacl_l2rules_parse_json(const char *text, size_t len, nffacl_l2rules **out, char *err, size_t errlen) {
+    return parse_with(text, len, out, err, errlen, parse_l2_json);
+}
+
+int nffacl_l2rules_from_array(const nffacl_l2_rule *r, size_t n, nffacl_l2rules **out) {
+    if (!out || (!r && n)) return NFFACL_ERR_INVALID_ARG;
+    nffacl_l2rules *x = new (std::nothrow) nffacl_l2rules();
+    if (!x) return NFFACL_ERR_NOMEM;
+    x->eth.assign(r, r + n);
+    *out = x;
+    return NFFACL_OK;
+}
+
+void nffacl_l2rules_free(nffacl_l2rules *rules) { delete rules; }
+
+int nffacl_l2rules_count(const nffacl_l2rules *rules, size_t *n) {
+    if (!rules || !n) return NFFACL_ERR_INVALID_ARG;
+    *n = rules->eth.size();
+    return NFFACL_OK;
+}
+
+int nffacl_l2rules_get(const nffacl_l2rules *rules, size_t i, nffacl_l2_rule *out) {
+    if (!rules || !out || i >= rules->eth.size()) return NFFACL_ERR_INVALID_ARG;
+    *out = rules->eth[i];
+    return NFFACL_OK;
+}
+
+int nffacl_l2_engine_create(int hip_device, const nffacl_l2rules *rules, nffacl_l2engine **out) {
+    if (!rules || !out) return NFFACL_ERR_INVALID_ARG;
+    *out = nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
+        (void)hipGetLastError();
+        set_last_error("no HIP device visible");
+        return NFFACL_ERR_NO_DEVICE;
+    }
+    if (hip_device < 0 || hip_device >= count) return NFFACL_ERR_INVALID_ARG;
+    HIP_CHECK(hipSetDevice(hip_device));
+    nffacl_l2engine *eng = new (std::nothrow) nffacl_l2engine();
+    if (!eng) return NFFACL_ERR_NOMEM;
+    eng->device = hip_device;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, hip_device) == hipSuccess && cus > 0)
+        eng->num_cus = cus;
+    L2Table *t = nullptr;
+    int st = upload_l2(hip_device, *rules, t);
+    if (st != NFFACL_OK) {
+        delete eng;
+        return st;
+    }
+    eng->active = t;
+    *out = eng;
+    return NFFACL_OK;
+}
+
+int nffacl_l2_engine_swap_rules(nffacl_l2engine *eng, const nffacl_l2rules *rules) {
+    if (!eng || !rules) return NFFACL_ERR_INVALID_ARG;
+    L2Table *t = nullptr;
+    int st = upload_l2(eng->device, *rules, t);
+    if (st != NFFACL_OK) return st;
+    L2Table *old_retired = nullptr;
+    {
+        std::lock_guard<std::mutex> g(eng->table_mu);
+        old_retired = eng->retired;
+        eng->retired = eng->active;
+        eng->active = t;
+    }
+    if (old_retired) {
+        HIP_CHECK(hipSetDevice(eng->device));
+        HIP_CHECK(hipDeviceSynchronize());
+        delete old_retired;
+    }
+    return NFFACL_OK;
+}
+
+void nffacl_l2_engine_destroy(nffacl_l2engine *eng) {
+    if (!eng) return;
+    (void)hipSetDevice(eng->device);
+    (void)hipDeviceSynchronize();
+    delete eng->active;
+    delete eng->retired;
+    if (eng->d_slots) (void)hipFree(eng->d_slots);
+    if (eng->d_port) (void)hipFree(eng->d_port);
+    if (eng->stream) (void)hipStreamDestroy(eng->stream);
+    delete eng;
+}
+
+static L2Table *acquire_l2(nffacl_l2engine *eng) {
+    std::lock_guard<std::mutex> g(eng->table_mu);
+    return eng->active;
+}
+
+int nffacl_l2_classify_device(nffacl_l2engine *eng, const uint8_t *d_slots, uint32_t stride, uint64_t n,
+                              uint32_t *d_port, uint64_t *d_permit_bits, void *stream) {
+    if (!eng) return NFFACL_ERR_INVALID_ARG;
+    if (n == 0) return NFFACL_OK;
+    if (!d_slots || stride < 64 || (stride % 16) != 0 || (reinterpret_cast<uintptr_t>(d_slots) % 16) != 0)
+        return NFFACL_ERR_INVALID_ARG;
+    if (!d_port && !d_permit_bits) return NFFACL_OK;
+    HIP_CHECK(hipSetDevice(eng->device));
+    return l2_launch_slots(eng, acquire_l2(eng), d_slots, stride, n, d_port, d_permit_bits,
+                           static_cast<hipStream_t>(stream));
+}
+
+int nffacl_l2_classify_frames_device(nffacl_l2engine *eng, const uint8_t *d_frames, const uint64_t *d_desc,
+                                     uint64_t n, uint32_t *d_port, uint64_t *d_permit_bits, void *stream) {
+    if (!eng) return NFFACL_ERR_INVALID_ARG;
+    if (n == 0) return NFFACL_OK;
+    if (!d_frames || !d_desc || (reinterpret_cast<uintptr_t>(d_frames) % 16) != 0) return NFFACL_ERR_INVALID_ARG;
+    if (!d_port && !d_permit_bits) return NFFACL_OK;
+    HIP_CHECK(hipSetDevice(eng->device));
+    return l2_launch_frames(eng, acquire_l2(eng), d_frames, d_desc, n, d_port, d_permit_bits,
+                            static_cast<hipStream_t>(stream));
+}
+
+int nffacl_l2_classify_host(nffacl_l2engine *eng, const uint8_t *h_slots, uint32_t stride, uint64_t n,
+                            uint32_t *h_port, uint8_t *h_permit) {
+    if (!eng) return NFFACL_ERR_INVALID_ARG;
+    if (n == 0) return NFFACL_OK;
+    if (!h_slots || stride < 64 || (stride % 16) != 0) return NFFACL_ERR_INVALID_ARG;
+    if (!h_port && !h_permit) return NFFACL_OK;
+    std::lock_guard<std::mutex> g(eng->host_mu);
+    HIP_CHECK(hipSetDevice(eng->device));
+    if (!eng->stream) HIP_CHECK(hipStreamCreateWithFlags(&eng->stream, hipStreamNonBlocking));
+    if (eng->cap_bytes < n * stride) {
+        if (eng->d_slots) (void)hipFree(eng->d_slots);
+        eng->d_slots = nullptr;
+        eng->cap_bytes = 0;
+        HIP_CHECK(hipMalloc(reinterpret_cast<void **>(&eng->d_slots), n * stride));
+        eng->cap_bytes = n * stride;
+    }
+    if (eng->cap_n < n) {
+        if (eng->d_port) (void)hipFree(eng->d_port);
+        eng->d_port = nullptr;
+        eng->cap_n = 0;
+        HIP_CHECK(hipMalloc(reinterpret_cast<void **>(&eng->d_port), n * 4));
+        eng->cap_n = n;
+    }
+    std::vector<uint32_t> tmp;
+    uint32_t *port = h_port;
+    if (!port) {
+        tmp.resize(n);
+        port = tmp.data();
+    }
+    HIP_CHECK(hipMemcpyAsync(eng->d_slots, h_slots, n * stride, hipMemcpyHostToDevice, eng->stream));
+    int st = l2_launch_slots(eng, acquire_l2(eng), eng->d_slots, stride, n, eng->d_port, nullptr, eng->stream);
+    if (st != NFFACL_OK) return st;
+    HIP_CHECK(hipMemcpyAsync(port, eng->d_port, n * 4, hipMemcpyDeviceToHost, eng->stream));
+    HIP_CHECK(hipStreamSynchronize(eng->stream));
+    if (h_permit)
+        for (uint64_t i = 0; i < n; ++i) h_permit[i] = port[i] != 0;
     return NFFACL_OK;
 }
 

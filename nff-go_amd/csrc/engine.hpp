@@ -49,6 +49,11 @@ struct nffacl_engine {
 };
 
 namespace nffacl {
+// The table launches issued now must use (swap_rules may replace it later).
+inline DevTable *acquire_table(nffacl_engine *eng) {
+    std::lock_guard<std::mutex> g(eng->table_mu);
+    return eng->active;
+}
 int prepare_kernels();
 int launch_slots(nffacl_engine *eng, const DevTable *t, const uint8_t *d_slots, uint32_t stride,
                  uint64_t n, uint32_t *d_port, uint64_t *d_permit, hipStream_t stream);

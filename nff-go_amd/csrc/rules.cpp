@@ -383,10 +383,15 @@ bool raw_l3_parse(const std::vector<RawL3Rule> &raw, nffacl_rules &out, ParseErr
     return true;
 }
 
-bool parse_text_table(const char *data, size_t len, nffacl_rules &out, ParseError &err) {
-    // bufio.Scanner + ScanLines (64 KiB max token), acl.go:156-173.
+namespace {
+
+// bufio.Scanner + ScanLines (64 KiB max token) + strings.Fields, the loop both
+// text loaders share (acl.go:97-112 for L2, 156-173 for L3): comment and empty
+// lines skipped, a missing last field defaults to "false", any other field
+// count is ParseRuleErr.
+bool scan_table(const char *data, size_t len, size_t nfields, const char *incomplete,
+                std::vector<std::vector<std::string>> &rows, ParseError &err) {
     constexpr size_t kMaxToken = 64 * 1024;
-    std::vector<RawL3Rule> raw;
     size_t pos = 0;
     while (pos < len) {
         const void *nl = std::memchr(data + pos, '\n', len - pos);
@@ -402,15 +407,117 @@ bool parse_text_table(const char *data, size_t len, nffacl_rules &out, ParseErro
         pos = nl ? end + 1 : len;
         if (line.empty() || line[0] == '#') continue;
         std::vector<std::string> f = go_fields(line);
-        if (f.size() == 5) {
+        if (f.size() == nfields - 1) {
             f.push_back("false");
-        } else if (f.size() != 6) {
-            wrap(err, NFFACL_ERR_PARSE_RULE, "Incomplete 5-tuple for rule parsing");
+        } else if (f.size() != nfields) {
+            wrap(err, NFFACL_ERR_PARSE_RULE, incomplete);
             return false;
         }
-        raw.push_back(RawL3Rule{f[0], f[1], f[2], f[3], f[4], f[5]});
+        rows.push_back(std::move(f));
     }
+    return true;
+}
+
+}  // namespace
+
+bool parse_text_table(const char *data, size_t len, nffacl_rules &out, ParseError &err) {
+    std::vector<std::vector<std::string>> rows;
+    if (!scan_table(data, len, 6, "Incomplete 5-tuple for rule parsing", rows, err)) return false;
+    std::vector<RawL3Rule> raw;
+    raw.reserve(rows.size());
+    for (auto &f : rows) raw.push_back(RawL3Rule{f[0], f[1], f[2], f[3], f[4], f[5]});
     return raw_l3_parse(raw, out, err);
+}
+
+// ---- L2 (acl.go:88-117, 356-383) ----------------------------------------------
+
+// go1.13 net.ParseMAC: 6-, 8- or 20-byte addresses in colon, dash or dotted
+// (Cisco) notation.
+bool go_parse_mac(const std::string &s, std::vector<uint8_t> &hw) {
+    auto xtoi2 = [&](size_t x, size_t lim, char e, uint8_t &b) -> bool {
+        // xtoi2(s[x:lim], e): two hex digits, then (if more bytes follow) e.
+        if (lim - x > 2 && s[x + 2] != e) return false;
+        const std::string two = s.substr(x, 2);
+        int n; size_t used; bool ok;
+        go_xtoi(two, 0, n, used, ok);
+        b = static_cast<uint8_t>(n);
+        return ok && used == 2;
+    };
+    hw.clear();
+    const size_t L = s.size();
+    if (L < 14) return false;
+    if (s[2] == ':' || s[2] == '-') {
+        if ((L + 1) % 3 != 0) return false;
+        const size_t n = (L + 1) / 3;
+        if (n != 6 && n != 8 && n != 20) return false;
+        hw.resize(n);
+        for (size_t i = 0, x = 0; i < n; ++i, x += 3)
+            if (!xtoi2(x, L, s[2], hw[i])) return false;
+    } else if (s[4] == '.') {
+        if ((L + 1) % 5 != 0) return false;
+        const size_t n = 2 * (L + 1) / 5;
+        if (n != 6 && n != 8 && n != 20) return false;
+        hw.resize(n);
+        for (size_t i = 0, x = 0; i < n; i += 2, x += 5) {
+            if (!xtoi2(x, x + 2, 0, hw[i])) return false;
+            if (!xtoi2(x + 2, L, s[4], hw[i + 1])) return false;
+        }
+    } else {
+        return false;
+    }
+    return true;
+}
+
+bool raw_l2_parse(const std::vector<RawL2Rule> &raw, nffacl_l2rules &out, ParseError &err) {
+    std::vector<nffacl_l2_rule> eth(raw.size());
+    for (size_t i = 0; i < raw.size(); ++i) {
+        const RawL2Rule &r = raw[i];
+        nffacl_l2_rule &e = eth[i];
+        e = nffacl_l2_rule{};
+        if (!parse_rule_result(r.rule, e.output_number, err)) return false;
+        std::vector<uint8_t> hw;
+        if (r.source != "ANY") {
+            e.saddr_not_any = 1;
+            if (!go_parse_mac(r.source, hw)) {
+                wrap(err, NFFACL_ERR_INCORRECT_ARG_IN_RULES, "Incorrect source MAC: " + r.source);
+                return false;
+            }
+            std::memcpy(e.saddr, hw.data(), 6);  // copy(SAddr[:], t): first 6 bytes
+        }
+        if (r.destination != "ANY") {
+            e.daddr_not_any = 1;
+            if (!go_parse_mac(r.destination, hw)) {
+                wrap(err, NFFACL_ERR_INCORRECT_ARG_IN_RULES, "Incorrect destination MAC: " + r.destination);
+                return false;
+            }
+            std::memcpy(e.daddr, hw.data(), 6);
+        }
+        const std::string &id = r.id;
+        if (id == "ANY") {
+            e.id = 0; e.id_mask = 0;
+        } else if (id == "ipv4" || id == "Ipv4" || id == "IPv4" || id == "IPV4" || id == "0x0800") {
+            e.id = 0x0800; e.id_mask = 0xffff;
+        } else if (id == "ipv6" || id == "Ipv6" || id == "IPv6" || id == "IPV6" || id == "0x86dd") {
+            e.id = 0x86dd; e.id_mask = 0xffff;
+        } else if (id == "arp" || id == "Arp" || id == "ARP" || id == "0x0806") {
+            e.id = 0x0806; e.id_mask = 0xffff;
+        } else {
+            wrap(err, NFFACL_ERR_INCORRECT_ARG_IN_RULES, "Incorrect  L3 protocol ID: " + id);
+            return false;
+        }
+    }
+    out.eth.insert(out.eth.end(), eth.begin(), eth.end());
+    return true;
+}
+
+bool parse_l2_text_table(const char *data, size_t len, nffacl_l2rules &out, ParseError &err) {
+    std::vector<std::vector<std::string>> rows;
+    if (!scan_table(data, len, 4, "Incomplete 3-tuple for rule parsing", rows, err)) return false;
+    std::vector<RawL2Rule> raw;
+    raw.reserve(rows.size());
+    // text column order Source Destination ID Rule (acl.go:108-109)
+    for (auto &f : rows) raw.push_back(RawL2Rule{f[3], f[0], f[1], f[2]});
+    return raw_l2_parse(raw, out, err);
 }
 
 }  // namespace nffacl
@@ -610,23 +717,34 @@ struct JsonCursor {
     }
 };
 
-bool ascii_ieq(const std::string &a, const char *b) {
-    size_t n = std::strlen(b);
-    if (a.size() != n) return false;
-    for (size_t i = 0; i < n; ++i) {
-        char x = a[i], y = b[i];
-        if (x >= 'A' && x <= 'Z') x = static_cast<char>(x - 'A' + 'a');
-        if (y >= 'A' && y <= 'Z') y = static_cast<char>(y - 'A' + 'a');
-        if (x != y) return false;
+// encoding/json's key matching for a struct field name (go1.13 fold.go):
+// ASCII case folding, plus — for names containing s/S or k/K, which select
+// equalFoldRight — U+017F (long s) matching s and U+212A (Kelvin) matching k.
+bool json_key_eq(const std::string &key, const char *field) {
+    size_t t = 0;
+    for (const char *f = field; *f; ++f) {
+        if (t >= key.size()) return false;
+        const unsigned char tb = static_cast<unsigned char>(key[t]);
+        const char lf = (*f >= 'A' && *f <= 'Z') ? static_cast<char>(*f - 'A' + 'a') : *f;
+        if (tb < 0x80) {
+            const char lt = (tb >= 'A' && tb <= 'Z') ? static_cast<char>(tb - 'A' + 'a') : static_cast<char>(tb);
+            const bool letter = lf >= 'a' && lf <= 'z';
+            if (letter ? lt != lf : static_cast<char>(tb) != *f) return false;
+            ++t;
+            continue;
+        }
+        if (lf == 's' && key.compare(t, 2, "\xC5\xBF") == 0) { t += 2; continue; }
+        if (lf == 'k' && key.compare(t, 3, "\xE2\x84\xAA") == 0) { t += 3; continue; }
+        return false;
     }
-    return true;
+    return t == key.size();
 }
 
-}  // namespace
-
-bool parse_json(const char *data, size_t len, nffacl_rules &out, ParseError &err) {
+// json.Unmarshal of {"<top>": [ {<fields>: string, ...}, ... ]} into a slice
+// of records of string fields (rawL2Rules acl.go:44-53, rawL3Rules :55-66).
+bool parse_json_records(const char *data, size_t len, const char *top, const char *const *fields, size_t nf,
+                        const char *type_name, std::vector<std::vector<std::string>> &rows, ParseError &err) {
     JsonCursor c{data, data + len, false, std::string()};
-    std::vector<RawL3Rule> raw;
     bool ok = true;
     c.ws();
     if (c.p >= c.end) {
@@ -635,26 +753,22 @@ bool parse_json(const char *data, size_t len, nffacl_rules &out, ParseError &err
         ok = c.literal("null");
     } else if (*c.p == '{') {
         ok = c.object([&](const std::string &key) -> bool {
-            if (!ascii_ieq(key, "L3Rules")) return c.skip();
+            if (!json_key_eq(key, top)) return c.skip();
             c.ws();
             if (c.p < c.end && *c.p == 'n') return c.literal("null");
             if (c.p >= c.end || *c.p != '[') {
                 c.type_error = true;
                 return c.skip();
             }
-            raw.clear();  // a later L3Rules key replaces the slice
+            rows.clear();  // a later matching key replaces the slice
             return c.array([&]() -> bool {
-                RawL3Rule r;
+                std::vector<std::string> r(nf);
                 c.ws();
                 bool elem_ok;
                 if (c.p < c.end && *c.p == '{') {
                     elem_ok = c.object([&](const std::string &k) -> bool {
-                        if (ascii_ieq(k, "SrcAddr")) return c.string_field(r.src_addr);
-                        if (ascii_ieq(k, "DstAddr")) return c.string_field(r.dst_addr);
-                        if (ascii_ieq(k, "ID")) return c.string_field(r.id);
-                        if (ascii_ieq(k, "SrcPort")) return c.string_field(r.src_port);
-                        if (ascii_ieq(k, "DstPort")) return c.string_field(r.dst_port);
-                        if (ascii_ieq(k, "OutputNumber")) return c.string_field(r.output_number);
+                        for (size_t i = 0; i < nf; ++i)
+                            if (json_key_eq(k, fields[i])) return c.string_field(r[i]);
                         return c.skip();
                     });
                 } else if (c.p < c.end && *c.p == 'n') {
@@ -663,7 +777,7 @@ bool parse_json(const char *data, size_t len, nffacl_rules &out, ParseError &err
                     c.type_error = true;
                     elem_ok = c.skip();
                 }
-                raw.push_back(r);
+                rows.push_back(std::move(r));
                 return elem_ok;
             });
         });
@@ -682,10 +796,32 @@ bool parse_json(const char *data, size_t len, nffacl_rules &out, ParseError &err
     }
     if (c.type_error) {
         err.code = NFFACL_ERR_PARSE_RULE_JSON;
-        err.message = "JSON error during rules parsing: json: cannot unmarshal value into rawL3Rules";
+        err.message = std::string("JSON error during rules parsing: json: cannot unmarshal value into ") + type_name;
         return false;
     }
+    return true;
+}
+
+}  // namespace
+
+bool parse_json(const char *data, size_t len, nffacl_rules &out, ParseError &err) {
+    static const char *const kFields[] = {"SrcAddr", "DstAddr", "ID", "SrcPort", "DstPort", "OutputNumber"};
+    std::vector<std::vector<std::string>> rows;
+    if (!parse_json_records(data, len, "L3Rules", kFields, 6, "rawL3Rules", rows, err)) return false;
+    std::vector<RawL3Rule> raw;
+    raw.reserve(rows.size());
+    for (auto &f : rows) raw.push_back(RawL3Rule{f[0], f[1], f[2], f[3], f[4], f[5]});
     return raw_l3_parse(raw, out, err);
+}
+
+bool parse_l2_json(const char *data, size_t len, nffacl_l2rules &out, ParseError &err) {
+    static const char *const kFields[] = {"Rule", "Source", "Destination", "ID"};
+    std::vector<std::vector<std::string>> rows;
+    if (!parse_json_records(data, len, "L2Rules", kFields, 4, "rawL2Rules", rows, err)) return false;
+    std::vector<RawL2Rule> raw;
+    raw.reserve(rows.size());
+    for (auto &f : rows) raw.push_back(RawL2Rule{f[0], f[1], f[2], f[3]});
+    return raw_l2_parse(raw, out, err);
 }
 
 }  // namespace nffacl

@@ -18,6 +18,10 @@ struct nffacl_rules {
     std::vector<nffacl_rule6> ip6;
 };
 
+struct nffacl_l2rules {
+    std::vector<nffacl_l2_rule> eth;  // L2Rules.eth, acl.go:457-460
+};
+
 namespace nffacl {
 
 // One line of a rule file after field splitting: acl.go:55-62 rawL3Rule.
@@ -39,6 +43,20 @@ bool parse_text_table(const char *data, size_t len, nffacl_rules &out, ParseErro
 
 // GetL3ACLFromJSON body (acl.go:129-133) over an in-memory file image.
 bool parse_json(const char *data, size_t len, nffacl_rules &out, ParseError &err);
+
+// rawL2Rule (acl.go:44-49).
+struct RawL2Rule {
+    std::string rule, source, destination, id;
+};
+
+// rawL2Parse (acl.go:356-383), GetL2ACLFromTextTable body (acl.go:97-117),
+// GetL2ACLFromJSON body (acl.go:78-83).
+bool raw_l2_parse(const std::vector<RawL2Rule> &raw, nffacl_l2rules &out, ParseError &err);
+bool parse_l2_text_table(const char *data, size_t len, nffacl_l2rules &out, ParseError &err);
+bool parse_l2_json(const char *data, size_t len, nffacl_l2rules &out, ParseError &err);
+
+// go1.13 net.ParseMAC (6-, 8- or 20-byte hardware addresses).
+bool go_parse_mac(const std::string &s, std::vector<uint8_t> &hw);
 
 // go1.13 net.ParseCIDR restricted to what rawL3Parse consumes: the masked
 // network address (4 bytes for dotted-quad input, 16 for IPv6 syntax) and the

@@ -169,6 +169,8 @@ struct Packet {
     bool L3ACLPermit(const L3Rules &rules) const {    // acl.go:495
         return L3ACLPort(rules) > 0;
     }
+    uint32_t L2ACLPort(const class L2Rules &rules) const;  // acl.go:472
+    bool L2ACLPermit(const class L2Rules &rules) const;    // acl.go:464
 };
 
 // Classify n packets in one GPU call (host staging inside libnffacl).
@@ -189,6 +191,102 @@ inline uint32_t Packet::L3ACLPort(const L3Rules &rules) const {
     const Packet *p = this;
     uint32_t port = 0;
     L3ACLPortBatch(&p, 1, &port, rules);
+    return port;
+}
+
+// ---- L2 ACL (acl.go:68-117, 356-383, 457-491) ----------------------------------
+
+// Owner of an nffacl_l2rules handle plus, lazily, its device table.
+class L2Rules {
+public:
+    explicit L2Rules(nffacl_l2rules *h) : h_(h) {}
+    L2Rules(const L2Rules &) = delete;
+    L2Rules &operator=(const L2Rules &) = delete;
+    ~L2Rules() {
+        if (eng_) nffacl_l2_engine_destroy(eng_);
+        if (h_) nffacl_l2rules_free(h_);
+    }
+    const nffacl_l2rules *handle() const { return h_; }
+
+    // The reference's unexported eth slice (acl.go:458-460).
+    std::vector<nffacl_l2_rule> eth() const {
+        size_t n = 0;
+        nffacl_l2rules_count(h_, &n);
+        std::vector<nffacl_l2_rule> v(n);
+        for (size_t i = 0; i < n; ++i) nffacl_l2rules_get(h_, i, &v[i]);
+        return v;
+    }
+
+    nffacl_l2engine *engine() const {
+        std::call_once(once_, [&] {
+            st_ = nffacl_l2_engine_create(0, h_, &eng_);
+            if (st_ != NFFACL_OK) err_ = nffacl_last_error();
+        });
+        if (st_ != NFFACL_OK)
+            throw std::runtime_error(std::string("nffacl_l2_engine_create: ") + nffacl_strerror(st_) + " " + err_);
+        return eng_;
+    }
+
+    // L2Rules{eth: ...} literal (acl_internal_test.go:1189-1191).
+    static std::shared_ptr<L2Rules> FromRecords(const std::vector<nffacl_l2_rule> &eth) {
+        nffacl_l2rules *h = nullptr;
+        if (nffacl_l2rules_from_array(eth.data(), eth.size(), &h) != NFFACL_OK)
+            throw std::runtime_error("nffacl_l2rules_from_array failed");
+        return std::make_shared<L2Rules>(h);
+    }
+
+private:
+    nffacl_l2rules *h_ = nullptr;
+    mutable std::once_flag once_;
+    mutable nffacl_l2engine *eng_ = nullptr;
+    mutable int st_ = NFFACL_OK;
+    mutable std::string err_;
+};
+
+using L2RulesOrError = std::pair<std::shared_ptr<L2Rules>, std::optional<common::NFError>>;
+
+namespace detail {
+template <class F>
+L2RulesOrError load_l2(F fn, const std::string &filename) {
+    nffacl_l2rules *h = nullptr;
+    char err[512] = {0};
+    const int st = fn(filename.c_str(), &h, err, sizeof err);
+    if (st != NFFACL_OK) return {nullptr, common::from_status(st, err)};
+    return {std::make_shared<L2Rules>(h), std::nullopt};
+}
+}  // namespace detail
+
+// acl.go:88.
+inline L2RulesOrError GetL2ACLFromTextTable(const std::string &filename) {
+    return detail::load_l2(nffacl_l2rules_load_text, filename);
+}
+
+// acl.go:70.
+inline L2RulesOrError GetL2ACLFromJSON(const std::string &filename) {
+    return detail::load_l2(nffacl_l2rules_load_json, filename);
+}
+
+// L2ACLPort over n packets in one GPU call (only the Ethernet header travels).
+inline void L2ACLPortBatch(const Packet *const *pkts, size_t n, uint32_t *ports, const L2Rules &rules) {
+    if (n == 0) return;
+    constexpr uint32_t kL2Slot = 64;
+    std::vector<uint8_t> slots(n * kL2Slot, 0);
+    for (size_t i = 0; i < n; ++i) {
+        const uint32_t len = pkts[i]->Len < types::EtherLen ? pkts[i]->Len : types::EtherLen;
+        if (len) std::memcpy(&slots[i * kL2Slot], pkts[i]->Ether, len);
+    }
+    const int st = nffacl_l2_classify_host(rules.engine(), slots.data(), kL2Slot, n, ports, nullptr);
+    if (st != NFFACL_OK)
+        throw std::runtime_error(std::string("nffacl_l2_classify_host: ") + nffacl_strerror(st) + " " +
+                                 nffacl_last_error());
+}
+
+inline bool Packet::L2ACLPermit(const L2Rules &rules) const { return L2ACLPort(rules) > 0; }
+
+inline uint32_t Packet::L2ACLPort(const L2Rules &rules) const {
+    const Packet *p = this;
+    uint32_t port = 0;
+    L2ACLPortBatch(&p, 1, &port, rules);
     return port;
 }
 

@@ -7,6 +7,8 @@ reference API this path replaces (packet/acl.go):
   GetL3ACLFromJSON(filename)      -> (L3Rules, NFError|None)   acl.go:121
   Engine(rules).L3ACLPort / L3ACLPermit over whole packet batches
                                    (acl.go:495-506, run on the GPU)
+  GetL2ACLFromTextTable / GetL2ACLFromJSON -> (L2Rules, NFError|None)  acl.go:88, 70
+  L2Engine(rules).L2ACLPort / L2ACLPermit                        acl.go:462-491
 
 There is no CPU fallback: every verdict comes from the HIP kernels in
 libnffacl.so.  Importing this module fails loudly if the library is missing.
@@ -63,6 +65,10 @@ RULE4 = np.dtype([("output_number", "<u4"), ("src_addr", "<u4"), ("dst_addr", "<
 RULE6 = np.dtype([("output_number", "<u4"), ("src_addr", "u1", 16), ("dst_addr", "u1", 16),
                   ("src_mask", "u1", 16), ("dst_mask", "u1", 16)] + _L4)
 assert RULE4.itemsize == 32 and RULE6.itemsize == 80
+L2RULE = np.dtype([("output_number", "<u4"), ("daddr_not_any", "u1"), ("saddr_not_any", "u1"),
+                   ("daddr", "u1", 6), ("saddr", "u1", 6), ("id_mask", "<u2"), ("id", "<u2"),
+                   ("reserved", "<u2")])
+assert L2RULE.itemsize == 24
 
 _vp, _sz, _u32, _u64, _i = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
 _pp = ctypes.POINTER(ctypes.c_void_p)
@@ -92,6 +98,37 @@ _engine_table_bytes = _sig("nffacl_engine_table_bytes", _i, _vp, ctypes.POINTER(
 _classify_device = _sig("nffacl_classify_device", _i, _vp, _vp, _u32, _u64, _vp, _vp, _vp)
 _classify_frames = _sig("nffacl_classify_frames_device", _i, _vp, _vp, _vp, _u64, _vp, _vp, _vp)
 _classify_host = _sig("nffacl_classify_host", _i, _vp, _vp, _u32, _u64, _vp, _vp)
+_l2_load_text = _sig("nffacl_l2rules_load_text", _i, ctypes.c_char_p, _pp, ctypes.c_char_p, _sz)
+_l2_parse_text = _sig("nffacl_l2rules_parse_text", _i, ctypes.c_char_p, _sz, _pp, ctypes.c_char_p, _sz)
+_l2_load_json = _sig("nffacl_l2rules_load_json", _i, ctypes.c_char_p, _pp, ctypes.c_char_p, _sz)
+_l2_parse_json = _sig("nffacl_l2rules_parse_json", _i, ctypes.c_char_p, _sz, _pp, ctypes.c_char_p, _sz)
+_l2_from_array = _sig("nffacl_l2rules_from_array", _i, _vp, _sz, _pp)
+_l2_free = _sig("nffacl_l2rules_free", None, _vp)
+_l2_count = _sig("nffacl_l2rules_count", _i, _vp, ctypes.POINTER(_sz))
+_l2_get = _sig("nffacl_l2rules_get", _i, _vp, _sz, _vp)
+_l2_engine_create = _sig("nffacl_l2_engine_create", _i, _i, _vp, _pp)
+_l2_engine_swap = _sig("nffacl_l2_engine_swap_rules", _i, _vp, _vp)
+_l2_engine_destroy = _sig("nffacl_l2_engine_destroy", None, _vp)
+_l2_classify_device = _sig("nffacl_l2_classify_device", _i, _vp, _vp, _u32, _u64, _vp, _vp, _vp)
+_l2_classify_frames = _sig("nffacl_l2_classify_frames_device", _i, _vp, _vp, _vp, _u64, _vp, _vp, _vp)
+_l2_classify_host = _sig("nffacl_l2_classify_host", _i, _vp, _vp, _u32, _u64, _vp, _vp)
+class Ticket(ctypes.Structure):
+    _fields_ = [("seq", ctypes.c_uint64), ("buf", ctypes.c_uint32), ("off", ctypes.c_uint32),
+                ("n", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+
+
+class BatcherStats(ctypes.Structure):
+    _fields_ = [("batches", ctypes.c_uint64), ("packets", ctypes.c_uint64), ("bursts", ctypes.c_uint64),
+                ("timeouts", ctypes.c_uint64)]
+
+
+_batcher_create = _sig("nffacl_batcher_create", _i, _vp, _u32, _u32, _u32, _u32, _pp)
+_batcher_submit = _sig("nffacl_batcher_submit", _i, _vp, _vp, _vp, _u32, ctypes.POINTER(Ticket))
+_batcher_wait = _sig("nffacl_batcher_wait", _i, _vp, ctypes.POINTER(Ticket), _vp)
+_batcher_classify = _sig("nffacl_batcher_classify", _i, _vp, _vp, _vp, _u32, _vp)
+_batcher_flush = _sig("nffacl_batcher_flush", _i, _vp)
+_batcher_stats = _sig("nffacl_batcher_get_stats", _i, _vp, ctypes.POINTER(BatcherStats))
+_batcher_destroy = _sig("nffacl_batcher_destroy", None, _vp)
 _strerror = _sig("nffacl_strerror", ctypes.c_char_p, _i)
 _last_error = _sig("nffacl_last_error", ctypes.c_char_p)
 _abi_version = _sig("nffacl_abi_version", _i)
@@ -103,7 +140,14 @@ EXPORTED_SYMBOLS = [
     "nffacl_engine_create", "nffacl_engine_create_ex", "nffacl_engine_swap_rules",
     "nffacl_engine_destroy", "nffacl_engine_algo", "nffacl_engine_table_bytes",
     "nffacl_classify_device", "nffacl_classify_frames_device", "nffacl_classify_host",
-    "nffacl_strerror", "nffacl_abi_version", "nffacl_last_error",
+    "nffacl_table_compile", "nffacl_strerror", "nffacl_abi_version", "nffacl_last_error",
+    "nffacl_l2rules_load_text", "nffacl_l2rules_parse_text", "nffacl_l2rules_load_json",
+    "nffacl_l2rules_parse_json", "nffacl_l2rules_from_array", "nffacl_l2rules_free",
+    "nffacl_l2rules_count", "nffacl_l2rules_get", "nffacl_l2_engine_create",
+    "nffacl_l2_engine_swap_rules", "nffacl_l2_engine_destroy", "nffacl_l2_classify_device",
+    "nffacl_l2_classify_frames_device", "nffacl_l2_classify_host",
+    "nffacl_batcher_create", "nffacl_batcher_submit", "nffacl_batcher_wait", "nffacl_batcher_classify",
+    "nffacl_batcher_flush", "nffacl_batcher_get_stats", "nffacl_batcher_destroy",
 ]
 
 
@@ -311,4 +355,231 @@ class Engine:
         return self.classify_host(slots, stride)[0]
 
     def L3ACLPermit(self, slots: np.ndarray, stride: int):
+        return self.classify_host(slots, stride)[1].astype(bool)
+
+
+class Batcher:
+    """Multi-producer burst aggregator (nffacl_batcher_*): the body of the
+    reference's VectorSeparateFunction (flow.go:131) shared by many threads.
+    ctypes drops the GIL during the calls, so Python threads really overlap."""
+
+    def __init__(self, engine: "Engine", stride: int = 80, max_batch: int = 1 << 16,
+                 max_delay_us: int = 100, nbuf: int = 4):
+        out = ctypes.c_void_p()
+        st = _batcher_create(engine._h, stride, max_batch, max_delay_us, nbuf, ctypes.byref(out))
+        if st != OK:
+            _raise(st, "nffacl_batcher_create")
+        self._h = out.value
+        self._engine = engine  # keep the engine alive
+        self.stride = stride
+
+    def close(self):
+        h, self._h = getattr(self, "_h", None), None
+        if h and _batcher_destroy is not None:
+            try:
+                _batcher_destroy(h)
+            except Exception:  # interpreter teardown
+                pass
+
+    def __del__(self):
+        self.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    @staticmethod
+    def frame_pointers(buf: np.ndarray, offsets, lens):
+        """(uint64 pointer array, uint32 length array) for frames inside `buf`."""
+        base = buf.ctypes.data
+        ptrs = (base + np.asarray(offsets, np.uint64)).astype(np.uint64)
+        return ptrs, np.ascontiguousarray(lens, np.uint32)
+
+    def classify(self, ptrs: np.ndarray, lens: np.ndarray | None) -> np.ndarray:
+        n = len(ptrs)
+        ports = np.zeros(n, np.uint32)
+        st = _batcher_classify(self._h, ptrs.ctypes.data, None if lens is None else lens.ctypes.data, n,
+                               ports.ctypes.data)
+        if st != OK:
+            _raise(st, "nffacl_batcher_classify")
+        return ports
+
+    def submit(self, ptrs: np.ndarray, lens: np.ndarray | None) -> Ticket:
+        t = Ticket()
+        st = _batcher_submit(self._h, ptrs.ctypes.data, None if lens is None else lens.ctypes.data, len(ptrs),
+                             ctypes.byref(t))
+        if st != OK:
+            _raise(st, "nffacl_batcher_submit")
+        return t
+
+    def wait(self, t: Ticket) -> np.ndarray:
+        ports = np.zeros(t.n, np.uint32)
+        st = _batcher_wait(self._h, ctypes.byref(t), ports.ctypes.data)
+        if st != OK:
+            _raise(st, "nffacl_batcher_wait")
+        return ports
+
+    def flush(self):
+        st = _batcher_flush(self._h)
+        if st != OK:
+            _raise(st, "nffacl_batcher_flush")
+
+    def stats(self) -> dict:
+        s = BatcherStats()
+        _batcher_stats(self._h, ctypes.byref(s))
+        return {k: getattr(s, k) for k, _ in BatcherStats._fields_}
+
+
+# ---- L2 ACL (acl.go:68-117, 356-383, 457-491) ---------------------------------
+
+class L2Rules:
+    """Owner of an nffacl_l2rules handle (the reference's *packet.L2Rules)."""
+
+    def __init__(self, handle):
+        self._h = handle
+
+    def __del__(self):
+        h, self._h = getattr(self, "_h", None), None
+        if h and _l2_free is not None:
+            try:
+                _l2_free(h)
+            except Exception:  # interpreter teardown
+                pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    @staticmethod
+    def _parse(fn, *args):
+        out = ctypes.c_void_p()
+        err = ctypes.create_string_buffer(512)
+        st = fn(*args, ctypes.byref(out), err, len(err))
+        if st != OK:
+            raise NFError(st, err.value.decode(errors="replace"))
+        return L2Rules(out.value)
+
+    @classmethod
+    def from_text_file(cls, path) -> "L2Rules":
+        return cls._parse(_l2_load_text, str(path).encode())
+
+    @classmethod
+    def parse_text(cls, text: bytes | str) -> "L2Rules":
+        b = text.encode() if isinstance(text, str) else bytes(text)
+        return cls._parse(_l2_parse_text, b, len(b))
+
+    @classmethod
+    def from_json_file(cls, path) -> "L2Rules":
+        return cls._parse(_l2_load_json, str(path).encode())
+
+    @classmethod
+    def parse_json(cls, text: bytes | str) -> "L2Rules":
+        b = text.encode() if isinstance(text, str) else bytes(text)
+        return cls._parse(_l2_parse_json, b, len(b))
+
+    @classmethod
+    def from_array(cls, eth) -> "L2Rules":
+        a = np.ascontiguousarray(eth if eth is not None else np.zeros(0, L2RULE), L2RULE)
+        out = ctypes.c_void_p()
+        st = _l2_from_array(a.ctypes.data if len(a) else None, len(a), ctypes.byref(out))
+        if st != OK:
+            _raise(st, "nffacl_l2rules_from_array")
+        return L2Rules(out.value)
+
+    def count(self) -> int:
+        n = _sz()
+        st = _l2_count(self._h, ctypes.byref(n))
+        if st != OK:
+            _raise(st, "nffacl_l2rules_count")
+        return n.value
+
+    def eth(self) -> np.ndarray:
+        n = self.count()
+        a = np.zeros(n, L2RULE)
+        for i in range(n):
+            _l2_get(self._h, i, a[i:i + 1].ctypes.data)
+        return a
+
+
+def GetL2ACLFromTextTable(filename):
+    """(rules, err) like the Go API; rules is None on error."""
+    try:
+        return L2Rules.from_text_file(filename), None
+    except NFError as e:
+        return None, e
+
+
+def GetL2ACLFromJSON(filename):
+    try:
+        return L2Rules.from_json_file(filename), None
+    except NFError as e:
+        return None, e
+
+
+class L2Engine:
+    """A compiled L2 rule table resident on one HIP device."""
+
+    def __init__(self, rules: L2Rules, device: int = 0):
+        out = ctypes.c_void_p()
+        st = _l2_engine_create(device, rules.handle, ctypes.byref(out))
+        if st != OK:
+            _raise(st, "nffacl_l2_engine_create")
+        self._h = out.value
+        self.device = device
+
+    def close(self):
+        h, self._h = getattr(self, "_h", None), None
+        if h and _l2_engine_destroy is not None:
+            try:
+                _l2_engine_destroy(h)
+            except Exception:  # interpreter teardown
+                pass
+
+    def __del__(self):
+        self.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def swap_rules(self, rules: L2Rules):
+        st = _l2_engine_swap(self._h, rules.handle)
+        if st != OK:
+            _raise(st, "nffacl_l2_engine_swap_rules")
+
+    def classify_device(self, slots, stride: int, n: int, port=None, permit_bits=None, stream=None):
+        s = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
+        st = _l2_classify_device(self._h, _ptr(slots), stride, n, _ptr(port), _ptr(permit_bits), s)
+        if st != OK:
+            _raise(st, "nffacl_l2_classify_device")
+
+    def classify_frames_device(self, frames, desc, n: int, port=None, permit_bits=None, stream=None):
+        s = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
+        st = _l2_classify_frames(self._h, _ptr(frames), _ptr(desc), n, _ptr(port), _ptr(permit_bits), s)
+        if st != OK:
+            _raise(st, "nffacl_l2_classify_frames_device")
+
+    def classify_host(self, slots: np.ndarray, stride: int, n: int | None = None):
+        """Host slots -> (port uint32[n], permit uint8[n])."""
+        slots = np.ascontiguousarray(slots, np.uint8)
+        if n is None:
+            n = slots.size // stride
+        if slots.size < n * stride:
+            raise ValueError("slot buffer too small")
+        port = np.zeros(n, np.uint32)
+        permit = np.zeros(n, np.uint8)
+        st = _l2_classify_host(self._h, slots.ctypes.data, stride, n, port.ctypes.data, permit.ctypes.data)
+        if st != OK:
+            _raise(st, "nffacl_l2_classify_host")
+        return port, permit
+
+    # Batch forms of the reference's per-packet API (acl.go:462-476)
+    def L2ACLPort(self, slots: np.ndarray, stride: int):
+        return self.classify_host(slots, stride)[0]
+
+    def L2ACLPermit(self, slots: np.ndarray, stride: int):
         return self.classify_host(slots, stride)[1].astype(bool)

@@ -402,3 +402,61 @@ def gen_imix(rules: GenRules, n: int, seed: int, align: int = 64, chunk: int = 1
         frames[idx[own]] = img[own]
     desc = (offs.astype(np.uint64) << np.uint64(16)) | lengths.astype(np.uint64)
     return frames, desc
+
+
+# ---- L2 ACL workload (§8f: GetL2ACLFromTextTable rules, Ethernet headers) ----------
+
+L2_RULE_SEED = 0x5EED0020
+L2_PACKET_SEED = 0x9AC70020
+_L2_IDS = [("ANY", 0), ("ipv4", 0x0800), ("IPv6", 0x86DD), ("arp", 0x0806)]
+
+
+@dataclass
+class GenL2Rules:
+    text: str
+    macs: np.ndarray  # (k, 6) uint8 pool the rules draw from
+
+
+def _mac_text(m, style: int) -> str:
+    h = [f"{b:02x}" for b in m]
+    if style == 0:
+        return ":".join(h)
+    if style == 1:
+        return "-".join(h).upper()
+    return ".".join(h[i] + h[i + 1] for i in range(0, 6, 2))
+
+
+def gen_l2_rules(n: int, seed: int = L2_RULE_SEED) -> GenL2Rules:
+    """n L2 rules "Source Destination ID Rule": each MAC a pool address with
+    p=0.6 else ANY (never both ANY unless ID is set, so rules stay live), MAC
+    notations colon / dash / dotted, outputs Accept/Reject/numeric."""
+    rng = np.random.default_rng(seed)
+    pool = rng.integers(0, 256, (max(8, n // 2), 6), dtype=np.uint8)
+    lines = ["# Source MAC, Destination MAC, L3 ID, Output port"]
+    for _ in range(n):
+        src = _mac_text(pool[rng.integers(len(pool))], int(rng.integers(3))) if rng.random() < 0.6 else "ANY"
+        dst = _mac_text(pool[rng.integers(len(pool))], int(rng.integers(3))) if rng.random() < 0.6 else "ANY"
+        ident = _L2_IDS[int(rng.integers(len(_L2_IDS)))][0]
+        if src == "ANY" and dst == "ANY" and ident == "ANY":
+            ident = "ipv6"
+        r = rng.random()
+        out = "Accept" if r < 0.6 else "Reject" if r < 0.9 else str(int(rng.integers(2, 16)))
+        lines.append(f"{src} {dst} {ident} {out}")
+    return GenL2Rules("\n".join(lines) + "\n", pool)
+
+
+def gen_l2_slots(rules: GenL2Rules, n: int, seed: int = L2_PACKET_SEED, stride: int = 64) -> np.ndarray:
+    """Dense slots whose Ethernet headers draw MACs from the rule pool (p=0.7)
+    and EtherTypes from IPv4/IPv6/ARP/VLAN/random; bytes 14.. random."""
+    rng = np.random.default_rng(seed)
+    buf = rng.integers(0, 256, (n, stride), dtype=np.uint8)
+    pool = rules.macs
+    for off in (0, 6):
+        take = rng.random(n) < 0.7
+        buf[take, off:off + 6] = pool[rng.integers(0, len(pool), int(take.sum()))]
+    et = np.array([0x0800, 0x86DD, 0x0806, 0x8100], np.uint16)[rng.integers(0, 4, n)]
+    rnd = rng.random(n) < 0.1
+    et[rnd] = rng.integers(0, 1 << 16, int(rnd.sum()), dtype=np.uint16)
+    buf[:, 12] = et >> 8
+    buf[:, 13] = et & 0xFF
+    return buf.reshape(-1)

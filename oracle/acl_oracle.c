@@ -18,6 +18,8 @@
  *   SwapBytesUint16        packet/packet.go:713-715
  *   IPv4Hdr / IPv6Hdr / UDPHdr layouts packet/packet.go:107-170
  *   types.IPv4Address = LE uint32 of wire bytes   types/ipv4.go:13-28
+ *   (*Packet).l2ACL        packet/acl.go:478-491   (L2 ACL, §8f next row)
+ *   EtherHdr layout        packet/packet.go:96-100 (DAddr, SAddr, EtherType)
  *
  * Packet memory convention: the reference reads raw mbuf memory; here a packet
  * is `len` bytes and any byte at index >= len reads as 0.
@@ -50,6 +52,15 @@ typedef struct {
     uint8_t SrcAddr[16], DstAddr[16], SrcMask[16], DstMask[16];
     orc_l4 L4;
 } orc_rule6;
+
+/* l2Rules, acl.go:413-421 (byte layout shared with tests/ via numpy). */
+typedef struct {
+    uint32_t OutputNumber;
+    uint8_t DAddrNotAny, SAddrNotAny;
+    uint8_t DAddr[6], SAddr[6];
+    uint16_t IDMask, ID;
+    uint16_t pad;
+} orc_l2rule;
 
 /* A packet: its bytes and the parse "pointers" (offsets) of packet.Packet. */
 typedef struct {
@@ -152,6 +163,26 @@ uint32_t oracle_l3acl(const uint8_t *data, uint32_t len, const orc_rule4 *ip4, s
 
 /* ---- batch drivers (std::thread-like shards over pthreads) ---------------- */
 
+/* (*Packet).l2ACL, acl.go:478-491: Ether.DAddr = bytes 0..5, SAddr = 6..11,
+ * EtherType = LE u16 of bytes 12..13 (compared after SwapBytesUint16). */
+uint32_t oracle_l2acl(const uint8_t *data, uint32_t len, const orc_l2rule *eth, size_t n) {
+    orc_packet p = {data, len, 0, 0};
+    uint8_t DAddr[6], SAddr[6];
+    for (int i = 0; i < 6; i++) {
+        DAddr[i] = at(&p, (uint32_t)i);
+        SAddr[i] = at(&p, (uint32_t)(6 + i));
+    }
+    const uint16_t EtherType = u16le(&p, 12);
+    for (size_t r = 0; r < n; r++) {
+        const orc_l2rule *rule = &eth[r];
+        if (rule->SAddrNotAny && memcmp(rule->SAddr, SAddr, 6) != 0) continue;
+        if (rule->DAddrNotAny && memcmp(rule->DAddr, DAddr, 6) != 0) continue;
+        if (((rule->ID ^ SwapBytesUint16(EtherType)) & rule->IDMask) != 0) continue;
+        return rule->OutputNumber;
+    }
+    return 0;
+}
+
 typedef struct {
     const uint8_t *base;
     const uint64_t *desc; /* NULL: dense slots */
@@ -163,6 +194,8 @@ typedef struct {
     size_t n6;
     uint32_t *out;
     int64_t *which; /* optional */
+    const orc_l2rule *eth; /* non-NULL: L2 ACL instead of L3 */
+    size_t neth;
 } orc_job;
 
 static void *orc_worker(void *arg) {
@@ -177,15 +210,16 @@ static void *orc_worker(void *arg) {
             pkt = j->base + i * (uint64_t)j->stride;
             len = j->stride;
         }
-        j->out[i] = oracle_l3acl_which(pkt, len, j->ip4, j->n4, j->ip6, j->n6,
-                                       j->which ? &j->which[i] : NULL);
+        j->out[i] = j->eth ? oracle_l2acl(pkt, len, j->eth, j->neth)
+                           : oracle_l3acl_which(pkt, len, j->ip4, j->n4, j->ip6, j->n6,
+                                                j->which ? &j->which[i] : NULL);
     }
     return NULL;
 }
 
-static int orc_run(const uint8_t *base, const uint64_t *desc, uint32_t stride, uint64_t n,
-                   const orc_rule4 *ip4, size_t n4, const orc_rule6 *ip6, size_t n6,
-                   uint32_t *out, int64_t *which, int threads) {
+static int orc_run_any(const uint8_t *base, const uint64_t *desc, uint32_t stride, uint64_t n,
+                       const orc_rule4 *ip4, size_t n4, const orc_rule6 *ip6, size_t n6,
+                       const orc_l2rule *eth, size_t neth, uint32_t *out, int64_t *which, int threads) {
     if (threads < 1) threads = 1;
     if ((uint64_t)threads > n) threads = n ? (int)n : 1;
     pthread_t *tid = (pthread_t *)calloc((size_t)threads, sizeof(pthread_t));
@@ -198,7 +232,7 @@ static int orc_run(const uint8_t *base, const uint64_t *desc, uint32_t stride, u
     uint64_t per = n / (uint64_t)threads, rem = n % (uint64_t)threads, first = 0;
     for (int t = 0; t < threads; t++) {
         uint64_t cnt = per + ((uint64_t)t < rem ? 1 : 0);
-        orc_job j = {base, desc, stride, first, cnt, ip4, n4, ip6, n6, out, which};
+        orc_job j = {base, desc, stride, first, cnt, ip4, n4, ip6, n6, out, which, eth, neth};
         jobs[t] = j;
         first += cnt;
     }
@@ -208,6 +242,12 @@ static int orc_run(const uint8_t *base, const uint64_t *desc, uint32_t stride, u
     free(tid);
     free(jobs);
     return 0;
+}
+
+static int orc_run(const uint8_t *base, const uint64_t *desc, uint32_t stride, uint64_t n,
+                   const orc_rule4 *ip4, size_t n4, const orc_rule6 *ip6, size_t n6,
+                   uint32_t *out, int64_t *which, int threads) {
+    return orc_run_any(base, desc, stride, n, ip4, n4, ip6, n6, NULL, 0, out, which, threads);
 }
 
 /* Dense slots: packet i is slots[i*stride .. (i+1)*stride). */
@@ -230,5 +270,19 @@ int oracle_classify_frames(const uint8_t *frames, const uint64_t *desc, uint64_t
     return orc_run(frames, desc, 0, n, ip4, n4, ip6, n6, out, NULL, threads);
 }
 
+/* L2 ACL over dense slots / packed frames. */
+int oracle_l2_classify_slots(const uint8_t *slots, uint32_t stride, uint64_t n, const orc_l2rule *eth,
+                             size_t neth, uint32_t *out, int threads) {
+    static const orc_l2rule none;
+    return orc_run_any(slots, NULL, stride, n, NULL, 0, NULL, 0, neth ? eth : &none, neth, out, NULL, threads);
+}
+
+int oracle_l2_classify_frames(const uint8_t *frames, const uint64_t *desc, uint64_t n, const orc_l2rule *eth,
+                              size_t neth, uint32_t *out, int threads) {
+    static const orc_l2rule none;
+    return orc_run_any(frames, desc, 0, n, NULL, 0, NULL, 0, neth ? eth : &none, neth, out, NULL, threads);
+}
+
+int oracle_l2rule_size(void) { return (int)sizeof(orc_l2rule); }
 int oracle_rule4_size(void) { return (int)sizeof(orc_rule4); }
 int oracle_rule6_size(void) { return (int)sizeof(orc_rule6); }

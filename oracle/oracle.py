@@ -12,7 +12,7 @@ from pathlib import Path
 
 import numpy as np
 
-from .rules_oracle import RULE4_DTYPE, RULE6_DTYPE
+from .rules_oracle import L2RULE_DTYPE, RULE4_DTYPE, RULE6_DTYPE
 
 _HERE = Path(__file__).resolve().parent
 _LIB_PATH = _HERE / "liboracle.so"
@@ -39,6 +39,13 @@ def _load():
         lib.oracle_classify_slots_which.argtypes = [vp, u32, u64, vp, sz, vp, sz, vp, vp, i]
         lib.oracle_classify_frames.restype = i
         lib.oracle_classify_frames.argtypes = [vp, vp, u64, vp, sz, vp, sz, vp, i]
+        lib.oracle_l2acl.restype = u32
+        lib.oracle_l2acl.argtypes = [vp, u32, vp, sz]
+        lib.oracle_l2_classify_slots.restype = i
+        lib.oracle_l2_classify_slots.argtypes = [vp, u32, u64, vp, sz, vp, i]
+        lib.oracle_l2_classify_frames.restype = i
+        lib.oracle_l2_classify_frames.argtypes = [vp, vp, u64, vp, sz, vp, i]
+        assert lib.oracle_l2rule_size() == L2RULE_DTYPE.itemsize
         assert lib.oracle_rule4_size() == RULE4_DTYPE.itemsize
         assert lib.oracle_rule6_size() == RULE6_DTYPE.itemsize
         _lib = lib
@@ -97,4 +104,40 @@ def classify_frames(frames: np.ndarray, desc: np.ndarray, a4=None, a6=None, thre
                                     len(a4), a6.ctypes.data, len(a6), out.ctypes.data, threads)
     if st != 0:
         raise RuntimeError("oracle_classify_frames failed")
+    return out
+
+
+def _l2(eth):
+    return np.ascontiguousarray(eth if eth is not None else np.zeros(0, L2RULE_DTYPE)).view(L2RULE_DTYPE)
+
+
+def l2acl(packet: bytes, eth=None) -> int:
+    """L2ACLPort of one packet (bytes past len(packet) read as 0)."""
+    lib = _load()
+    eth = _l2(eth)
+    buf = np.frombuffer(bytes(packet) or b"\0", np.uint8)
+    return lib.oracle_l2acl(buf.ctypes.data, len(packet), eth.ctypes.data, len(eth))
+
+
+def l2_classify_slots(slots: np.ndarray, stride: int, n: int, eth=None, threads: int = 1) -> np.ndarray:
+    lib = _load()
+    eth = _l2(eth)
+    slots = np.ascontiguousarray(slots, np.uint8)
+    assert slots.size >= n * stride
+    out = np.zeros(n, np.uint32)
+    if lib.oracle_l2_classify_slots(slots.ctypes.data, stride, n, eth.ctypes.data, len(eth),
+                                    out.ctypes.data, threads) != 0:
+        raise RuntimeError("oracle_l2_classify_slots failed")
+    return out
+
+
+def l2_classify_frames(frames: np.ndarray, desc: np.ndarray, eth=None, threads: int = 1) -> np.ndarray:
+    lib = _load()
+    eth = _l2(eth)
+    frames = np.ascontiguousarray(frames, np.uint8)
+    desc = np.ascontiguousarray(desc, np.uint64)
+    out = np.zeros(len(desc), np.uint32)
+    if lib.oracle_l2_classify_frames(frames.ctypes.data, desc.ctypes.data, len(desc), eth.ctypes.data,
+                                     len(eth), out.ctypes.data, threads) != 0:
+        raise RuntimeError("oracle_l2_classify_frames failed")
     return out

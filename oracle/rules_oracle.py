@@ -12,6 +12,9 @@ go1.13.1):
   parseL4Port            packet/acl.go:357-383   strconv.ParseUint(s, 10, 16)
   parseRuleResult        packet/acl.go:385-398   strconv.ParseUint(s, 10, 32)
   parseAddr4/6           packet/acl.go:400-411   net.ParseCIDR -> LE uint32 / 16 bytes
+  GetL2ACLFromTextTable  packet/acl.go:88-117    (L2 rules, §8f next row)
+  GetL2ACLFromJSON       packet/acl.go:70-84
+  rawL2Parse             packet/acl.go:356-383   net.ParseMAC
 
 Pinning: the expected records of the reference's parse KATs
 (packet/acl_internal_test.go:91-161, via tests/golden/make_kats.py) and the
@@ -44,6 +47,10 @@ RULE4_DTYPE = np.dtype([("output_number", "<u4"), ("src_addr", "<u4"), ("dst_add
 RULE6_DTYPE = np.dtype([("output_number", "<u4"), ("src_addr", "u1", 16), ("dst_addr", "u1", 16),
                         ("src_mask", "u1", 16), ("dst_mask", "u1", 16)] + L4_FIELDS)
 assert RULE4_DTYPE.itemsize == 32 and RULE6_DTYPE.itemsize == 80
+L2RULE_DTYPE = np.dtype([("output_number", "<u4"), ("daddr_not_any", "u1"), ("saddr_not_any", "u1"),
+                         ("daddr", "u1", 6), ("saddr", "u1", 6), ("id_mask", "<u2"), ("id", "<u2"),
+                         ("reserved", "<u2")])
+assert L2RULE_DTYPE.itemsize == 24
 
 
 class OracleParseError(Exception):
@@ -381,9 +388,10 @@ def raw_l3_parse(raw: list) -> L3Rules:
     return rules
 
 
-def parse_text_table(data: bytes) -> L3Rules:
-    """GetL3ACLFromTextTable body over a file image (acl.go:156-177)."""
-    raw = []
+def _scan_table(data: bytes, nfields: int, incomplete: str) -> list:
+    """bufio.ScanLines + strings.Fields loop shared by both text loaders
+    (acl.go:97-112, 156-173)."""
+    rows = []
     lines = data.split(b"\n")
     if lines and lines[-1] == b"":
         lines.pop()  # ScanLines yields no empty final token
@@ -395,12 +403,17 @@ def parse_text_table(data: bytes) -> L3Rules:
         if len(line) == 0 or line[0:1] == b"#":
             continue
         f = go_fields(line)
-        if len(f) == 5:
+        if len(f) == nfields - 1:
             f.append(b"false")
-        elif len(f) != 6:
-            raise OracleParseError(PARSE_RULE_ERR, "Incomplete 5-tuple for rule parsing")
-        raw.append(tuple(f))
-    return raw_l3_parse(raw)
+        elif len(f) != nfields:
+            raise OracleParseError(PARSE_RULE_ERR, incomplete)
+        rows.append(tuple(f))
+    return rows
+
+
+def parse_text_table(data: bytes) -> L3Rules:
+    """GetL3ACLFromTextTable body over a file image (acl.go:156-177)."""
+    return raw_l3_parse(_scan_table(data, 6, "Incomplete 5-tuple for rule parsing"))
 
 
 def load_text_table(path) -> L3Rules:
@@ -419,24 +432,29 @@ def _reject_constant(name):
     raise ValueError(f"invalid JSON literal {name}")
 
 
-def parse_json(data: bytes) -> L3Rules:
-    """GetL3ACLFromJSON body (acl.go:129-133): json.Unmarshal into rawL3Rules
-    (exported fields matched case-insensitively, the last matching key wins,
-    null leaves the field as is, a non-string value is an UnmarshalTypeError),
-    then rawL3Parse."""
+def json_key_matches(key: str, field_name: str) -> bool:
+    """encoding/json field lookup (go1.13 fold.go): ASCII case folding, plus
+    U+017F (long s) for s and U+212A (Kelvin) for k."""
+    key = key.replace("\u017f", "s").replace("\u212a", "k")
+    return key.isascii() and key.lower() == field_name.lower()
+
+
+def _json_records(data: bytes, top: str, fields: tuple) -> list:
+    """json.Unmarshal of {top: [{field: string}]} (the last matching key wins,
+    null leaves the field as is, a non-string value is an UnmarshalTypeError)."""
     try:
         doc = json.loads(data.decode("utf-8", errors="replace"), parse_constant=_reject_constant,
                          object_pairs_hook=lambda pairs: ("obj", pairs))
     except ValueError as e:
         raise OracleParseError(PARSE_RULE_JSON_ERR, f"JSON error during rules parsing: {e}") from None
     if doc is None:
-        return L3Rules()
+        return []
     if not (isinstance(doc, tuple) and doc[0] == "obj"):
         raise OracleParseError(PARSE_RULE_JSON_ERR, "JSON error during rules parsing: not an object")
     type_error = False
     arr = None
     for k, v in doc[1]:
-        if k.lower() == "l3rules":
+        if json_key_matches(k, top):
             if v is None:
                 continue
             if not isinstance(v, list):
@@ -445,23 +463,29 @@ def parse_json(data: bytes) -> L3Rules:
             arr = v
     raw = []
     for elem in arr or []:
-        rec = {f: b"" for f in _JSON_FIELDS}
+        rec = {f: b"" for f in fields}
         if elem is not None and not (isinstance(elem, tuple) and elem[0] == "obj"):
             type_error = True
         elif elem is not None:
             for k, v in elem[1]:
-                for f in _JSON_FIELDS:
-                    if k.lower() == f.lower():
+                for f in fields:
+                    if json_key_matches(k, f):
                         if isinstance(v, str):
                             # lone surrogates from \u escapes -> U+FFFD, as Go does
                             rec[f] = v.encode("utf-16", "surrogatepass").decode("utf-16", "replace").encode("utf-8")
                         elif v is not None:
                             type_error = True
                         break
-        raw.append(tuple(rec[f] for f in _JSON_FIELDS))
+        raw.append(tuple(rec[f] for f in fields))
     if type_error:
         raise OracleParseError(PARSE_RULE_JSON_ERR, "JSON error during rules parsing: type mismatch")
-    return raw_l3_parse(raw)
+    return raw
+
+
+def parse_json(data: bytes) -> L3Rules:
+    """GetL3ACLFromJSON body (acl.go:129-133): json.Unmarshal into rawL3Rules,
+    then rawL3Parse."""
+    return raw_l3_parse(_json_records(data, "L3Rules", _JSON_FIELDS))
 
 
 def load_json(path) -> L3Rules:
@@ -471,3 +495,125 @@ def load_json(path) -> L3Rules:
     except OSError as e:
         raise OracleParseError(FILE_ERR, f"file error during rules parsing: {e}") from None
     return parse_json(data)
+
+
+# --------------------------------------------------------------------------
+# L2 rules (acl.go:68-117, 356-383)
+# --------------------------------------------------------------------------
+
+@dataclass
+class Rule2:
+    output_number: int = 0
+    daddr_not_any: bool = False
+    saddr_not_any: bool = False
+    daddr: bytes = bytes(6)
+    saddr: bytes = bytes(6)
+    id_mask: int = 0
+    id: int = 0
+
+
+@dataclass
+class L2Rules:
+    eth: list = field(default_factory=list)
+
+    def array(self) -> np.ndarray:
+        a = np.zeros(len(self.eth), L2RULE_DTYPE)
+        for i, r in enumerate(self.eth):
+            a[i] = (r.output_number, int(r.daddr_not_any), int(r.saddr_not_any),
+                    np.frombuffer(r.daddr, "u1"), np.frombuffer(r.saddr, "u1"), r.id_mask, r.id, 0)
+        return a
+
+
+_HEX = "0123456789abcdefABCDEF"
+
+
+def go_parse_mac(s: bytes):
+    """go1.13 net.ParseMAC: bytes of a 6/8/20-byte address, or None."""
+    s = s.decode("latin-1")  # byte-wise, as Go indexes the string
+
+    def two_hex(x: str):
+        if len(x) != 2 or x[0] not in _HEX or x[1] not in _HEX:
+            return None
+        return int(x, 16)
+
+    if len(s) < 14:
+        return None
+    out = []
+    if s[2] in ":-":
+        sep = s[2]
+        if (len(s) + 1) % 3:
+            return None
+        n = (len(s) + 1) // 3
+        if n not in (6, 8, 20):
+            return None
+        for i in range(n):
+            grp = s[3 * i:3 * i + 2]
+            if 3 * i + 2 < len(s) and s[3 * i + 2] != sep:
+                return None
+            b = two_hex(grp)
+            if b is None:
+                return None
+            out.append(b)
+    elif s[4] == ".":
+        if (len(s) + 1) % 5:
+            return None
+        n = 2 * (len(s) + 1) // 5
+        if n not in (6, 8, 20):
+            return None
+        for g in range(n // 2):
+            x = 5 * g
+            if x + 4 < len(s) and s[x + 4] != ".":
+                return None
+            hi, lo = two_hex(s[x:x + 2]), two_hex(s[x + 2:x + 4])
+            if hi is None or lo is None:
+                return None
+            out += [hi, lo]
+    else:
+        return None
+    return bytes(out)
+
+
+_L2_IDS = {
+    b"ANY": (0, 0),
+    **{k: (0x0800, 0xFFFF) for k in (b"ipv4", b"Ipv4", b"IPv4", b"IPV4", b"0x0800")},
+    **{k: (0x86DD, 0xFFFF) for k in (b"ipv6", b"Ipv6", b"IPv6", b"IPV6", b"0x86dd")},
+    **{k: (0x0806, 0xFFFF) for k in (b"arp", b"Arp", b"ARP", b"0x0806")},
+}
+
+
+def raw_l2_parse(raw: list) -> L2Rules:
+    """rawL2Parse (acl.go:356-383); raw items are (Rule, Source, Destination, ID)."""
+    rules = L2Rules()
+    for rule, src, dst, ident in raw:
+        r = Rule2(output_number=parse_rule_result(rule))
+        if src != b"ANY":
+            r.saddr_not_any = True
+            hw = go_parse_mac(src)
+            if hw is None:
+                raise OracleParseError(INCORRECT_ARG_IN_RULES, f"Incorrect source MAC: {src!r}")
+            r.saddr = hw[:6]
+        if dst != b"ANY":
+            r.daddr_not_any = True
+            hw = go_parse_mac(dst)
+            if hw is None:
+                raise OracleParseError(INCORRECT_ARG_IN_RULES, f"Incorrect destination MAC: {dst!r}")
+            r.daddr = hw[:6]
+        if ident not in _L2_IDS:
+            raise OracleParseError(INCORRECT_ARG_IN_RULES, f"Incorrect  L3 protocol ID: {ident!r}")
+        r.id, r.id_mask = _L2_IDS[ident]
+        rules.eth.append(r)
+    return rules
+
+
+def parse_l2_text_table(data: bytes) -> L2Rules:
+    """GetL2ACLFromTextTable body (acl.go:97-117): Source Destination ID [Rule]."""
+    rows = _scan_table(data, 4, "Incomplete 3-tuple for rule parsing")
+    return raw_l2_parse([(f[3], f[0], f[1], f[2]) for f in rows])
+
+
+_L2_JSON_FIELDS = ("Rule", "Source", "Destination", "ID")
+
+
+def parse_l2_json(data: bytes) -> L2Rules:
+    """GetL2ACLFromJSON body (acl.go:78-83)."""
+    return raw_l2_parse(_json_records(data, "L2Rules", _L2_JSON_FIELDS))

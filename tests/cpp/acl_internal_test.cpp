@@ -5,8 +5,10 @@
 // the same "want outNum iff every field is ok" rule.
 //
 //   ./acl_internal_test parse   TestGetL3ACLFromJSON, TestGetL3ACLFromTextTable (CPU)
-//   ./acl_internal_test match   TestInternal_l4ACL_*, TestInternal_l3ACL_* (GPU: every
-//                               verdict comes from libnffacl's HIP kernels)
+//   ./acl_internal_test match   TestInternal_l4ACL_*, TestInternal_l3ACL_*,
+//                               TestInternal_l2ACL_* (GPU: every verdict comes from
+//                               libnffacl's HIP kernels)
+//   L2: TestGetL2ACLFromJSON / TestGetL2ACLFromTextTable (parse, CPU)
 //
 // Test packets follow packet/utils_for_test.go:33-126 (InitEmpty*Packet +
 // initEtherAddrs/initIPv4Addrs/initIPv6Addrs/initPorts, payload 100 bytes).
@@ -415,7 +417,134 @@ static void TestVectorSeparatorStability(T &t) {
         agg.Push(cp, flow::vBurstSize, [&](const uint32_t *p, size_t n) { got.insert(got.end(), p, p + n); });
     agg.Flush();
     for (size_t i = 0; i < got.size(); ++i)
-        if ((got[i] != 0) != (i % 3 == 0)) t.Errorf("aggregator packet %zu: got %u", i, got[i]);
+        if ((got[i] != 0) != (i % flow::vBurstSize % 3 == 0)) t.Errorf("aggregator packet %zu: got %u", i, got[i]);
+    if (got.size() != 2 * flow::vBurstSize) t.Errorf("aggregator returned %zu verdicts", got.size());
+}
+
+// ---- L2 (acl_internal_test.go:66-89, 174-273, 1144-1273) -------------------------
+struct MacAddrTest { const char *raw; uint8_t addr[6]; bool notAny; };
+struct IdTest16 { const char *raw; uint16_t id, mask; };
+static const MacAddrTest l2srcs[] = {{"ANY", {0}, false}, {"00:11:22:33:44:55", {0x00, 0x11, 0x22, 0x33, 0x44, 0x55}, true}};
+static const MacAddrTest l2dsts[] = {{"ANY", {0}, false}, {"01:11:21:31:41:51", {0x01, 0x11, 0x21, 0x31, 0x41, 0x51}, true}};
+static const IdTest16 l2ids[] = {{"ANY", 0, 0}, {"IPv4", 0x0800, 0xffff}, {"IPv6", 0x86dd, 0xffff}, {"arp", 0x0806, 0xffff}};
+
+struct TestL2Rule { std::string Rule, Source, Destination, ID; nffacl_l2_rule want; };
+
+// generateTestL2Rules (:174-213); `orig` uses all four decisions (the
+// reference's text variant iterates a nil slice and tests nothing).
+static std::vector<TestL2Rule> generateTestL2Rules(bool orig) {
+    std::vector<TestL2Rule> table;
+    const int nd = orig ? 4 : 2;
+    for (int ri = 0; ri < nd; ++ri)
+        for (const MacAddrTest &src : l2srcs)
+            for (const MacAddrTest &dst : l2dsts)
+                for (const IdTest16 &id : l2ids) {
+                    nffacl_l2_rule w{};
+                    w.output_number = rules_ctx[ri].out;
+                    w.daddr_not_any = dst.notAny;
+                    w.saddr_not_any = src.notAny;
+                    std::memcpy(w.daddr, dst.addr, 6);
+                    std::memcpy(w.saddr, src.addr, 6);
+                    w.id_mask = id.mask;
+                    w.id = id.id;
+                    table.push_back(TestL2Rule{rules_ctx[ri].raw, src.raw, dst.raw, id.raw, w});
+                }
+    return table;
+}
+
+static void check_l2(T &t, const TestL2Rule &r, const packet::L2RulesOrError &got, const char *what) {
+    if (got.second) {
+        t.Errorf("%s returned error %s", what, got.second->Error().c_str());
+        return;
+    }
+    auto v = got.first->eth();
+    if (v.empty() || std::memcmp(&v[0], &r.want, sizeof r.want) != 0)
+        t.Errorf("Incorrect parse L2 rule %s %s %s %s", r.Source.c_str(), r.Destination.c_str(), r.ID.c_str(),
+                 r.Rule.c_str());
+}
+
+// TestGetL2ACLFromJSON (:217-243)
+static void TestGetL2ACLFromJSON(T &t) {
+    for (const TestL2Rule &r : generateTestL2Rules(false)) {
+        const std::string doc = "{\"L2Rules\":[{\"Rule\":\"" + r.Rule + "\",\"Source\":\"" + r.Source +
+                                "\",\"Destination\":\"" + r.Destination + "\",\"ID\":\"" + r.ID + "\"}]}";
+        const std::string f = tmpfile_with(doc, ".json");
+        check_l2(t, r, packet::GetL2ACLFromJSON(f), "GetL2ACLFromJSON");
+        std::remove(f.c_str());
+    }
+}
+
+// TestGetL2ACLFromTextTable (:247-273)
+static void TestGetL2ACLFromTextTable(T &t) {
+    for (const TestL2Rule &r : generateTestL2Rules(true)) {
+        const std::string text = "# Source MAC, Destination MAC, L3 ID, Output port\n" + r.Source + " " +
+                                 r.Destination + " " + r.ID + " " + r.Rule;
+        const std::string f = tmpfile_with(text, ".orig");
+        check_l2(t, r, packet::GetL2ACLFromTextTable(f), "GetL2ACLFromTextTable");
+        std::remove(f.c_str());
+    }
+}
+
+struct MacAddr { uint8_t addr[6]; bool notAny, ok; };
+struct IDMask16 { uint16_t id, mask; bool ok; };
+
+// getARPRequestTestPacket (utils_for_test.go:95-104 -> arp.go:79-93)
+static std::vector<uint8_t> arpRequestPacket() {
+    std::vector<uint8_t> p(types::EtherLen + 28, 0);
+    std::memset(&p[0], 0xff, 6);
+    std::memcpy(&p[6], kSMAC, 6);
+    p[12] = 0x08; p[13] = 0x06;
+    const uint8_t hdr[8] = {0, 1, 0x08, 0x00, 6, 4, 0, 1};  // HType, PType, HLen, PLen, Operation
+    std::memcpy(&p[14], hdr, 8);
+    std::memcpy(&p[22], kSMAC, 6);
+    const uint8_t spa[4] = {127, 0, 0, 1}, tpa[4] = {128, 9, 9, 5};
+    std::memcpy(&p[28], spa, 4);
+    std::memset(&p[32], 0xff, 6);
+    std::memcpy(&p[38], tpa, 4);
+    return p;
+}
+
+static void l2Table(T &t, const std::vector<uint8_t> &frame, const IDMask16 (&idMsk)[4], const MacAddr (&srcMac)[3],
+                    const MacAddr (&dstMac)[3]) {
+    packet::Packet pkt{frame.data(), static_cast<uint32_t>(frame.size())};
+    const uint32_t outs[] = {0, 1, 65535};
+    for (uint32_t outNum : outs)
+        for (const IDMask16 &im : idMsk)
+            for (const MacAddr &src : srcMac)
+                for (const MacAddr &dst : dstMac) {
+                    nffacl_l2_rule r{};
+                    r.output_number = outNum;
+                    r.saddr_not_any = src.notAny;
+                    r.daddr_not_any = dst.notAny;
+                    std::memcpy(r.saddr, src.addr, 6);
+                    std::memcpy(r.daddr, dst.addr, 6);
+                    r.id_mask = im.mask;
+                    r.id = im.id;
+                    auto rules = packet::L2Rules::FromRecords({r});
+                    const uint32_t got = pkt.L2ACLPort(*rules);
+                    const uint32_t want = (im.ok && src.ok && dst.ok) ? outNum : 0;
+                    if (got != want) t.Errorf("Incorrect result for rule out=%u id=%04x: got %u want %u", outNum, im.id, got, want);
+                }
+}
+
+// TestInternal_l2ACL_packetIPv4 (:1144-1207)
+static void TestInternal_l2ACL_packetIPv4(T &t) {
+    const IDMask16 idMsk[4] = {{0, 0, true}, {0x0800, 0xffff, true}, {0x86dd, 0xffff, false}, {0x0806, 0xffff, false}};
+    const MacAddr srcMac[3] = {{{0}, false, true}, {{0x01, 0x11, 0x21, 0x31, 0x41, 0x51}, true, true},
+                               {{0, 0x55, 0x55, 0x55, 0x55, 0}, true, false}};
+    const MacAddr dstMac[3] = {{{0}, false, true}, {{0x00, 0x11, 0x22, 0x33, 0x44, 0x55}, true, true},
+                               {{0x01, 0x11, 0x21, 0x31, 0x41, 0x51}, true, false}};
+    l2Table(t, ipv4Packet(types::UDPNumber, types::UDPLen, true), idMsk, srcMac, dstMac);
+}
+
+// TestInternal_l2ACL_packetARP (:1209-1273)
+static void TestInternal_l2ACL_packetARP(T &t) {
+    const IDMask16 idMsk[4] = {{0, 0, true}, {0x0800, 0xffff, false}, {0x86dd, 0xffff, false}, {0x0806, 0xffff, true}};
+    const MacAddr srcMac[3] = {{{0}, false, true}, {{0x01, 0x11, 0x21, 0x31, 0x41, 0x51}, true, true},
+                               {{0x0, 0x11, 0x22, 0x33, 0x44, 0x55}, true, false}};
+    const MacAddr dstMac[3] = {{{0}, false, true}, {{0xff, 0xff, 0xff, 0xff, 0xff, 0xff}, true, true},
+                               {{0x01, 0x11, 0x21, 0x31, 0x41, 0x51}, true, false}};
+    l2Table(t, arpRequestPacket(), idMsk, srcMac, dstMac);
 }
 
 int main(int argc, char **argv) {
@@ -424,6 +553,8 @@ int main(int argc, char **argv) {
         run("TestGetL3ACLFromJSON", TestGetL3ACLFromJSON);
         run("TestGetL3ACLFromTextTable", TestGetL3ACLFromTextTable);
         run("TestGetL3ACLErrors", TestGetL3ACLErrors);
+        run("TestGetL2ACLFromJSON", TestGetL2ACLFromJSON);
+        run("TestGetL2ACLFromTextTable", TestGetL2ACLFromTextTable);
     }
     if (which == "match" || which == "all") {
         run("TestInternal_l4ACL_packetIPv4_TCP", TestInternal_l4ACL_packetIPv4_TCP);
@@ -434,6 +565,8 @@ int main(int argc, char **argv) {
         run("TestInternal_l3ACL_l4ACL_packetIPv4_ICMP", TestInternal_l3ACL_l4ACL_packetIPv4_ICMP);
         run("TestInternal_l3ACL_l4ACL_packetIPv6_ICMP", TestInternal_l3ACL_l4ACL_packetIPv6_ICMP);
         run("TestVectorSeparatorStability", TestVectorSeparatorStability);
+        run("TestInternal_l2ACL_packetIPv4", TestInternal_l2ACL_packetIPv4);
+        run("TestInternal_l2ACL_packetARP", TestInternal_l2ACL_packetARP);
     }
     std::printf(g_failed ? "FAIL\n" : "ok\n");
     return g_failed ? 1 : 0;

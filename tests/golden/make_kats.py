@@ -10,12 +10,17 @@ Sources (aregm/nff-go, read as text):
   packet/acl_internal_test.go:266-370   generateTestL3Rules cartesian product
   packet/acl_internal_test.go:501-1141  match KATs (l4ACL + six l3ACL tables)
   packet/packet_test.go:22-267          header-parse KAT (8 hex frames)
+  packet/acl_internal_test.go:66-89, 174-243   L2 parse KAT (rulesL2Ctxt, generateTestL2Rules)
+  packet/acl_internal_test.go:1144-1273 L2 match KATs (IPv4 UDP and ARP request packets)
+  packet/utils_for_test.go:95-104, packet/arp.go:60-93   ARP request test packet,
+  packet/arp_test.go:22                 its layout pinned by gtLineARPRequest
 
 Outputs:
   kat_packets.json    the test packets as hex
   acl_match_kats.npz  7369 (packet, single-rule table, expected port) cases
   parse_kats.json     (rule-file line, expected ip4/ip6 record) cases
   parse_l3_kat.json   8 frames + the header fields packet_test.go expects
+  l2_kats.json        L2 parse cases (JSON + text) and the 216 L2 match cases
 
 Run:  python tests/golden/make_kats.py   (deterministic; no inputs)
 """
@@ -218,6 +223,78 @@ def parse_l3_kat():
     return out
 
 
+# ---- L2 (acl_internal_test.go:66-89, 174-243, 1144-1273) -------------------------
+BCAST = bytes([0xff] * 6)
+
+
+def arp_request(sha: bytes, spa: bytes, tpa: bytes) -> bytes:
+    """InitARPRequestPacket (arp.go:79-93 over initARPCommonData :60-73 and
+    InitEmptyARPPacket packet.go:563-573): Ether + 28-byte ARP, fresh mbuf zeros."""
+    eth = BCAST + sha + b"\x08\x06"
+    arp = struct.pack(">HHBBH", 1, 0x0800, 6, 4, 1) + sha + spa + BCAST + tpa
+    return eth + arp
+
+
+# arp_test.go:22 (gtLineARPRequest, made with gopacket) for the parameters of
+# TestInitARPCommonDataPacket / TestInitARPRequestPacket: pins arp_request().
+GT_ARP_REQUEST = "ffffffffffff00070daff4540806000108000604000100070daff45418a6ac01ffffffffffff18a6ad9f"
+assert arp_request(bytes.fromhex("00070daff454"), bytes([24, 166, 172, 1]),
+                   bytes([24, 166, 173, 159])).hex() == GT_ARP_REQUEST
+
+# getARPRequestTestPacket (utils_for_test.go:95-104)
+PACKETS["arp_request"] = arp_request(SMAC, V4_SRC, V4_DST)
+
+L2_RULES = [("Accept", 1), ("Reject", 0), ("3", 3), ("", 0)]  # "" only in the text format
+L2_SRCS = [("ANY", bytes(6), False), ("00:11:22:33:44:55", DMAC, True)]
+L2_DSTS = [("ANY", bytes(6), False), ("01:11:21:31:41:51", SMAC, True)]
+L2_IDS = [("ANY", 0, 0), ("IPv4", 0x0800, 0xffff), ("IPv6", 0x86dd, 0xffff), ("arp", 0x0806, 0xffff)]
+
+
+def l2_parse_cases():
+    """generateTestL2Rules: JSON over decisions = rules[:2] (the reference's
+    text-format test iterates an empty decision list, :180-182, so the text
+    cases here reuse all four decisions — an extension, not a transcription)."""
+    cases = []
+    for fmt, decisions in (("json", L2_RULES[:2]), ("text", L2_RULES)):
+        for rr, gout in decisions:
+            for s in L2_SRCS:
+                for d in L2_DSTS:
+                    for rid, gid, gmask in L2_IDS:
+                        cases.append(dict(
+                            format=fmt, raw=dict(Rule=rr, Source=s[0], Destination=d[0], ID=rid),
+                            want=dict(output_number=gout, daddr_not_any=d[2], saddr_not_any=s[2],
+                                      daddr=d[1].hex(), saddr=s[1].hex(), id_mask=gmask, id=gid)))
+    return cases
+
+
+def l2_match_cases():
+    """TestInternal_l2ACL_packetIPv4 / _packetARP (:1144-1273): one single-rule
+    table per (output, id, src, dst) combination; want = output iff all ok."""
+    outs = [0, 1, 65535]
+    tables = {
+        "ipv4_udp": (
+            [(0, 0, True), (0x0800, 0xffff, True), (0x86dd, 0xffff, False), (0x0806, 0xffff, False)],
+            [(bytes(6), False, True), (SMAC, True, True), (bytes([0, 0x55, 0x55, 0x55, 0x55, 0]), True, False)],
+            [(bytes(6), False, True), (DMAC, True, True), (SMAC, True, False)]),
+        "arp_request": (
+            [(0, 0, True), (0x0800, 0xffff, False), (0x86dd, 0xffff, False), (0x0806, 0xffff, True)],
+            [(bytes(6), False, True), (SMAC, True, True), (DMAC, True, False)],
+            [(bytes(6), False, True), (BCAST, True, True), (SMAC, True, False)]),
+    }
+    cases = []
+    for pkt, (ids, srcs, dsts) in tables.items():
+        for out in outs:
+            for idv, idm, idok in ids:
+                for sa, sna, sok in srcs:
+                    for da, dna, dok in dsts:
+                        cases.append(dict(
+                            packet=pkt,
+                            rule=dict(output_number=out, daddr_not_any=dna, saddr_not_any=sna,
+                                      daddr=da.hex(), saddr=sa.hex(), id_mask=idm, id=idv),
+                            want=out if (idok and sok and dok) else 0))
+    return cases
+
+
 def main():
     (HERE / "kat_packets.json").write_text(json.dumps({k: v.hex() for k, v in PACKETS.items()}, indent=1) + "\n")
     c4, c6 = match_cases()
@@ -237,8 +314,13 @@ def main():
     (HERE / "parse_kats.json").write_text(
         "[\n" + ",\n".join(json.dumps(c, separators=(",", ":")) for c in parse_cases()) + "\n]\n")
     (HERE / "parse_l3_kat.json").write_text(json.dumps(parse_l3_kat(), indent=1) + "\n")
+    l2 = dict(parse=l2_parse_cases(), match=l2_match_cases())
+    (HERE / "l2_kats.json").write_text(
+        "{\"parse\": [\n" + ",\n".join(json.dumps(c, separators=(",", ":")) for c in l2["parse"]) +
+        "\n], \"match\": [\n" + ",\n".join(json.dumps(c, separators=(",", ":")) for c in l2["match"]) + "\n]}\n")
     print(f"match KATs: {len(c4)} ipv4 + {len(c6)} ipv6 = {len(c4) + len(c6)}; "
-          f"parse KATs: {len(parse_cases())}; parse-L3 frames: {len(PARSE_LINES)}")
+          f"parse KATs: {len(parse_cases())}; parse-L3 frames: {len(PARSE_LINES)}; "
+          f"L2 parse: {len(l2['parse'])}, L2 match: {len(l2['match'])}")
 
 
 if __name__ == "__main__":

@@ -26,7 +26,9 @@ def _run(binary, which):
 
 def test_cpp_parse_tests(binary):
     out = _run(binary, "parse")
-    assert "--- PASS: TestGetL3ACLFromTextTable" in out and "--- PASS: TestGetL3ACLFromJSON" in out
+    for name in ("TestGetL3ACLFromTextTable", "TestGetL3ACLFromJSON", "TestGetL3ACLErrors",
+                 "TestGetL2ACLFromJSON", "TestGetL2ACLFromTextTable"):
+        assert f"--- PASS: {name}" in out, out
 
 
 @pytest.mark.gpu
@@ -35,5 +37,6 @@ def test_cpp_match_tests(binary):
     for name in ("TestInternal_l4ACL_packetIPv4_TCP", "TestInternal_l3ACL_packetIPv4_TCP",
                  "TestInternal_l3ACL_l4ACL_packetIPv4_TCP", "TestInternal_l3ACL_l4ACL_packetIPv6_TCP",
                  "TestInternal_l3ACL_l4ACL_packetIPv6_UDP", "TestInternal_l3ACL_l4ACL_packetIPv4_ICMP",
-                 "TestInternal_l3ACL_l4ACL_packetIPv6_ICMP", "TestVectorSeparatorStability"):
+                 "TestInternal_l3ACL_l4ACL_packetIPv6_ICMP", "TestVectorSeparatorStability",
+                 "TestInternal_l2ACL_packetIPv4", "TestInternal_l2ACL_packetARP"):
         assert f"--- PASS: {name}" in out, out
