@@ -209,6 +209,16 @@ NFFACL_API int nffacl_table_compile(const nffacl_rules *rules, int algo, uint32_
 
 /* ---- classification ------------------------------------------------------ */
 
+/* Parse flags (the *_ex entry points).  0 = the reference's l3ACL exactly. */
+enum nffacl_parse_flags {
+    /* Parse L3 with ParseAllKnownL3CheckVLAN (packet/vlan.go:104-117) instead
+     * of ParseAllKnownL3: one 802.1Q tag (EtherType 0x8100) moves the L3
+     * header 4 bytes and the tag's EtherType selects IPv4/IPv6.  The
+     * reference's L3ACLPermit never does this (a tagged frame gets 0); the
+     * flag serves pipelines that composed the VLAN-aware parse themselves. */
+    NFFACL_PARSE_VLAN = 1u
+};
+
 /* Device-resident dense slots: packet i occupies d_slots[i*stride, (i+1)*stride)
  * with its frame starting at byte 0 (the Ether header) and zero padding after
  * the frame.  stride % 16 == 0, stride >= 64, d_slots 16-byte aligned.
@@ -227,11 +237,21 @@ NFFACL_API int nffacl_classify_frames_device(nffacl_engine *eng, const uint8_t *
                                   const uint64_t *d_desc, uint64_t n, uint32_t *d_port,
                                   uint64_t *d_permit_bits, void *stream);
 
+/* The same with parse flags (enum nffacl_parse_flags). */
+NFFACL_API int nffacl_classify_device_ex(nffacl_engine *eng, const uint8_t *d_slots, uint32_t stride,
+                                         uint64_t n, uint32_t *d_port, uint64_t *d_permit_bits,
+                                         void *stream, uint32_t flags);
+NFFACL_API int nffacl_classify_frames_device_ex(nffacl_engine *eng, const uint8_t *d_frames,
+                                                const uint64_t *d_desc, uint64_t n, uint32_t *d_port,
+                                                uint64_t *d_permit_bits, void *stream, uint32_t flags);
+
 /* Host slots in, host verdicts out: pinned staging + async H2D / kernel / D2H,
  * double-buffered across chunks.  Synchronous.  h_port / h_permit may be NULL
  * (h_permit gets one byte per packet, 0 or 1). */
 NFFACL_API int nffacl_classify_host(nffacl_engine *eng, const uint8_t *h_slots, uint32_t stride,
                          uint64_t n, uint32_t *h_port, uint8_t *h_permit);
+NFFACL_API int nffacl_classify_host_ex(nffacl_engine *eng, const uint8_t *h_slots, uint32_t stride,
+                                       uint64_t n, uint32_t *h_port, uint8_t *h_permit, uint32_t flags);
 
 /* ---- burst aggregator (host ingest) ----------------
  *
@@ -310,7 +330,13 @@ NFFACL_API void nffacl_l2rules_free(nffacl_l2rules *rules);
 NFFACL_API int nffacl_l2rules_count(const nffacl_l2rules *rules, size_t *n);
 NFFACL_API int nffacl_l2rules_get(const nffacl_l2rules *rules, size_t i, nffacl_l2_rule *out);
 
+/* algo: NFFACL_ALGO_LINEAR (file-order scan) or NFFACL_ALGO_INDEXED (one hashed
+ * probe per rule shape; AUTO picks it when the rules use <= 8 distinct
+ * MAC/EtherType mask shapes, which every parsed rule file does). */
 NFFACL_API int nffacl_l2_engine_create(int hip_device, const nffacl_l2rules *rules, nffacl_l2engine **out);
+NFFACL_API int nffacl_l2_engine_create_ex(int hip_device, const nffacl_l2rules *rules, int algo,
+                                          nffacl_l2engine **out);
+NFFACL_API int nffacl_l2_engine_algo(const nffacl_l2engine *eng);
 NFFACL_API int nffacl_l2_engine_swap_rules(nffacl_l2engine *eng, const nffacl_l2rules *rules);
 NFFACL_API void nffacl_l2_engine_destroy(nffacl_l2engine *eng);
 

@@ -4,6 +4,8 @@
 // the bursts' submitters.
 #include "batcher.hpp"
 
+#include <sys/prctl.h>
+
 #include <algorithm>
 #include <cstring>
 #include <new>
@@ -16,14 +18,17 @@ using Clock = std::chrono::steady_clock;
 
 namespace {
 
+// Mapped (device-addressable) and coherent (fine-grained): the GPU reads the
+// slots the CPU just wrote and the CPU reads the verdicts, with no cache
+// maintenance between batches.
+constexpr unsigned kHostFlags = hipHostMallocMapped | hipHostMallocCoherent;
+
 void release_buffers(nffacl_batcher *b) {
     if (!b->bufs) return;
     for (uint32_t i = 0; i < b->nbuf; ++i) {
         BatchBuf &x = b->bufs[i];
         if (x.h_slots) (void)hipHostFree(x.h_slots);
         if (x.h_port) (void)hipHostFree(x.h_port);
-        if (x.d_slots) (void)hipFree(x.d_slots);
-        if (x.d_port) (void)hipFree(x.d_port);
         if (x.stream) (void)hipStreamDestroy(x.stream);
         if (x.done) (void)hipEventDestroy(x.done);
     }
@@ -45,18 +50,16 @@ void launch_one(nffacl_batcher *b, std::unique_lock<std::mutex> &lk) {
     b->launch_idx = (i + 1) % b->nbuf;
     lk.unlock();
     while (x.written.load(std::memory_order_acquire) < n) std::this_thread::yield();  // copies in progress
-    int st = NFFACL_OK;
-    hipError_t e = hipMemcpyAsync(x.d_slots, x.h_slots, size_t(n) * b->stride, hipMemcpyHostToDevice, x.stream);
-    if (e == hipSuccess) {
-        st = launch_slots(b->eng, acquire_table(b->eng), x.d_slots, b->stride, n, x.d_port, nullptr, x.stream);
-        if (st == NFFACL_OK) e = hipMemcpyAsync(x.h_port, x.d_port, size_t(n) * 4, hipMemcpyDeviceToHost, x.stream);
-        if (st == NFFACL_OK && e == hipSuccess) e = hipEventRecord(x.done, x.stream);
-    }
+    // zero-copy: the kernel reads the mapped slots and writes the mapped ports
+    hipError_t e = hipSuccess;
+    int st = launch_slots(b->eng, acquire_table(b->eng), x.d_slots, b->stride, n, x.d_port, nullptr, x.stream);
+    if (st == NFFACL_OK) e = hipEventRecord(x.done, x.stream);
     lk.lock();
     if (e != hipSuccess || st != NFFACL_OK) {
         if (e != hipSuccess) set_last_error(std::string("batcher launch: ") + hipGetErrorString(e));
         b->error = st != NFFACL_OK ? st : NFFACL_ERR_HIP;
         x.state = BatchBuf::DONE;  // wake the waiters with the error
+        x.done_seq.store(x.seq, std::memory_order_release);
         b->cv_done.notify_all();
         return;
     }
@@ -69,6 +72,7 @@ void launch_one(nffacl_batcher *b, std::unique_lock<std::mutex> &lk) {
 
 void launcher_main(nffacl_batcher *b) {
     (void)hipSetDevice(b->eng->device);
+    (void)prctl(PR_SET_TIMERSLACK, 1000UL);  // µs-scale deadlines, not the default 50 µs slack
     std::unique_lock<std::mutex> lk(b->mu);
     while (true) {
         BatchBuf &x = b->bufs[b->launch_idx];
@@ -77,13 +81,21 @@ void launcher_main(nffacl_batcher *b) {
             continue;
         }
         if (x.state == BatchBuf::OPEN && x.count > 0) {
-            const auto deadline = x.opened + b->max_delay;
-            if (b->stop || Clock::now() >= deadline) {
+            // ship when the batch is old enough or its producers went quiet
+            const auto deadline = std::min(x.opened + b->max_delay, b->last_submit + b->idle);
+            const auto now = Clock::now();
+            if (b->stop || now >= deadline) {
                 if (!b->stop) ++b->timeouts;
                 seal_open(b);  // open_idx == launch_idx here
                 continue;
             }
-            b->cv_work.wait_until(lk, deadline);
+            if (deadline - now < std::chrono::microseconds(50)) {  // short: spin, no sleep
+                lk.unlock();
+                std::this_thread::yield();
+                lk.lock();
+            } else {
+                b->cv_work.wait_until(lk, deadline);
+            }
             continue;
         }
         if (b->stop) break;
@@ -95,13 +107,15 @@ void launcher_main(nffacl_batcher *b) {
 
 void completer_main(nffacl_batcher *b) {
     (void)hipSetDevice(b->eng->device);
+    (void)prctl(PR_SET_TIMERSLACK, 1000UL);
     std::unique_lock<std::mutex> lk(b->mu);
     while (true) {
         b->cv_inflight.wait(lk, [&] { return !b->inflight.empty() || b->launcher_done; });
         if (b->inflight.empty()) break;
         const uint32_t i = b->inflight.front();
         lk.unlock();
-        const hipError_t e = hipEventSynchronize(b->bufs[i].done);
+        hipError_t e;
+        while ((e = hipEventQuery(b->bufs[i].done)) == hipErrorNotReady) std::this_thread::yield();  // poll: no interrupt wake-up latency
         lk.lock();
         b->inflight.pop_front();
         if (e != hipSuccess) {
@@ -110,6 +124,7 @@ void completer_main(nffacl_batcher *b) {
         }
         BatchBuf &x = b->bufs[i];
         x.state = BatchBuf::DONE;
+        x.done_seq.store(x.seq, std::memory_order_release);
         if (x.readers == 0) {
             x.state = BatchBuf::FREE;
             b->cv_free.notify_all();
@@ -133,6 +148,7 @@ int nffacl_batcher_create(nffacl_engine *eng, uint32_t stride, uint32_t max_batc
     b->stride = stride;
     b->max_batch = max_batch;
     b->max_delay = std::chrono::microseconds(max_delay_us);
+    b->idle = std::chrono::microseconds(std::max<uint32_t>(2, max_delay_us / 8));
     b->nbuf = nbuf;
     b->bufs.reset(new (std::nothrow) BatchBuf[nbuf]);
     if (!b->bufs) {
@@ -141,10 +157,10 @@ int nffacl_batcher_create(nffacl_engine *eng, uint32_t stride, uint32_t max_batc
     }
     for (uint32_t i = 0; i < nbuf; ++i) {
         BatchBuf &x = b->bufs[i];
-        hipError_t e = hipHostMalloc(reinterpret_cast<void **>(&x.h_slots), size_t(max_batch) * stride, hipHostMallocDefault);
-        if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&x.h_port), size_t(max_batch) * 4, hipHostMallocDefault);
-        if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&x.d_slots), size_t(max_batch) * stride);
-        if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&x.d_port), size_t(max_batch) * 4);
+        hipError_t e = hipHostMalloc(reinterpret_cast<void **>(&x.h_slots), size_t(max_batch) * stride, kHostFlags);
+        if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&x.h_port), size_t(max_batch) * 4, kHostFlags);
+        if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void **>(&x.d_slots), x.h_slots, 0);
+        if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void **>(&x.d_port), x.h_port, 0);
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&x.stream, hipStreamNonBlocking);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&x.done, hipEventDisableTiming);
         if (e != hipSuccess) {
@@ -188,7 +204,8 @@ int nffacl_batcher_submit(nffacl_batcher *b, const uint8_t *const *frames, const
         }
         x = &cur;
         off = cur.count;
-        if (off == 0) cur.opened = Clock::now();
+        b->last_submit = Clock::now();
+        if (off == 0) cur.opened = b->last_submit;
         cur.count += n;
         ++cur.readers;
         ++b->bursts;
@@ -212,8 +229,13 @@ int nffacl_batcher_wait(nffacl_batcher *b, const nffacl_ticket *t, uint32_t *por
     if (!b || !t) return NFFACL_ERR_INVALID_ARG;
     if (t->n == 0) return NFFACL_OK;
     if (t->buf >= b->nbuf) return NFFACL_ERR_INVALID_ARG;
-    std::unique_lock<std::mutex> lk(b->mu);
     BatchBuf &x = b->bufs[t->buf];
+    // spin first (the reference's flow-function clones busy-poll their cores),
+    // then block
+    const auto spin_until = Clock::now() + std::chrono::microseconds(500);
+    while (x.done_seq.load(std::memory_order_acquire) != t->seq && Clock::now() < spin_until)
+        std::this_thread::yield();
+    std::unique_lock<std::mutex> lk(b->mu);
     if (x.seq != t->seq || x.state == BatchBuf::FREE) return NFFACL_ERR_INVALID_ARG;
     b->cv_done.wait(lk, [&] { return x.state == BatchBuf::DONE; });
     const int st = b->error;

@@ -8,8 +8,9 @@
 // is full or its oldest burst has waited `max_delay_us`, and each clone blocks
 // only until its own batch's verdicts are back.
 //
-// Buffers: `nbuf` batch buffers, each = pinned slots + pinned ports on the host,
-// slots + ports in HBM, a stream and an event.  States cycle
+// Buffers: `nbuf` batch buffers, each = mapped pinned slots + ports on the host
+// (the kernel reads the slots and writes the verdicts over PCIe directly:
+// one launch per batch, no copies), a stream and an event.  States cycle
 //   FREE -> OPEN (accepting bursts) -> SEALED -> LAUNCHED -> DONE -> FREE
 // (DONE -> FREE once every burst of the batch has collected its verdicts).
 #pragma once
@@ -38,10 +39,11 @@ struct BatchBuf {
     uint32_t count = 0;     // packets reserved
     uint32_t readers = 0;   // bursts that have not collected their verdicts yet
     std::atomic<uint32_t> written{0};  // packets whose bytes are in h_slots
+    std::atomic<uint64_t> done_seq{0}; // == seq once the verdicts are in h_port
     std::chrono::steady_clock::time_point opened;
-    uint8_t *h_slots = nullptr;
+    uint8_t *h_slots = nullptr;   // mapped pinned host memory
     uint32_t *h_port = nullptr;
-    uint8_t *d_slots = nullptr;
+    uint8_t *d_slots = nullptr;   // device aliases of h_slots / h_port
     uint32_t *d_port = nullptr;
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
@@ -53,7 +55,9 @@ struct nffacl_batcher {
     nffacl_engine *eng = nullptr;
     uint32_t stride = 64;
     uint32_t max_batch = 0;
-    std::chrono::microseconds max_delay{100};
+    std::chrono::microseconds max_delay{100};  // since the batch's first burst
+    std::chrono::microseconds idle{10};        // since the batch's last burst
+    std::chrono::steady_clock::time_point last_submit;
     uint32_t nbuf = 0;
     std::unique_ptr<nffacl::BatchBuf[]> bufs;
 

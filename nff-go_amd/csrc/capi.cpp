@@ -303,9 +303,16 @@ int nffacl_engine_table_bytes(const nffacl_engine *eng, uint64_t *bytes) {
 
 // ---- classification ---------------------------------------------------------
 
+static bool flags_ok(uint32_t flags) { return (flags & ~uint32_t(NFFACL_PARSE_VLAN)) == 0; }
+
 int nffacl_classify_device(nffacl_engine *eng, const uint8_t *d_slots, uint32_t stride, uint64_t n,
                            uint32_t *d_port, uint64_t *d_permit_bits, void *stream) {
-    if (!eng) return NFFACL_ERR_INVALID_ARG;
+    return nffacl_classify_device_ex(eng, d_slots, stride, n, d_port, d_permit_bits, stream, 0);
+}
+
+int nffacl_classify_device_ex(nffacl_engine *eng, const uint8_t *d_slots, uint32_t stride, uint64_t n,
+                              uint32_t *d_port, uint64_t *d_permit_bits, void *stream, uint32_t flags) {
+    if (!eng || !flags_ok(flags)) return NFFACL_ERR_INVALID_ARG;
     if (n == 0) return NFFACL_OK;
     if (!d_slots || stride < 64 || (stride % 16) != 0 ||
         (reinterpret_cast<uintptr_t>(d_slots) % 16) != 0)
@@ -313,19 +320,25 @@ int nffacl_classify_device(nffacl_engine *eng, const uint8_t *d_slots, uint32_t 
     if (!d_port && !d_permit_bits) return NFFACL_OK;
     HIP_CHECK(hipSetDevice(eng->device));
     return launch_slots(eng, acquire_table(eng), d_slots, stride, n, d_port, d_permit_bits,
-                        static_cast<hipStream_t>(stream));
+                        static_cast<hipStream_t>(stream), flags);
 }
 
 int nffacl_classify_frames_device(nffacl_engine *eng, const uint8_t *d_frames, const uint64_t *d_desc,
                                   uint64_t n, uint32_t *d_port, uint64_t *d_permit_bits, void *stream) {
-    if (!eng) return NFFACL_ERR_INVALID_ARG;
+    return nffacl_classify_frames_device_ex(eng, d_frames, d_desc, n, d_port, d_permit_bits, stream, 0);
+}
+
+int nffacl_classify_frames_device_ex(nffacl_engine *eng, const uint8_t *d_frames, const uint64_t *d_desc,
+                                     uint64_t n, uint32_t *d_port, uint64_t *d_permit_bits, void *stream,
+                                     uint32_t flags) {
+    if (!eng || !flags_ok(flags)) return NFFACL_ERR_INVALID_ARG;
     if (n == 0) return NFFACL_OK;
     if (!d_frames || !d_desc || (reinterpret_cast<uintptr_t>(d_frames) % 16) != 0)
         return NFFACL_ERR_INVALID_ARG;
     if (!d_port && !d_permit_bits) return NFFACL_OK;
     HIP_CHECK(hipSetDevice(eng->device));
     return launch_frames(eng, acquire_table(eng), d_frames, d_desc, n, d_port, d_permit_bits,
-                         static_cast<hipStream_t>(stream));
+                         static_cast<hipStream_t>(stream), flags);
 }
 
 // Staging sized to the request: small bursts get small pinned buffers, large
@@ -358,7 +371,12 @@ static int ensure_host_pipeline(nffacl_engine *eng, uint32_t stride, uint64_t n)
 
 int nffacl_classify_host(nffacl_engine *eng, const uint8_t *h_slots, uint32_t stride, uint64_t n,
                          uint32_t *h_port, uint8_t *h_permit) {
-    if (!eng) return NFFACL_ERR_INVALID_ARG;
+    return nffacl_classify_host_ex(eng, h_slots, stride, n, h_port, h_permit, 0);
+}
+
+int nffacl_classify_host_ex(nffacl_engine *eng, const uint8_t *h_slots, uint32_t stride, uint64_t n,
+                            uint32_t *h_port, uint8_t *h_permit, uint32_t flags) {
+    if (!eng || !flags_ok(flags)) return NFFACL_ERR_INVALID_ARG;
     if (n == 0) return NFFACL_OK;
     if (!h_slots || stride < 64 || (stride % 16) != 0) return NFFACL_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> g(eng->host_mu);
@@ -393,7 +411,7 @@ int nffacl_classify_host(nffacl_engine *eng, const uint8_t *h_slots, uint32_t st
             src = eng->h_stage[b];
         }
         HIP_CHECK(hipMemcpyAsync(eng->d_slots[b], src, cnt * stride, hipMemcpyHostToDevice, eng->streams[b]));
-        st = launch_slots(eng, t, eng->d_slots[b], stride, cnt, eng->d_port[b], nullptr, eng->streams[b]);
+        st = launch_slots(eng, t, eng->d_slots[b], stride, cnt, eng->d_port[b], nullptr, eng->streams[b], flags);
         if (st != NFFACL_OK) return st;
         HIP_CHECK(hipMemcpyAsync(eng->h_port[b], eng->d_port[b], cnt * 4, hipMemcpyDeviceToHost, eng->streams[b]));
         HIP_CHECK(hipEventRecord(eng->done[b], eng->streams[b]));
@@ -446,7 +464,18 @@ int nffacl_l2rules_get(const nffacl_l2rules *rules, size_t i, nffacl_l2_rule *ou
 }
 
 int nffacl_l2_engine_create(int hip_device, const nffacl_l2rules *rules, nffacl_l2engine **out) {
+    return nffacl_l2_engine_create_ex(hip_device, rules, NFFACL_ALGO_AUTO, out);
+}
+
+int nffacl_l2_engine_algo(const nffacl_l2engine *eng) {
+    if (!eng || !eng->active) return NFFACL_ERR_INVALID_ARG;
+    return eng->active->meta.algo;
+}
+
+int nffacl_l2_engine_create_ex(int hip_device, const nffacl_l2rules *rules, int algo, nffacl_l2engine **out) {
     if (!rules || !out) return NFFACL_ERR_INVALID_ARG;
+    if (algo != NFFACL_ALGO_AUTO && algo != NFFACL_ALGO_LINEAR && algo != NFFACL_ALGO_INDEXED)
+        return NFFACL_ERR_INVALID_ARG;
     *out = nullptr;
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
@@ -456,14 +485,17 @@ int nffacl_l2_engine_create(int hip_device, const nffacl_l2rules *rules, nffacl_
     }
     if (hip_device < 0 || hip_device >= count) return NFFACL_ERR_INVALID_ARG;
     HIP_CHECK(hipSetDevice(hip_device));
+    int pst = l2_prepare_kernels();
+    if (pst != NFFACL_OK) return pst;
     nffacl_l2engine *eng = new (std::nothrow) nffacl_l2engine();
     if (!eng) return NFFACL_ERR_NOMEM;
     eng->device = hip_device;
+    eng->algo_req = algo;
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, hip_device) == hipSuccess && cus > 0)
         eng->num_cus = cus;
     L2Table *t = nullptr;
-    int st = upload_l2(hip_device, *rules, t);
+    int st = upload_l2(hip_device, *rules, algo, t);
     if (st != NFFACL_OK) {
         delete eng;
         return st;
@@ -476,7 +508,7 @@ int nffacl_l2_engine_create(int hip_device, const nffacl_l2rules *rules, nffacl_
 int nffacl_l2_engine_swap_rules(nffacl_l2engine *eng, const nffacl_l2rules *rules) {
     if (!eng || !rules) return NFFACL_ERR_INVALID_ARG;
     L2Table *t = nullptr;
-    int st = upload_l2(eng->device, *rules, t);
+    int st = upload_l2(eng->device, *rules, eng->algo_req, t);
     if (st != NFFACL_OK) return st;
     L2Table *old_retired = nullptr;
     {

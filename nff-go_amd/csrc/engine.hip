@@ -74,9 +74,23 @@ struct Fields {
 // the slot/frame end as 0) for the rare IPv4 header whose IHL != 5 puts the L4
 // ports somewhere other than bytes 34..37; it runs in a divergent branch that
 // only lanes with IP options take.
+// `vlan` (wave-uniform launch flag NFFACL_PARSE_VLAN) selects
+// ParseAllKnownL3CheckVLAN (packet/vlan.go:104-117) over ParseAllKnownL3: a
+// frame whose EtherType is 0x8100 has its L3 header 4 bytes (one dword) later
+// and the tag's EtherType decides the family, so a tagged lane shifts d[3..14]
+// down by one dword and parses as usual (d[15] is never read afterwards).
 template <class FarDwords>
-__device__ __forceinline__ void parse_fields(const uint32_t (&d)[16], bool live, Fields &f,
-                                             FarDwords far) {
+__device__ __forceinline__ void parse_fields(uint32_t (&d)[16], bool live, Fields &f, FarDwords far,
+                                             bool vlan) {
+    uint32_t l3dw = 3u;  // dword holding the first L3 byte (at byte 2 of it)
+    if (vlan) {
+        const bool tagged = (d[3] & 0xFFFFu) == 0x0081u;  // 0x8100 on the wire
+        if (ballot(tagged)) {
+#pragma unroll
+            for (int k = 3; k < 15; ++k) d[k] = tagged ? d[k + 1] : d[k];
+            l3dw = tagged ? 4u : 3u;
+        }
+    }
     // ParseAllKnownL3: EtherType at wire bytes 12-13 (packet.go:238-243, 264-269)
     const uint32_t et = d[3] & 0xFFFFu;
     f.is4 = live && et == 0x0008u;  // 0x0800 on the wire
@@ -87,7 +101,7 @@ __device__ __forceinline__ void parse_fields(const uint32_t (&d)[16], bool live,
     uint32_t pw = f.is6 ? funnel16(d[14], d[13]) : funnel16(d[9], d[8]);
     if (f.is4 && ihl != 5u) {
         uint32_t lo, hi;
-        far(3u + ihl, lo, hi);  // L4 bytes 14+4*IHL .. 17+4*IHL = dword 3+IHL, byte 2
+        far(l3dw + ihl, lo, hi);  // L4 bytes L3+4*IHL .. +3 = dword l3dw+IHL, byte 2
         pw = funnel16(hi, lo);
     }
     f.ports = swap_halves(pw);
@@ -246,6 +260,7 @@ struct LinearArgs {
     uint32_t n4;
     const uint32_t *rec6;
     uint32_t n6;
+    uint32_t flags;  // NFFACL_PARSE_*
 };
 
 
@@ -261,7 +276,7 @@ k_linear_slots(const uint8_t *__restrict__ slots, uint32_t stride, uint64_t n, L
         Fields f;
         parse_fields(d, live, f, [&](uint32_t k, uint32_t &lo, uint32_t &hi) {
             far_dwords(pkt, stride, k, lo, hi);
-        });
+        }, a.flags & NFFACL_PARSE_VLAN);
         const uint32_t res = classify_linear(f, a.rec4, a.n4, a.rec6, a.n6);
         store_verdicts(base, lane, live, res, port_out, permit_out);
     }
@@ -283,7 +298,7 @@ k_linear_frames(const uint8_t *__restrict__ frames, const uint64_t *__restrict__
         Fields f;
         parse_fields(d, live, f, [&](uint32_t k, uint32_t &lo, uint32_t &hi) {
             far_dwords(pkt, len, k, lo, hi);
-        });
+        }, a.flags & NFFACL_PARSE_VLAN);
         const uint32_t res = classify_linear(f, a.rec4, a.n4, a.rec6, a.n6);
         store_verdicts(base, lane, live, res, port_out, permit_out);
     }
@@ -303,6 +318,7 @@ struct FamArgs {
 struct IndexedArgs {
     const uint32_t *tab;  // device table (global memory)
     uint32_t tab_dwords;  // multiple of 4
+    uint32_t flags;       // NFFACL_PARSE_*
     FamArgs f4, f6;
 };
 
@@ -442,10 +458,14 @@ k_indexed_slots(const uint8_t *__restrict__ slots, uint32_t stride, uint64_t n, 
     const uint64_t wave0 = uint64_t(blockIdx.x) * wpb + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t step = uint64_t(gridDim.x) * wpb * 64;
     constexpr bool COAL = MODE != 0;
+    constexpr bool NT = MODE >= 2;
+    constexpr bool PF = MODE == 3;  // coalesced + next-batch register prefetch
     const uint32_t mine = COAL ? coal_packet(lane) : lane;  // packet of this lane within the batch
     uint64_t base = wave0 * 64;
     uint32_t d[16];
+    u32x4 nv[4];
     if (!COAL && base < n) load16(slots + (base + lane < n ? base + lane : 0) * stride, d);
+    if (PF && base + 64 <= n) load_coal<NT>(slots + base * 64, lane, nv);
     for (; base < n; base += step) {
         const uint64_t idx = base + mine;
         const bool live = idx < n;
@@ -454,7 +474,14 @@ k_indexed_slots(const uint8_t *__restrict__ slots, uint32_t stride, uint64_t n, 
         if (COAL) {
             if (base + 64 <= n) {
                 u32x4 cv[4];
-                load_coal<MODE == 2>(slots + base * 64, lane, cv);
+                if (PF) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) cv[j] = nv[j];
+                    const uint64_t nb = base + step;
+                    if (nb + 64 <= n) load_coal<NT>(slots + nb * 64, lane, nv);
+                } else {
+                    load_coal<NT>(slots + base * 64, lane, cv);
+                }
                 transpose_batch(cv, lane, cur);
             } else {
                 load16(pkt, cur);
@@ -468,7 +495,7 @@ k_indexed_slots(const uint8_t *__restrict__ slots, uint32_t stride, uint64_t n, 
         Fields f;
         parse_fields(cur, live, f, [&](uint32_t k, uint32_t &lo, uint32_t &hi) {
             far_dwords(pkt, stride, k, lo, hi);
-        });
+        }, a.flags & NFFACL_PARSE_VLAN);
         const uint32_t res = classify_any<NS, LDS>(a, f);
         if (live && port_out) port_out[idx] = res;
         if (permit_out) {
@@ -500,7 +527,7 @@ k_indexed_frames(const uint8_t *__restrict__ frames, const uint64_t *__restrict_
         Fields f;
         parse_fields(d, live, f, [&](uint32_t k, uint32_t &lo, uint32_t &hi) {
             far_dwords(pkt, len, k, lo, hi);
-        });
+        }, a.flags & NFFACL_PARSE_VLAN);
         const uint32_t res = classify_any<NS, LDS>(a, f);
         store_verdicts(base, lane, live, res, port_out, permit_out);
     }
@@ -608,9 +635,10 @@ int prepare_kernels() {
     static std::once_flag once;
     static hipError_t err = hipSuccess;
     std::call_once(once, [] {
-        const hipError_t e[8] = {allow_lds(dev::k_indexed_slots<2, true, 0>), allow_lds(dev::k_indexed_slots<4, true, 0>),
+        const hipError_t e[10] = {allow_lds(dev::k_indexed_slots<2, true, 0>), allow_lds(dev::k_indexed_slots<4, true, 0>),
                                  allow_lds(dev::k_indexed_slots<2, true, 1>), allow_lds(dev::k_indexed_slots<4, true, 1>),
                                  allow_lds(dev::k_indexed_slots<2, true, 2>), allow_lds(dev::k_indexed_slots<4, true, 2>),
+                                 allow_lds(dev::k_indexed_slots<2, true, 3>), allow_lds(dev::k_indexed_slots<4, true, 3>),
                                  allow_lds(dev::k_indexed_frames<2, true>), allow_lds(dev::k_indexed_frames<4, true>)};
         for (hipError_t x : e)
             if (x != hipSuccess) err = x;
@@ -623,20 +651,24 @@ int prepare_kernels() {
 }
 
 int launch_slots(nffacl_engine *eng, const DevTable *t, const uint8_t *d_slots, uint32_t stride,
-                 uint64_t n, uint32_t *d_port, uint64_t *d_permit, hipStream_t stream) {
+                 uint64_t n, uint32_t *d_port, uint64_t *d_permit, hipStream_t stream, uint32_t flags) {
     if (n == 0) return NFFACL_OK;
     if (t->meta.algo == NFFACL_ALGO_INDEXED) {
-        const dev::IndexedArgs a = indexed_args(t);
+        dev::IndexedArgs a = indexed_args(t);
+        a.flags = flags;
         const IndexedLaunch L = indexed_launch(t);
         const uint32_t grid = grid_for(eng, n, L.block, L.per_cu);
         const dim3 g(grid), b(L.block);
         // load mode: 0 one row per lane, 1 lane-contiguous + transpose (64-byte
-        // slots only), 2 = 1 with non-temporal loads
-        const int mode = stride == 64 ? std::min(2, std::max(0, tune_env("NFFACL_TUNE_COAL", 1))) : 0;
+        // slots only), 2 = 1 with non-temporal loads (default: C2 0.220 ms vs
+        // 0.246 / 0.249 for modes 1 / 0, interleaved A/B in one process,
+        // profiles/r1_ab/ab_c2.json)
+        const int mode = stride == 64 ? std::min(3, std::max(0, tune_env("NFFACL_TUNE_COAL", 2))) : 0;
 #define NFFACL_SLOTS(NS_, LDS_, M_) \
     hipLaunchKernelGGL((dev::k_indexed_slots<NS_, LDS_, M_>), g, b, LDS_ ? L.lds_bytes : 0, stream, d_slots, stride, n, a, d_port, d_permit)
 #define NFFACL_SLOTS_M(NS_, LDS_) \
-    do { if (mode == 2) NFFACL_SLOTS(NS_, LDS_, 2); else if (mode == 1) NFFACL_SLOTS(NS_, LDS_, 1); else NFFACL_SLOTS(NS_, LDS_, 0); } while (0)
+    do { if (mode == 3) NFFACL_SLOTS(NS_, LDS_, 3); else if (mode == 2) NFFACL_SLOTS(NS_, LDS_, 2); \
+         else if (mode == 1) NFFACL_SLOTS(NS_, LDS_, 1); else NFFACL_SLOTS(NS_, LDS_, 0); } while (0)
         if (L.lds && L.ns == 2) NFFACL_SLOTS_M(2, true);
         else if (L.lds) NFFACL_SLOTS_M(4, true);
         else if (L.ns == 2) NFFACL_SLOTS_M(2, false);
@@ -646,7 +678,7 @@ int launch_slots(nffacl_engine *eng, const DevTable *t, const uint8_t *d_slots, 
     } else {
         const uint32_t block = 256;
         dev::LinearArgs a{t->d_blob + t->meta.off_rec4, t->meta.n4, t->d_blob + t->meta.off_rec6,
-                          t->meta.n6};
+                          t->meta.n6, flags};
         const uint32_t grid = grid_for(eng, n, block, 8);
         hipLaunchKernelGGL(dev::k_linear_slots, dim3(grid), dim3(block), 0, stream, d_slots, stride,
                            n, a, d_port, d_permit);
@@ -657,10 +689,11 @@ int launch_slots(nffacl_engine *eng, const DevTable *t, const uint8_t *d_slots, 
 
 int launch_frames(nffacl_engine *eng, const DevTable *t, const uint8_t *d_frames,
                   const uint64_t *d_desc, uint64_t n, uint32_t *d_port, uint64_t *d_permit,
-                  hipStream_t stream) {
+                  hipStream_t stream, uint32_t flags) {
     if (n == 0) return NFFACL_OK;
     if (t->meta.algo == NFFACL_ALGO_INDEXED) {
-        const dev::IndexedArgs a = indexed_args(t);
+        dev::IndexedArgs a = indexed_args(t);
+        a.flags = flags;
         const IndexedLaunch L = indexed_launch(t);
         const uint32_t grid = grid_for(eng, n, L.block, L.per_cu);
         const dim3 g(grid), b(L.block);
@@ -675,7 +708,7 @@ int launch_frames(nffacl_engine *eng, const DevTable *t, const uint8_t *d_frames
     } else {
         const uint32_t block = 256;
         dev::LinearArgs a{t->d_blob + t->meta.off_rec4, t->meta.n4, t->d_blob + t->meta.off_rec6,
-                          t->meta.n6};
+                          t->meta.n6, flags};
         const uint32_t grid = grid_for(eng, n, block, 8);
         hipLaunchKernelGGL(dev::k_linear_frames, dim3(grid), dim3(block), 0, stream, d_frames, d_desc,
                            n, a, d_port, d_permit);

@@ -56,8 +56,8 @@ inline DevTable *acquire_table(nffacl_engine *eng) {
 }
 int prepare_kernels();
 int launch_slots(nffacl_engine *eng, const DevTable *t, const uint8_t *d_slots, uint32_t stride,
-                 uint64_t n, uint32_t *d_port, uint64_t *d_permit, hipStream_t stream);
+                 uint64_t n, uint32_t *d_port, uint64_t *d_permit, hipStream_t stream, uint32_t flags = 0);
 int launch_frames(nffacl_engine *eng, const DevTable *t, const uint8_t *d_frames,
                   const uint64_t *d_desc, uint64_t n, uint32_t *d_port, uint64_t *d_permit,
-                  hipStream_t stream);
+                  hipStream_t stream, uint32_t flags = 0);
 }  // namespace nffacl

@@ -1,16 +1,19 @@
 // l2.hip — HIP kernels (gfx950) for nff-go's L2 ACL: (*Packet).l2ACL,
 // packet/acl.go:478-491, behind L2ACLPort / L2ACLPermit (acl.go:462-476).
 //
-// One wave64 = 64 consecutive packets, one packet per lane.  Each lane needs
-// only the first 16 bytes of its frame (one 16-byte load); the rule records
-// are wave-uniform and stream through the scalar data cache, so each rule is
-// four masked compares on all 64 packets at once, and a ballot of
-// still-undecided lanes ends the scan at the wave's last first-match (the
-// reference's `return rule.OutputNumber`).
+// One wave64 = 64 consecutive packets, one packet per lane; each lane needs
+// only the 16-byte line holding its Ethernet header (one load).
+//  * LINEAR: records are wave-uniform and stream through the scalar data
+//    cache; a ballot of still-undecided lanes ends the scan at the wave's
+//    last first-match (the reference's `return rule.OutputNumber`).
+//  * HASH: per rule shape one hashed probe (see l2.hpp); tables staged in LDS
+//    per workgroup when they fit, read through L1/L2 otherwise.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cstring>
+#include <map>
 #include <string>
 
 #include "devutil.hpp"
@@ -18,50 +21,113 @@
 
 namespace nffacl {
 
-std::vector<uint32_t> compile_l2(const std::vector<nffacl_l2_rule> &eth) {
-    std::vector<uint32_t> rec;
-    rec.reserve(eth.size() * kL2RecDwords);
-    for (const nffacl_l2_rule &r : eth) {
-        uint8_t val[12] = {0}, msk[12] = {0};
-        if (r.daddr_not_any) {
-            std::memcpy(val, r.daddr, 6);
-            std::memset(msk, 0xff, 6);
-        }
-        if (r.saddr_not_any) {
-            std::memcpy(val + 6, r.saddr, 6);
-            std::memset(msk + 6, 0xff, 6);
-        }
-        uint32_t v[3], m[3];
-        std::memcpy(v, val, 12);
-        std::memcpy(m, msk, 12);
-        // (rule.ID ^ SwapBytesUint16(EtherType)) & rule.IDMask  (acl.go:486):
-        // the big-endian EtherType compared with ID is, in wire-byte (LE) form,
-        // the byte-swapped ID / IDMask.
-        const uint32_t em = static_cast<uint32_t>(((r.id_mask & 0xffu) << 8) | (r.id_mask >> 8));
-        const uint32_t ev = static_cast<uint32_t>(((r.id & 0xffu) << 8) | (r.id >> 8)) & em;
-        const uint32_t w[kL2RecDwords] = {v[0] & m[0], v[1] & m[1], v[2] & m[2], ev | (em << 16),
-                                          m[0], m[1], m[2], r.output_number};
-        rec.insert(rec.end(), w, w + kL2RecDwords);
-        if (!r.daddr_not_any && !r.saddr_not_any && em == 0) break;  // later rules unreachable
+namespace {
+
+struct Masked {
+    std::array<uint32_t, 4> v, m;  // pre-masked value, mask (m3 = EtherType mask, low 16 bits)
+};
+
+Masked masked_rule(const nffacl_l2_rule &r) {
+    uint8_t val[12] = {0}, msk[12] = {0};
+    if (r.daddr_not_any) {
+        std::memcpy(val, r.daddr, 6);
+        std::memset(msk, 0xff, 6);
     }
-    return rec;
+    if (r.saddr_not_any) {
+        std::memcpy(val + 6, r.saddr, 6);
+        std::memset(msk + 6, 0xff, 6);
+    }
+    Masked x;
+    std::memcpy(x.v.data(), val, 12);
+    std::memcpy(x.m.data(), msk, 12);
+    // (rule.ID ^ SwapBytesUint16(EtherType)) & rule.IDMask (acl.go:486): the
+    // big-endian EtherType compared with ID is, in wire-byte (LE) form, the
+    // byte-swapped ID / IDMask.
+    x.m[3] = static_cast<uint32_t>(((r.id_mask & 0xffu) << 8) | (r.id_mask >> 8));
+    x.v[3] = static_cast<uint32_t>(((r.id & 0xffu) << 8) | (r.id >> 8));
+    for (int k = 0; k < 4; ++k) x.v[k] &= x.m[k];
+    return x;
+}
+
+}  // namespace
+
+L2Compiled compile_l2(const std::vector<nffacl_l2_rule> &eth, int algo) {
+    L2Compiled c;
+    std::vector<Masked> rules;
+    for (const nffacl_l2_rule &r : eth) {
+        rules.push_back(masked_rule(r));
+        const Masked &x = rules.back();
+        if ((x.m[0] | x.m[1] | x.m[2] | x.m[3]) == 0) break;  // later rules unreachable
+    }
+    // shapes in order of first appearance
+    std::vector<std::array<uint32_t, 4>> shapes;
+    std::vector<std::vector<uint32_t>> members;
+    for (uint32_t i = 0; i < rules.size(); ++i) {
+        auto it = std::find(shapes.begin(), shapes.end(), rules[i].m);
+        if (it == shapes.end()) {
+            shapes.push_back(rules[i].m);
+            members.emplace_back();
+            it = shapes.end() - 1;
+        }
+        members[it - shapes.begin()].push_back(i);
+    }
+    const bool hash = algo != NFFACL_ALGO_LINEAR && shapes.size() <= kL2MaxShapes;
+    if (!hash) {
+        c.algo = NFFACL_ALGO_LINEAR;
+        for (uint32_t i = 0; i < rules.size(); ++i) {
+            const Masked &x = rules[i];
+            const uint32_t w[kL2RecDwords] = {x.v[0], x.v[1], x.v[2], x.v[3] | (x.m[3] << 16),
+                                              x.m[0], x.m[1], x.m[2], eth[i].output_number};
+            c.blob.insert(c.blob.end(), w, w + kL2RecDwords);
+        }
+        c.n_rules = static_cast<uint32_t>(rules.size());
+    } else {
+        c.algo = NFFACL_ALGO_INDEXED;
+        c.n_shapes = static_cast<uint32_t>(shapes.size());
+        for (uint32_t s = 0; s < shapes.size(); ++s) {
+            uint32_t cap = 4;
+            while (cap < 2 * members[s].size()) cap <<= 1;
+            L2Shape &S = c.shapes[s];
+            std::copy(shapes[s].begin(), shapes[s].end(), S.m);
+            S.off = static_cast<uint32_t>(c.blob.size());
+            S.cap_mask = cap - 1;
+            S.first = members[s].front();
+            c.blob.resize(c.blob.size() + size_t(cap) * kL2EntDwords, 0);
+            for (uint32_t i : members[s]) {  // ascending rule index: the first key owner wins
+                const auto &v = rules[i].v;
+                uint32_t h = l2_hash(v[0], v[1], v[2], v[3]) & S.cap_mask;
+                while (true) {
+                    uint32_t *e = &c.blob[S.off + size_t(h) * kL2EntDwords];
+                    if (e[4] == 0) {
+                        e[0] = v[0]; e[1] = v[1]; e[2] = v[2]; e[3] = v[3];
+                        e[4] = i + 1;
+                        e[5] = eth[i].output_number;
+                        break;
+                    }
+                    if (e[0] == v[0] && e[1] == v[1] && e[2] == v[2] && e[3] == v[3]) break;  // shadowed
+                    h = (h + 1) & S.cap_mask;
+                }
+            }
+        }
+        std::sort(c.shapes, c.shapes + c.n_shapes,
+                  [](const L2Shape &a, const L2Shape &b) { return a.first < b.first; });
+        c.n_rules = static_cast<uint32_t>(rules.size());
+    }
+    if (c.blob.empty()) c.blob.assign(kL2RecDwords, 0);  // keep a valid allocation
+    return c;
 }
 
 L2Table::~L2Table() {
-    if (d_rec) (void)hipFree(d_rec);
+    if (d_blob) (void)hipFree(d_blob);
 }
 
-int upload_l2(int device, const nffacl_l2rules &rules, L2Table *&out) {
-    const std::vector<uint32_t> rec = compile_l2(rules.eth);
+int upload_l2(int device, const nffacl_l2rules &rules, int algo, L2Table *&out) {
     HIP_TRY(hipSetDevice(device));
     L2Table *t = new L2Table();
-    t->n = static_cast<uint32_t>(rec.size() / kL2RecDwords);
-    // at least one record so the device pointer is always valid
-    const size_t bytes = std::max<size_t>(rec.size(), kL2RecDwords) * sizeof(uint32_t);
-    hipError_t e = hipMalloc(reinterpret_cast<void **>(&t->d_rec), bytes);
-    if (e == hipSuccess) e = hipMemset(t->d_rec, 0, bytes);
-    if (e == hipSuccess && !rec.empty())
-        e = hipMemcpy(t->d_rec, rec.data(), rec.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+    t->meta = compile_l2(rules.eth, algo);
+    const size_t bytes = t->meta.blob.size() * sizeof(uint32_t);
+    hipError_t e = hipMalloc(reinterpret_cast<void **>(&t->d_blob), bytes);
+    if (e == hipSuccess) e = hipMemcpy(t->d_blob, t->meta.blob.data(), bytes, hipMemcpyHostToDevice);
     if (e != hipSuccess) {
         set_last_error(std::string("L2 table upload: ") + hipGetErrorString(e));
         delete t;
@@ -73,8 +139,17 @@ int upload_l2(int device, const nffacl_l2rules &rules, L2Table *&out) {
 
 namespace dev {
 
-__device__ __forceinline__ uint32_t classify_l2(const uint32_t (&p)[4], bool live,
-                                                const uint32_t *__restrict__ rec, uint32_t n) {
+extern __shared__ uint32_t l2_lds[];
+
+struct L2Args {
+    const uint32_t *tab;
+    uint32_t tab_dwords;
+    uint32_t n;  // LINEAR: records; HASH: shapes
+    L2Shape shapes[kL2MaxShapes];
+};
+
+__device__ __forceinline__ uint32_t classify_l2_linear(const uint32_t (&p)[4], bool live,
+                                                       const uint32_t *__restrict__ rec, uint32_t n) {
     uint32_t res = 0;
     bool pend = live;
     for (uint32_t r = 0; r < n; ++r) {
@@ -90,23 +165,74 @@ __device__ __forceinline__ uint32_t classify_l2(const uint32_t (&p)[4], bool liv
     return res;
 }
 
-__global__ void __launch_bounds__(256)
-k_l2_slots(const uint8_t *__restrict__ slots, uint32_t stride, uint64_t n, const uint32_t *__restrict__ rec,
-           uint32_t nrec, uint32_t *__restrict__ port_out, uint64_t *__restrict__ permit_out) {
+template <bool LDS>
+__device__ __forceinline__ u32x4 l2_ld4(const uint32_t *__restrict__ g, uint32_t i) {
+    return LDS ? *reinterpret_cast<const u32x4 *>(&l2_lds[i]) : *reinterpret_cast<const u32x4 *>(g + i);
+}
+
+template <bool LDS>
+__device__ __forceinline__ uint32_t classify_l2_hash(const uint32_t (&p)[4], bool live, const L2Args &a) {
+    uint32_t best = 0xFFFFFFFFu, res = 0;
+    for (uint32_t s = 0; s < a.n; ++s) {
+        const L2Shape &S = a.shapes[s];
+        bool active = live && S.first < best;  // shapes ascend by first rule index
+        if (!ballot(active)) break;
+        const uint32_t k0 = p[0] & S.m[0], k1 = p[1] & S.m[1], k2 = p[2] & S.m[2], k3 = p[3] & S.m[3];
+        uint32_t h = l2_hash(k0, k1, k2, k3) & S.cap_mask;
+        while (ballot(active)) {
+            if (active) {
+                const uint32_t at = S.off + h * kL2EntDwords;
+                const u32x4 e = l2_ld4<LDS>(a.tab, at);
+                const u32x4 f = l2_ld4<LDS>(a.tab, at + 4);
+                if (f.x == 0u) {
+                    active = false;  // empty slot: key absent
+                } else if (e.x == k0 && e.y == k1 && e.z == k2 && e.w == k3) {
+                    if (f.x - 1u < best) { best = f.x - 1u; res = f.y; }
+                    active = false;
+                } else {
+                    h = (h + 1u) & S.cap_mask;
+                }
+            }
+        }
+    }
+    return res;
+}
+
+template <int ALGO, bool LDS>
+__device__ __forceinline__ uint32_t classify_l2(const uint32_t (&p)[4], bool live, const L2Args &a) {
+    if (ALGO == NFFACL_ALGO_LINEAR) return classify_l2_linear(p, live, a.tab, a.n);
+    return classify_l2_hash<LDS>(p, live, a);
+}
+
+template <bool LDS>
+__device__ __forceinline__ void l2_stage(const L2Args &a) {
+    if (!LDS) return;
+    const u32x4 *src = reinterpret_cast<const u32x4 *>(a.tab);
+    u32x4 *dst = reinterpret_cast<u32x4 *>(l2_lds);
+    for (uint32_t i = threadIdx.x; i < a.tab_dwords / 4; i += blockDim.x) dst[i] = src[i];
+    __syncthreads();
+}
+
+template <int ALGO, bool LDS>
+__global__ void __launch_bounds__(1024)
+k_l2_slots(const uint8_t *__restrict__ slots, uint32_t stride, uint64_t n, L2Args a,
+           uint32_t *__restrict__ port_out, uint64_t *__restrict__ permit_out) {
+    l2_stage<LDS>(a);
     NFFACL_WAVE_LOOP(n) {
         const uint64_t idx = base + lane;
         const bool live = idx < n;
         const u32x4 v = *reinterpret_cast<const u32x4 *>(slots + (live ? idx : 0) * stride);
         const uint32_t p[4] = {v.x, v.y, v.z, v.w};
-        store_verdicts(base, lane, live, classify_l2(p, live, rec, nrec), port_out, permit_out);
+        store_verdicts(base, lane, live, classify_l2<ALGO, LDS>(p, live, a), port_out, permit_out);
     }
 }
 
 // Packed frames: desc = offset << 16 | length; bytes >= length read as 0.
-__global__ void __launch_bounds__(256)
-k_l2_frames(const uint8_t *__restrict__ frames, const uint64_t *__restrict__ desc, uint64_t n,
-            const uint32_t *__restrict__ rec, uint32_t nrec, uint32_t *__restrict__ port_out,
-            uint64_t *__restrict__ permit_out) {
+template <int ALGO, bool LDS>
+__global__ void __launch_bounds__(1024)
+k_l2_frames(const uint8_t *__restrict__ frames, const uint64_t *__restrict__ desc, uint64_t n, L2Args a,
+            uint32_t *__restrict__ port_out, uint64_t *__restrict__ permit_out) {
+    l2_stage<LDS>(a);
     NFFACL_WAVE_LOOP(n) {
         const uint64_t idx = base + lane;
         const bool live = idx < n;
@@ -114,24 +240,70 @@ k_l2_frames(const uint8_t *__restrict__ frames, const uint64_t *__restrict__ des
         const u32x4 v = *reinterpret_cast<const u32x4 *>(frames + (ds >> 16));
         uint32_t p[4] = {v.x, v.y, v.z, v.w};
         clip_dwords<4>(p, static_cast<uint32_t>(ds & 0xFFFFu));
-        store_verdicts(base, lane, live, classify_l2(p, live, rec, nrec), port_out, permit_out);
+        store_verdicts(base, lane, live, classify_l2<ALGO, LDS>(p, live, a), port_out, permit_out);
     }
 }
 
 }  // namespace dev
 
-static uint32_t l2_grid(const nffacl_l2engine *eng, uint64_t n, uint32_t block) {
-    const uint64_t blocks_needed = ((n + 63) / 64 * 64 + block - 1) / block;
-    const uint64_t cap = uint64_t(eng->num_cus) * 8;
-    return static_cast<uint32_t>(std::max<uint64_t>(1, std::min(blocks_needed, cap)));
+namespace {
+
+constexpr size_t kL2LdsMax = 72 * 1024;  // two workgroups per CU keep their own copy
+
+struct L2Launch {
+    dev::L2Args a;
+    bool lds;
+    uint32_t block, grid;
+    size_t lds_bytes;
+};
+
+L2Launch l2_plan(const nffacl_l2engine *eng, const L2Table *t, uint64_t n) {
+    L2Launch L{};
+    L.a.tab = t->d_blob;
+    L.a.tab_dwords = static_cast<uint32_t>(t->meta.blob.size());
+    const bool hash = t->meta.algo == NFFACL_ALGO_INDEXED;
+    L.a.n = hash ? t->meta.n_shapes : t->meta.n_rules;
+    std::copy(t->meta.shapes, t->meta.shapes + kL2MaxShapes, L.a.shapes);
+    L.lds_bytes = t->meta.blob.size() * sizeof(uint32_t);
+    L.lds = hash && L.lds_bytes <= kL2LdsMax;
+    L.block = L.lds ? 1024 : 256;
+    const uint32_t per_cu = L.lds ? 2 : 8;
+    const uint64_t blocks_needed = ((n + 63) / 64 * 64 + L.block - 1) / L.block;
+    L.grid = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(blocks_needed, uint64_t(eng->num_cus) * per_cu)));
+    return L;
+}
+
+}  // namespace
+
+int l2_prepare_kernels() {
+    static std::once_flag once;
+    static hipError_t err = hipSuccess;
+    std::call_once(once, [] {
+        const void *k[2] = {reinterpret_cast<const void *>(dev::k_l2_slots<NFFACL_ALGO_INDEXED, true>),
+                            reinterpret_cast<const void *>(dev::k_l2_frames<NFFACL_ALGO_INDEXED, true>)};
+        for (const void *f : k) {
+            hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kL2LdsMax));
+            if (e != hipSuccess) err = e;
+        }
+    });
+    if (err != hipSuccess) {
+        set_last_error(std::string("hipFuncSetAttribute(L2 LDS): ") + hipGetErrorString(err));
+        return NFFACL_ERR_HIP;
+    }
+    return NFFACL_OK;
 }
 
 int l2_launch_slots(nffacl_l2engine *eng, const L2Table *t, const uint8_t *d_slots, uint32_t stride,
                     uint64_t n, uint32_t *d_port, uint64_t *d_permit, hipStream_t stream) {
     if (n == 0) return NFFACL_OK;
-    constexpr uint32_t block = 256;
-    hipLaunchKernelGGL(dev::k_l2_slots, dim3(l2_grid(eng, n, block)), dim3(block), 0, stream, d_slots, stride, n,
-                       t->d_rec, t->n, d_port, d_permit);
+    const L2Launch L = l2_plan(eng, t, n);
+    const dim3 g(L.grid), b(L.block);
+    if (t->meta.algo == NFFACL_ALGO_LINEAR)
+        hipLaunchKernelGGL((dev::k_l2_slots<NFFACL_ALGO_LINEAR, false>), g, b, 0, stream, d_slots, stride, n, L.a, d_port, d_permit);
+    else if (L.lds)
+        hipLaunchKernelGGL((dev::k_l2_slots<NFFACL_ALGO_INDEXED, true>), g, b, L.lds_bytes, stream, d_slots, stride, n, L.a, d_port, d_permit);
+    else
+        hipLaunchKernelGGL((dev::k_l2_slots<NFFACL_ALGO_INDEXED, false>), g, b, 0, stream, d_slots, stride, n, L.a, d_port, d_permit);
     HIP_TRY(hipGetLastError());
     return NFFACL_OK;
 }
@@ -139,9 +311,14 @@ int l2_launch_slots(nffacl_l2engine *eng, const L2Table *t, const uint8_t *d_slo
 int l2_launch_frames(nffacl_l2engine *eng, const L2Table *t, const uint8_t *d_frames, const uint64_t *d_desc,
                      uint64_t n, uint32_t *d_port, uint64_t *d_permit, hipStream_t stream) {
     if (n == 0) return NFFACL_OK;
-    constexpr uint32_t block = 256;
-    hipLaunchKernelGGL(dev::k_l2_frames, dim3(l2_grid(eng, n, block)), dim3(block), 0, stream, d_frames, d_desc,
-                       n, t->d_rec, t->n, d_port, d_permit);
+    const L2Launch L = l2_plan(eng, t, n);
+    const dim3 g(L.grid), b(L.block);
+    if (t->meta.algo == NFFACL_ALGO_LINEAR)
+        hipLaunchKernelGGL((dev::k_l2_frames<NFFACL_ALGO_LINEAR, false>), g, b, 0, stream, d_frames, d_desc, n, L.a, d_port, d_permit);
+    else if (L.lds)
+        hipLaunchKernelGGL((dev::k_l2_frames<NFFACL_ALGO_INDEXED, true>), g, b, L.lds_bytes, stream, d_frames, d_desc, n, L.a, d_port, d_permit);
+    else
+        hipLaunchKernelGGL((dev::k_l2_frames<NFFACL_ALGO_INDEXED, false>), g, b, 0, stream, d_frames, d_desc, n, L.a, d_port, d_permit);
     HIP_TRY(hipGetLastError());
     return NFFACL_OK;
 }

@@ -1,14 +1,21 @@
 // l2.hpp — L2 ACL engine behind the nffacl_l2engine handle (internal).
 //
-// The reference's L2 ACL (packet/acl.go:462-491) compares the Ethernet header
+// The reference's L2 ACL (packet/acl.go:478-491) compares the Ethernet header
 // only: destination MAC (wire bytes 0..5), source MAC (6..11) and EtherType
-// (12..13).  Compiled form: one 8-dword record per rule in file order,
-//   [0..2] value dwords of wire bytes 0..11 (little-endian dwords, pre-masked)
-//   [3]    EtherType value (LE 16 of wire bytes 12..13) | its mask << 16
-//   [4..6] masks of wire bytes 0..11 (0xff per constrained MAC byte)
-//   [7]    OutputNumber
-// so a rule matches packet dwords p0..p3 iff
-//   ((p0^v0)&m0) | ((p1^v1)&m1) | ((p2^v2)&m2) | ((p3^v3)&(v3>>16)) == 0.
+// (12..13), each either exact or ANY (an arbitrary EtherType mask through
+// nffacl_l2rules_from_array).  A packet is the four little-endian dwords
+// p0..p3 of wire bytes 0..15; a rule is a value v and a mask m over them
+// (m3 = EtherType mask in its low 16 bits), matching iff ((p ^ v) & m) == 0.
+//
+// Two compiled forms, both first-match exact:
+//  LINEAR  8-dword records in file order, scanned wave-uniformly:
+//            [0..2] v0..v2, [3] v3 | m3 << 16, [4..6] m0..m2, [7] OutputNumber
+//  HASH    rules grouped by *shape* (their mask m0..m3); per shape an
+//          open-addressing table keyed by the masked header, holding the
+//          first (lowest-index) rule with that key.  A packet probes every
+//          shape whose first rule precedes its best match so far; the answer
+//          is the lowest rule index found — the reference's first match.
+//          Entry (8 dwords): k0..k3, rule index + 1 (0 = empty), OutputNumber, 0, 0.
 // Rules after the first unconstrained rule (matches everything) are dropped.
 #pragma once
 
@@ -24,23 +31,51 @@
 namespace nffacl {
 
 constexpr uint32_t kL2RecDwords = 8;
+constexpr uint32_t kL2EntDwords = 8;
+constexpr uint32_t kL2MaxShapes = 8;
 
-// Host compilation of an L2 rule list into device records.
-std::vector<uint32_t> compile_l2(const std::vector<nffacl_l2_rule> &eth);
+struct L2Shape {
+    uint32_t m[4];     // header masks of this shape
+    uint32_t off;      // dword offset of its table in the blob
+    uint32_t cap_mask; // table capacity - 1 (power of two)
+    uint32_t first;    // lowest rule index of the shape
+    uint32_t pad;
+};
+
+struct L2Compiled {
+    int algo = NFFACL_ALGO_LINEAR;
+    std::vector<uint32_t> blob;  // LINEAR records or HASH tables
+    uint32_t n_rules = 0;        // live rules (LINEAR records)
+    uint32_t n_shapes = 0;
+    L2Shape shapes[kL2MaxShapes] = {};
+};
+
+// Host compilation (AUTO -> HASH when the rules have <= kL2MaxShapes shapes).
+L2Compiled compile_l2(const std::vector<nffacl_l2_rule> &eth, int algo);
+
+// Header hash shared by the host compiler and the kernel.
+__host__ __device__ inline uint32_t l2_hash(uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
+    uint32_t h = k0 * 0x9E3779B1u ^ k1 * 0x85EBCA77u ^ k2 * 0xC2B2AE3Du ^ k3 * 0x27D4EB2Fu;
+    h ^= h >> 15;
+    h *= 0x2C1B3C6Du;
+    h ^= h >> 13;
+    return h;
+}
 
 struct L2Table {
-    uint32_t *d_rec = nullptr;
-    uint32_t n = 0;
+    uint32_t *d_blob = nullptr;
+    L2Compiled meta;
     ~L2Table();
 };
 
-int upload_l2(int device, const nffacl_l2rules &rules, L2Table *&out);
+int upload_l2(int device, const nffacl_l2rules &rules, int algo, L2Table *&out);
 
 }  // namespace nffacl
 
 struct nffacl_l2engine {
     int device = 0;
     int num_cus = 256;
+    int algo_req = NFFACL_ALGO_AUTO;
     std::mutex table_mu;
     nffacl::L2Table *active = nullptr;
     nffacl::L2Table *retired = nullptr;
@@ -53,6 +88,7 @@ struct nffacl_l2engine {
 };
 
 namespace nffacl {
+int l2_prepare_kernels();
 int l2_launch_slots(nffacl_l2engine *eng, const L2Table *t, const uint8_t *d_slots, uint32_t stride,
                     uint64_t n, uint32_t *d_port, uint64_t *d_permit, hipStream_t stream);
 int l2_launch_frames(nffacl_l2engine *eng, const L2Table *t, const uint8_t *d_frames,

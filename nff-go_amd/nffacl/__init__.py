@@ -55,6 +55,7 @@ ERR_NO_DEVICE = -103
 ERR_UNSUPPORTED = -104
 
 ALGO_AUTO, ALGO_LINEAR, ALGO_INDEXED = 0, 1, 2
+PARSE_VLAN = 1  # ParseAllKnownL3CheckVLAN (packet/vlan.go:104-117) instead of ParseAllKnownL3
 
 # ---- record layouts ------------------------------------------------------------
 _L4 = [("id", "u1"), ("id_mask", "u1"), ("valid", "u1"), ("reserved", "u1"),
@@ -95,9 +96,9 @@ _engine_swap = _sig("nffacl_engine_swap_rules", _i, _vp, _vp)
 _engine_destroy = _sig("nffacl_engine_destroy", None, _vp)
 _engine_algo = _sig("nffacl_engine_algo", _i, _vp)
 _engine_table_bytes = _sig("nffacl_engine_table_bytes", _i, _vp, ctypes.POINTER(_u64))
-_classify_device = _sig("nffacl_classify_device", _i, _vp, _vp, _u32, _u64, _vp, _vp, _vp)
-_classify_frames = _sig("nffacl_classify_frames_device", _i, _vp, _vp, _vp, _u64, _vp, _vp, _vp)
-_classify_host = _sig("nffacl_classify_host", _i, _vp, _vp, _u32, _u64, _vp, _vp)
+_classify_device = _sig("nffacl_classify_device_ex", _i, _vp, _vp, _u32, _u64, _vp, _vp, _vp, _u32)
+_classify_frames = _sig("nffacl_classify_frames_device_ex", _i, _vp, _vp, _vp, _u64, _vp, _vp, _vp, _u32)
+_classify_host = _sig("nffacl_classify_host_ex", _i, _vp, _vp, _u32, _u64, _vp, _vp, _u32)
 _l2_load_text = _sig("nffacl_l2rules_load_text", _i, ctypes.c_char_p, _pp, ctypes.c_char_p, _sz)
 _l2_parse_text = _sig("nffacl_l2rules_parse_text", _i, ctypes.c_char_p, _sz, _pp, ctypes.c_char_p, _sz)
 _l2_load_json = _sig("nffacl_l2rules_load_json", _i, ctypes.c_char_p, _pp, ctypes.c_char_p, _sz)
@@ -107,6 +108,8 @@ _l2_free = _sig("nffacl_l2rules_free", None, _vp)
 _l2_count = _sig("nffacl_l2rules_count", _i, _vp, ctypes.POINTER(_sz))
 _l2_get = _sig("nffacl_l2rules_get", _i, _vp, _sz, _vp)
 _l2_engine_create = _sig("nffacl_l2_engine_create", _i, _i, _vp, _pp)
+_l2_engine_create_ex = _sig("nffacl_l2_engine_create_ex", _i, _i, _vp, _i, _pp)
+_l2_engine_algo = _sig("nffacl_l2_engine_algo", _i, _vp)
 _l2_engine_swap = _sig("nffacl_l2_engine_swap_rules", _i, _vp, _vp)
 _l2_engine_destroy = _sig("nffacl_l2_engine_destroy", None, _vp)
 _l2_classify_device = _sig("nffacl_l2_classify_device", _i, _vp, _vp, _u32, _u64, _vp, _vp, _vp)
@@ -140,10 +143,12 @@ EXPORTED_SYMBOLS = [
     "nffacl_engine_create", "nffacl_engine_create_ex", "nffacl_engine_swap_rules",
     "nffacl_engine_destroy", "nffacl_engine_algo", "nffacl_engine_table_bytes",
     "nffacl_classify_device", "nffacl_classify_frames_device", "nffacl_classify_host",
+    "nffacl_classify_device_ex", "nffacl_classify_frames_device_ex", "nffacl_classify_host_ex",
     "nffacl_table_compile", "nffacl_strerror", "nffacl_abi_version", "nffacl_last_error",
     "nffacl_l2rules_load_text", "nffacl_l2rules_parse_text", "nffacl_l2rules_load_json",
     "nffacl_l2rules_parse_json", "nffacl_l2rules_from_array", "nffacl_l2rules_free",
     "nffacl_l2rules_count", "nffacl_l2rules_get", "nffacl_l2_engine_create",
+    "nffacl_l2_engine_create_ex", "nffacl_l2_engine_algo",
     "nffacl_l2_engine_swap_rules", "nffacl_l2_engine_destroy", "nffacl_l2_classify_device",
     "nffacl_l2_classify_frames_device", "nffacl_l2_classify_host",
     "nffacl_batcher_create", "nffacl_batcher_submit", "nffacl_batcher_wait", "nffacl_batcher_classify",
@@ -323,20 +328,21 @@ class Engine:
         if st != OK:
             _raise(st, "nffacl_engine_swap_rules")
 
-    def classify_device(self, slots, stride: int, n: int, port=None, permit_bits=None, stream=None):
+    def classify_device(self, slots, stride: int, n: int, port=None, permit_bits=None, stream=None, flags: int = 0):
         """Asynchronous on `stream` (a torch.cuda.Stream, raw handle or None)."""
         s = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
-        st = _classify_device(self._h, _ptr(slots), stride, n, _ptr(port), _ptr(permit_bits), s)
+        st = _classify_device(self._h, _ptr(slots), stride, n, _ptr(port), _ptr(permit_bits), s, flags)
         if st != OK:
             _raise(st, "nffacl_classify_device")
 
-    def classify_frames_device(self, frames, desc, n: int, port=None, permit_bits=None, stream=None):
+    def classify_frames_device(self, frames, desc, n: int, port=None, permit_bits=None, stream=None,
+                               flags: int = 0):
         s = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
-        st = _classify_frames(self._h, _ptr(frames), _ptr(desc), n, _ptr(port), _ptr(permit_bits), s)
+        st = _classify_frames(self._h, _ptr(frames), _ptr(desc), n, _ptr(port), _ptr(permit_bits), s, flags)
         if st != OK:
             _raise(st, "nffacl_classify_frames_device")
 
-    def classify_host(self, slots: np.ndarray, stride: int, n: int | None = None):
+    def classify_host(self, slots: np.ndarray, stride: int, n: int | None = None, flags: int = 0):
         """Host slots (uint8, n*stride bytes) -> (port uint32[n], permit uint8[n])."""
         slots = np.ascontiguousarray(slots, np.uint8)
         if n is None:
@@ -345,7 +351,7 @@ class Engine:
             raise ValueError("slot buffer too small")
         port = np.zeros(n, np.uint32)
         permit = np.zeros(n, np.uint8)
-        st = _classify_host(self._h, slots.ctypes.data, stride, n, port.ctypes.data, permit.ctypes.data)
+        st = _classify_host(self._h, slots.ctypes.data, stride, n, port.ctypes.data, permit.ctypes.data, flags)
         if st != OK:
             _raise(st, "nffacl_classify_host")
         return port, permit
@@ -521,9 +527,9 @@ def GetL2ACLFromJSON(filename):
 class L2Engine:
     """A compiled L2 rule table resident on one HIP device."""
 
-    def __init__(self, rules: L2Rules, device: int = 0):
+    def __init__(self, rules: L2Rules, device: int = 0, algo: int = ALGO_AUTO):
         out = ctypes.c_void_p()
-        st = _l2_engine_create(device, rules.handle, ctypes.byref(out))
+        st = _l2_engine_create_ex(device, rules.handle, algo, ctypes.byref(out))
         if st != OK:
             _raise(st, "nffacl_l2_engine_create")
         self._h = out.value
@@ -545,6 +551,10 @@ class L2Engine:
 
     def __exit__(self, *exc):
         self.close()
+
+    @property
+    def algo(self) -> int:
+        return _l2_engine_algo(self._h)
 
     def swap_rules(self, rules: L2Rules):
         st = _l2_engine_swap(self._h, rules.handle)

@@ -19,6 +19,9 @@
  *   IPv4Hdr / IPv6Hdr / UDPHdr layouts packet/packet.go:107-170
  *   types.IPv4Address = LE uint32 of wire bytes   types/ipv4.go:13-28
  *   (*Packet).l2ACL        packet/acl.go:478-491   (L2 ACL, §8f next row)
+ *   ParseAllKnownL3CheckVLAN packet/vlan.go:104-117 (+ GetEtherType :53-62,
+ *                          ParseL3CheckVLAN :66-75) — the VLAN-aware parse the
+ *                          NFFACL_PARSE_VLAN flag substitutes for ParseAllKnownL3
  *   EtherHdr layout        packet/packet.go:96-100 (DAddr, SAddr, EtherType)
  *
  * Packet memory convention: the reference reads raw mbuf memory; here a packet
@@ -82,7 +85,8 @@ static uint32_t u32le(const orc_packet *p, uint32_t off) {
 
 static uint16_t SwapBytesUint16(uint16_t x) { return (uint16_t)(x << 8 | x >> 8); }
 
-enum { EtherLen = 14, IPv6Len = 40, SwapIPV4Number = 0x0008, SwapIPV6Number = 0xdd86 };
+enum { EtherLen = 14, VLANLen = 4, IPv6Len = 40, SwapIPV4Number = 0x0008, SwapIPV6Number = 0xdd86,
+       SwapVLANNumber = 0x0081 };
 
 /* ParseAllKnownL3: returns 4, 6 or 0 */
 static int ParseAllKnownL3(orc_packet *p) {
@@ -91,6 +95,21 @@ static int ParseAllKnownL3(orc_packet *p) {
     if (et == SwapIPV4Number) return 4;        /* GetIPv4 */
     if (et == SwapIPV6Number) return 6;        /* GetIPv6 */
     return 0;                                  /* ARP or unknown: no ACL verdict */
+}
+
+/* ParseAllKnownL3CheckVLAN: one 802.1Q tag moves L3 by VLANLen and the
+ * EtherType compared is the tag's (GetEtherType). */
+static int ParseAllKnownL3CheckVLAN(orc_packet *p) {
+    uint16_t et = u16le(p, 12);
+    if (et == SwapVLANNumber) {               /* ParseL3CheckVLAN */
+        p->L3 = EtherLen + VLANLen;
+        et = u16le(p, EtherLen + 2);          /* VLANHdr.EtherType */
+    } else {
+        p->L3 = EtherLen;
+    }
+    if (et == SwapIPV4Number) return 4;
+    if (et == SwapIPV6Number) return 6;
+    return 0;
 }
 
 static void ParseL4ForIPv4(orc_packet *p) {
@@ -110,11 +129,13 @@ static int l4ACL(const orc_packet *p, const orc_l4 *L4) {
 
 /* l3ACL.  *which (if non-NULL) receives the index of the matching rule in its
  * family slice, or -1 when no rule matches. */
-uint32_t oracle_l3acl_which(const uint8_t *data, uint32_t len, const orc_rule4 *ip4, size_t n4,
-                            const orc_rule6 *ip6, size_t n6, int64_t *which) {
+enum { ORC_PARSE_VLAN = 1 };
+
+uint32_t oracle_l3acl_flags(const uint8_t *data, uint32_t len, const orc_rule4 *ip4, size_t n4,
+                            const orc_rule6 *ip6, size_t n6, int64_t *which, uint32_t flags) {
     orc_packet pkt = {data, len, 0, 0};
     if (which) *which = -1;
-    int fam = ParseAllKnownL3(&pkt);
+    int fam = (flags & ORC_PARSE_VLAN) ? ParseAllKnownL3CheckVLAN(&pkt) : ParseAllKnownL3(&pkt);
     if (fam == 4) {
         uint32_t SrcAddr = u32le(&pkt, pkt.L3 + 12);
         uint32_t DstAddr = u32le(&pkt, pkt.L3 + 16);
@@ -154,6 +175,11 @@ uint32_t oracle_l3acl_which(const uint8_t *data, uint32_t len, const orc_rule4 *
         return 0;
     }
     return 0;
+}
+
+uint32_t oracle_l3acl_which(const uint8_t *data, uint32_t len, const orc_rule4 *ip4, size_t n4,
+                            const orc_rule6 *ip6, size_t n6, int64_t *which) {
+    return oracle_l3acl_flags(data, len, ip4, n4, ip6, n6, which, 0);
 }
 
 uint32_t oracle_l3acl(const uint8_t *data, uint32_t len, const orc_rule4 *ip4, size_t n4,
@@ -196,6 +222,7 @@ typedef struct {
     int64_t *which; /* optional */
     const orc_l2rule *eth; /* non-NULL: L2 ACL instead of L3 */
     size_t neth;
+    uint32_t flags;        /* ORC_PARSE_VLAN */
 } orc_job;
 
 static void *orc_worker(void *arg) {
@@ -211,15 +238,16 @@ static void *orc_worker(void *arg) {
             len = j->stride;
         }
         j->out[i] = j->eth ? oracle_l2acl(pkt, len, j->eth, j->neth)
-                           : oracle_l3acl_which(pkt, len, j->ip4, j->n4, j->ip6, j->n6,
-                                                j->which ? &j->which[i] : NULL);
+                           : oracle_l3acl_flags(pkt, len, j->ip4, j->n4, j->ip6, j->n6,
+                                                j->which ? &j->which[i] : NULL, j->flags);
     }
     return NULL;
 }
 
 static int orc_run_any(const uint8_t *base, const uint64_t *desc, uint32_t stride, uint64_t n,
                        const orc_rule4 *ip4, size_t n4, const orc_rule6 *ip6, size_t n6,
-                       const orc_l2rule *eth, size_t neth, uint32_t *out, int64_t *which, int threads) {
+                       const orc_l2rule *eth, size_t neth, uint32_t *out, int64_t *which, int threads,
+                       uint32_t flags) {
     if (threads < 1) threads = 1;
     if ((uint64_t)threads > n) threads = n ? (int)n : 1;
     pthread_t *tid = (pthread_t *)calloc((size_t)threads, sizeof(pthread_t));
@@ -232,7 +260,7 @@ static int orc_run_any(const uint8_t *base, const uint64_t *desc, uint32_t strid
     uint64_t per = n / (uint64_t)threads, rem = n % (uint64_t)threads, first = 0;
     for (int t = 0; t < threads; t++) {
         uint64_t cnt = per + ((uint64_t)t < rem ? 1 : 0);
-        orc_job j = {base, desc, stride, first, cnt, ip4, n4, ip6, n6, out, which, eth, neth};
+        orc_job j = {base, desc, stride, first, cnt, ip4, n4, ip6, n6, out, which, eth, neth, flags};
         jobs[t] = j;
         first += cnt;
     }
@@ -247,7 +275,20 @@ static int orc_run_any(const uint8_t *base, const uint64_t *desc, uint32_t strid
 static int orc_run(const uint8_t *base, const uint64_t *desc, uint32_t stride, uint64_t n,
                    const orc_rule4 *ip4, size_t n4, const orc_rule6 *ip6, size_t n6,
                    uint32_t *out, int64_t *which, int threads) {
-    return orc_run_any(base, desc, stride, n, ip4, n4, ip6, n6, NULL, 0, out, which, threads);
+    return orc_run_any(base, desc, stride, n, ip4, n4, ip6, n6, NULL, 0, out, which, threads, 0);
+}
+
+/* Dense slots / packed frames with parse flags (ORC_PARSE_VLAN). */
+int oracle_classify_slots_flags(const uint8_t *slots, uint32_t stride, uint64_t n, const orc_rule4 *ip4,
+                                size_t n4, const orc_rule6 *ip6, size_t n6, uint32_t *out, int threads,
+                                uint32_t flags) {
+    return orc_run_any(slots, NULL, stride, n, ip4, n4, ip6, n6, NULL, 0, out, NULL, threads, flags);
+}
+
+int oracle_classify_frames_flags(const uint8_t *frames, const uint64_t *desc, uint64_t n, const orc_rule4 *ip4,
+                                 size_t n4, const orc_rule6 *ip6, size_t n6, uint32_t *out, int threads,
+                                 uint32_t flags) {
+    return orc_run_any(frames, desc, 0, n, ip4, n4, ip6, n6, NULL, 0, out, NULL, threads, flags);
 }
 
 /* Dense slots: packet i is slots[i*stride .. (i+1)*stride). */
@@ -274,13 +315,13 @@ int oracle_classify_frames(const uint8_t *frames, const uint64_t *desc, uint64_t
 int oracle_l2_classify_slots(const uint8_t *slots, uint32_t stride, uint64_t n, const orc_l2rule *eth,
                              size_t neth, uint32_t *out, int threads) {
     static const orc_l2rule none;
-    return orc_run_any(slots, NULL, stride, n, NULL, 0, NULL, 0, neth ? eth : &none, neth, out, NULL, threads);
+    return orc_run_any(slots, NULL, stride, n, NULL, 0, NULL, 0, neth ? eth : &none, neth, out, NULL, threads, 0);
 }
 
 int oracle_l2_classify_frames(const uint8_t *frames, const uint64_t *desc, uint64_t n, const orc_l2rule *eth,
                               size_t neth, uint32_t *out, int threads) {
     static const orc_l2rule none;
-    return orc_run_any(frames, desc, 0, n, NULL, 0, NULL, 0, neth ? eth : &none, neth, out, NULL, threads);
+    return orc_run_any(frames, desc, 0, n, NULL, 0, NULL, 0, neth ? eth : &none, neth, out, NULL, threads, 0);
 }
 
 int oracle_l2rule_size(void) { return (int)sizeof(orc_l2rule); }

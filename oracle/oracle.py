@@ -39,6 +39,10 @@ def _load():
         lib.oracle_classify_slots_which.argtypes = [vp, u32, u64, vp, sz, vp, sz, vp, vp, i]
         lib.oracle_classify_frames.restype = i
         lib.oracle_classify_frames.argtypes = [vp, vp, u64, vp, sz, vp, sz, vp, i]
+        lib.oracle_classify_slots_flags.restype = i
+        lib.oracle_classify_slots_flags.argtypes = [vp, u32, u64, vp, sz, vp, sz, vp, i, u32]
+        lib.oracle_classify_frames_flags.restype = i
+        lib.oracle_classify_frames_flags.argtypes = [vp, vp, u64, vp, sz, vp, sz, vp, i, u32]
         lib.oracle_l2acl.restype = u32
         lib.oracle_l2acl.argtypes = [vp, u32, vp, sz]
         lib.oracle_l2_classify_slots.restype = i
@@ -66,14 +70,18 @@ def l3acl(packet: bytes, a4=None, a6=None) -> int:
     return lib.oracle_l3acl(buf.ctypes.data, len(packet), a4.ctypes.data, len(a4), a6.ctypes.data, len(a6))
 
 
-def classify_slots(slots: np.ndarray, stride: int, n: int, a4=None, a6=None, threads: int = 1) -> np.ndarray:
+PARSE_VLAN = 1  # ParseAllKnownL3CheckVLAN instead of ParseAllKnownL3
+
+
+def classify_slots(slots: np.ndarray, stride: int, n: int, a4=None, a6=None, threads: int = 1,
+                   flags: int = 0) -> np.ndarray:
     lib = _load()
     a4, a6 = _rules(a4, a6)
     slots = np.ascontiguousarray(slots, np.uint8)
     assert slots.size >= n * stride
     out = np.zeros(n, np.uint32)
-    st = lib.oracle_classify_slots(slots.ctypes.data, stride, n, a4.ctypes.data, len(a4),
-                                   a6.ctypes.data, len(a6), out.ctypes.data, threads)
+    st = lib.oracle_classify_slots_flags(slots.ctypes.data, stride, n, a4.ctypes.data, len(a4),
+                                         a6.ctypes.data, len(a6), out.ctypes.data, threads, flags)
     if st != 0:
         raise RuntimeError("oracle_classify_slots failed")
     return out
@@ -94,14 +102,15 @@ def classify_slots_which(slots: np.ndarray, stride: int, n: int, a4=None, a6=Non
     return out, which
 
 
-def classify_frames(frames: np.ndarray, desc: np.ndarray, a4=None, a6=None, threads: int = 1) -> np.ndarray:
+def classify_frames(frames: np.ndarray, desc: np.ndarray, a4=None, a6=None, threads: int = 1,
+                    flags: int = 0) -> np.ndarray:
     lib = _load()
     a4, a6 = _rules(a4, a6)
     frames = np.ascontiguousarray(frames, np.uint8)
     desc = np.ascontiguousarray(desc, np.uint64)
     out = np.zeros(len(desc), np.uint32)
-    st = lib.oracle_classify_frames(frames.ctypes.data, desc.ctypes.data, len(desc), a4.ctypes.data,
-                                    len(a4), a6.ctypes.data, len(a6), out.ctypes.data, threads)
+    st = lib.oracle_classify_frames_flags(frames.ctypes.data, desc.ctypes.data, len(desc), a4.ctypes.data,
+                                          len(a4), a6.ctypes.data, len(a6), out.ctypes.data, threads, flags)
     if st != 0:
         raise RuntimeError("oracle_classify_frames failed")
     return out

@@ -14,6 +14,8 @@ Sources (aregm/nff-go, read as text):
   packet/acl_internal_test.go:1144-1273 L2 match KATs (IPv4 UDP and ARP request packets)
   packet/utils_for_test.go:95-104, packet/arp.go:60-93   ARP request test packet,
   packet/arp_test.go:22                 its layout pinned by gtLineARPRequest
+  packet/vlan_test.go:23-67,239-269     VLAN-tagged IPv4/TCP frame + the headers
+                                        ParseAllKnownL3CheckVLAN must find in it
 
 Outputs:
   kat_packets.json    the test packets as hex
@@ -21,6 +23,7 @@ Outputs:
   parse_kats.json     (rule-file line, expected ip4/ip6 record) cases
   parse_l3_kat.json   8 frames + the header fields packet_test.go expects
   l2_kats.json        L2 parse cases (JSON + text) and the 216 L2 match cases
+  vlan_kat.json       the tagged frame and its expected L3/L4 fields
 
 Run:  python tests/golden/make_kats.py   (deterministic; no inputs)
 """
@@ -295,6 +298,16 @@ def l2_match_cases():
     return cases
 
 
+# ---- VLAN parse KAT (vlan_test.go:23-67, TestParseAllKnownL3CheckVLAN :239-269) ----
+VLAN_KAT = dict(
+    hex="00400540ef240060089fb1f3810000200800450000288a1b00004006000083972015839720811770048a"
+        "0000000100000d9550107c7000000000",
+    tci=32, inner_ethertype=0x0800,
+    src=[131, 151, 32, 21], dst=[131, 151, 32, 129], proto=6,  # IPv4HeaderVLAN
+    sport=6000, dport=1162,                                   # TCPHeaderVLAN
+)
+
+
 def main():
     (HERE / "kat_packets.json").write_text(json.dumps({k: v.hex() for k, v in PACKETS.items()}, indent=1) + "\n")
     c4, c6 = match_cases()
@@ -314,6 +327,7 @@ def main():
     (HERE / "parse_kats.json").write_text(
         "[\n" + ",\n".join(json.dumps(c, separators=(",", ":")) for c in parse_cases()) + "\n]\n")
     (HERE / "parse_l3_kat.json").write_text(json.dumps(parse_l3_kat(), indent=1) + "\n")
+    (HERE / "vlan_kat.json").write_text(json.dumps(VLAN_KAT, indent=1) + "\n")
     l2 = dict(parse=l2_parse_cases(), match=l2_match_cases())
     (HERE / "l2_kats.json").write_text(
         "{\"parse\": [\n" + ",\n".join(json.dumps(c, separators=(",", ":")) for c in l2["parse"]) +

@@ -210,9 +210,13 @@ def _bits(port):
     return np.bitwise_or.reduce(b.reshape(-1, 64) << np.arange(64, dtype=np.uint64), axis=1)
 
 
+L2_ALGOS = [nffacl.ALGO_LINEAR, nffacl.ALGO_INDEXED]
+
+
 @pytest.mark.gpu
+@pytest.mark.parametrize("algo", L2_ALGOS)
 @pytest.mark.parametrize("stride", [64, 128])
-def test_gpu_match_kats(torch_cuda, l2kats, packets, stride):
+def test_gpu_match_kats(torch_cuda, l2kats, packets, stride, algo):
     """All 216 L2 match KATs: one single-rule engine per case over both packets."""
     names = ["ipv4_udp", "arp_request"]
     slots = np.zeros((2, stride), np.uint8)
@@ -220,27 +224,55 @@ def test_gpu_match_kats(torch_cuda, l2kats, packets, stride):
         f = packets[nm][:stride]
         slots[i, :len(f)] = np.frombuffer(f, np.uint8)
     for c in l2kats["match"]:
-        with nffacl.L2Engine(nffacl.L2Rules.from_array(rule_record(c["rule"]))) as eng:
+        with nffacl.L2Engine(nffacl.L2Rules.from_array(rule_record(c["rule"])), algo=algo) as eng:
+            assert eng.algo == algo
             p, _ = _gpu_ports(torch_cuda, eng, slots.reshape(-1), stride, 2)
         assert p[names.index(c["packet"])] == c["want"], c
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("nrules", [1, 16, 256, 2048])
-def test_gpu_synthetic(torch_cuda, nrules):
+@pytest.mark.parametrize("algo", L2_ALGOS)
+@pytest.mark.parametrize("nrules", [1, 16, 256, 2048, 20000])
+def test_gpu_synthetic(torch_cuda, nrules, algo):
     g = synth.gen_l2_rules(nrules, synth.L2_RULE_SEED + nrules)
     rules = nffacl.L2Rules.parse_text(g.text)
     eth = ro.parse_l2_text_table(g.text.encode()).array()
     assert rules.eth().tobytes() == eth.tobytes()
     n = (1 << 18) + 37
     slots = synth.gen_l2_slots(g, n, synth.L2_PACKET_SEED + nrules)
-    with nffacl.L2Engine(rules) as eng:
+    with nffacl.L2Engine(rules, algo=algo) as eng:
+        assert eng.algo == algo
         p, b = _gpu_ports(torch_cuda, eng, slots, 64, n)
     want = oracle.l2_classify_slots(slots, 64, n, eth, threads=16)
     np.testing.assert_array_equal(p, want)
     np.testing.assert_array_equal(b, _bits(want))
     if nrules >= 16:
         assert 0 < (want != 0).sum() < n  # both verdicts occur
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("algo", L2_ALGOS)
+def test_gpu_odd_masks(torch_cuda, algo):
+    """from_array rules with partial EtherType masks and repeated keys: <= 8
+    shapes hash, > 8 fall back to LINEAR under AUTO; both exact."""
+    rng = np.random.default_rng(5)
+    for nshapes in (3, 8, 12):
+        masks = rng.integers(1, 1 << 16, nshapes)
+        eth = np.zeros(400, nffacl.L2RULE)
+        eth["output_number"] = rng.integers(0, 5, 400)
+        eth["id_mask"] = masks[rng.integers(0, nshapes, 400)]
+        eth["id"] = rng.integers(0, 4, 400) * 0x0101
+        eth["saddr_not_any"] = rng.random(400) < 0.3
+        eth["saddr"] = rng.integers(0, 2, (400, 6))
+        n = 1 << 14
+        slots = rng.integers(0, 2, (n, 64), dtype=np.uint8)
+        slots[:, 12:14] = rng.integers(0, 4, (n, 1)) * np.array([1, 1], np.uint8)
+        slots = slots.reshape(-1)
+        with nffacl.L2Engine(nffacl.L2Rules.from_array(eth), algo=algo) as eng:
+            p, _ = _gpu_ports(torch_cuda, eng, slots, 64, n)
+        np.testing.assert_array_equal(p, oracle.l2_classify_slots(slots, 64, n, eth))
+    with nffacl.L2Engine(nffacl.L2Rules.from_array(eth)) as eng:
+        assert eng.algo == nffacl.ALGO_LINEAR  # 12 shapes
 
 
 @pytest.mark.gpu

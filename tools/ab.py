@@ -21,8 +21,10 @@ cfg = sys.argv[1] if len(sys.argv) > 1 else "c2"
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 10
 VARIANTS = {
     "rows": {"NFFACL_TUNE_COAL": "0"},
-    "coal": {"NFFACL_TUNE_COAL": "1"},
     "coal_nt": {"NFFACL_TUNE_COAL": "2"},
+    "pf_768": {"NFFACL_TUNE_COAL": "3", "NFFACL_TUNE_BLOCK": "768"},
+    "pf_896": {"NFFACL_TUNE_COAL": "3", "NFFACL_TUNE_BLOCK": "896"},
+    "pf_1024x1": {"NFFACL_TUNE_COAL": "3", "NFFACL_TUNE_PER_CU": "1"},
 }
 n = 1 << 24
 if cfg == "c1":
