@@ -89,6 +89,51 @@ def pmc_traffic(cfg: str, algo: str, n: int):
         return None
 
 
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline_frames(frames: np.ndarray, desc: np.ndarray, a4, a6, budget_s: float):
+    """C3: the oracle over the same packed IMIX frames (descriptor order)."""
+    from oracle import oracle
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    cores = max(1, min(cores, 16))
+    n = len(desc)
+    cal = min(n, 1 << 15)
+    t = time.perf_counter()
+    oracle.classify_frames(frames, desc[:cal], a4, a6, threads=cores)
+    rate = cal / max(time.perf_counter() - t, 1e-6)
+    sample = int(min(n, max(cal, rate * budget_s)))
+    passes, done, dt = 0, 0, 0.0
+    while True:
+        t = time.perf_counter()
+        ports = oracle.classify_frames(frames, desc[:sample], a4, a6, threads=cores)
+        dt += time.perf_counter() - t
+        passes += 1
+        done += sample
+        if dt >= budget_s or passes >= 50:
+            break
+    one = min(sample, 1 << 15)
+    t1 = time.perf_counter()
+    oracle.classify_frames(frames, desc[:one], a4, a6, threads=1)
+    dt1 = time.perf_counter() - t1
+    return {
+        "value": round(done / dt / 1e6, 3), "unit": "Mpps", "cores": cores, "kind": "port",
+        "sample": f"first {sample} IMIX frames x {passes} pass(es) (oracle/acl_oracle.c = acl.go l3ACL "
+                  f"restated in C, {cores} threads, {dt:.1f}s)",
+        "single_core_mpps": round(one / dt1 / 1e6, 3),
+    }, ports[:sample]
+
+
 def cpu_baseline(slots: np.ndarray, n: int, a4, a6, budget_s: float, eth=None):
     from oracle import oracle
     if eth is not None:
@@ -172,6 +217,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host", action="store_true", help="skip the PCIe-inclusive measurement")
+    ap.add_argument("--no-scatter", action="store_true",
+                    help="N>1: skip the root-scattered (scatter+classify+gather) measurement")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend for N>1 (nccl = RCCL on ROCm)")
     args = ap.parse_args()
@@ -182,6 +229,8 @@ def main():
     from nffacl import dist as nd
 
     rank, world, local = nd.world()
+    if os.environ.get("NFFACL_BENCH_ONE_GPU") == "1":  # rehearse N ranks on one GPU (gloo)
+        local = 0
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
     torch.cuda.set_device(local)
@@ -200,8 +249,8 @@ def main():
     if l2_mode:
         rules = nffacl.L2Rules.parse_text(text)
         n4, n6 = rules.count(), 0
-        eng = nffacl.L2Engine(rules, device=local)
-        algo_name = "linear"
+        eng = nffacl.L2Engine(rules, device=local, algo=algo_id)
+        algo_name = {nffacl.ALGO_LINEAR: "linear", nffacl.ALGO_INDEXED: "indexed"}[eng.algo]
     else:
         rules = nffacl.L3Rules.parse_text(text)
         n4, n6 = rules.counts()
@@ -303,10 +352,33 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBPS, 4),
             "traffic": pmc_traffic(cfg, algo_name, n),
             "kernel_ms_mean": round(float(kms.mean()), 5), "kernel_ms_min": round(float(kms.min()), 5),
-            "kernel_ms_max": round(float(kms.max()), 5),
+            "kernel_ms_p50": round(float(np.median(kms)), 5), "kernel_ms_max": round(float(kms.max()), 5),
+            "kernel_ms_all": [round(float(x), 4) for x in kms],
         },
         "bit_exact_sample": bit_exact,
     }
+
+    # ---- N>1: root-scattered curve (SURVEY.md §8e curve 2; not `value`) ----
+    # rank 0's resident batch is scattered over RCCL/xGMI, classified on every
+    # rank, verdicts gathered back; bit-exact vs rank 0's own classify above.
+    if world > 1 and not args.no_scatter and not frames_mode and not l2_mode:
+        def classify_shard(sl, cnt):
+            sl = sl.to(dev)  # gloo rehearsal: shards arrive in host memory
+            p = torch.empty(cnt, dtype=torch.int32, device=dev)
+            eng.classify_device(sl, 64, cnt, p, None, stream)
+            return p
+        root = d_slots if rank == 0 else None
+        nd.scatter_classify_gather(root, n, 64, classify_shard, dev)  # warm-up
+        times = []
+        for _ in range(3):
+            full, secs = nd.scatter_classify_gather(root, n, 64, classify_shard, dev)
+            times.append(secs)
+        if rank == 0:
+            best = min(times)
+            out["scatter_inclusive"] = {
+                "mpps": round(n / best / 1e6, 1), "ms": round(best * 1e3, 3), "packets": n,
+                "bytes_scattered": n * 64, "bit_exact_vs_local": bool(torch.equal(full.cpu(), port.cpu())),
+            }
 
     # ---- PCIe-inclusive rate (not `value`) ----
     if rank == 0 and not args.no_host and not frames_mode:
@@ -319,9 +391,13 @@ def main():
         out["host_inclusive_mpps"] = round(m / dt / 1e6, 1)
         out["host_inclusive_bit_exact_sample"] = bool((hp[idx[idx < m]] == got[idx[idx < m]]).all())
 
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not frames_mode:
-        cb, cports = cpu_baseline(slots, n, a4, a6, args.cpu_seconds, eth)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        if frames_mode:
+            cb, cports = cpu_baseline_frames(frames, desc, a4, a6, args.cpu_seconds)
+        else:
+            cb, cports = cpu_baseline(slots, n, a4, a6, args.cpu_seconds, eth)
         cb["bit_exact_vs_gpu"] = bool((cports == got[: len(cports)]).all())
+        cb["cpu_model"] = cpu_model()
         out["cpu_baseline"] = cb
     elif rank == 0:
         out["cpu_baseline"] = None

@@ -252,6 +252,36 @@ __device__ __forceinline__ void transpose_batch(const u32x4 (&v)[4], uint32_t la
     }
 }
 
+// Row-swap variant (MODE 4): lane l = 16r + c loads, for instruction j, the
+// 16 bytes at 1024j + 64c + 16r — chunk r of packet 16j + c; every
+// instruction still covers one contiguous KiB.  Register j of row r then holds
+// M[r][j] = chunk r of packet 16j + c, and a 4x4 transpose across the four
+// 16-lane rows (v_permlane16_swap on register pairs (0,1), (2,3), then
+// v_permlane32_swap on (0,2), (1,3): 4 instructions per dword plane) leaves
+// register m of row r = chunk m of packet 16r + c = packet `lane` — no
+// per-lane packet remap, no permit re-order.
+template <bool NT>
+__device__ __forceinline__ void load_rowswap(const uint8_t *__restrict__ wave_base, uint32_t lane, u32x4 (&v)[4]) {
+    const u32x4 *q = reinterpret_cast<const u32x4 *>(wave_base) + 4u * (lane & 15u) + (lane >> 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = NT ? __builtin_nontemporal_load(q + 64 * j) : q[64 * j];
+}
+
+__device__ __forceinline__ void rowswap_batch(const u32x4 (&v)[4], uint32_t (&d)[16]) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {  // dword plane k of every chunk
+        uint32_t a0 = v[0][k], a1 = v[1][k], a2 = v[2][k], a3 = v[3][k];
+        const auto p01 = __builtin_amdgcn_permlane16_swap(a0, a1, false, false);
+        const auto p23 = __builtin_amdgcn_permlane16_swap(a2, a3, false, false);
+        const auto q02 = __builtin_amdgcn_permlane32_swap(p01[0], p23[0], false, false);
+        const auto q13 = __builtin_amdgcn_permlane32_swap(p01[1], p23[1], false, false);
+        d[0 + k] = q02[0];
+        d[4 + k] = q13[0];
+        d[8 + k] = q02[1];
+        d[12 + k] = q13[1];
+    }
+}
+
 // Packet index (within the wave's 64) held by lane l after transpose_batch.
 __device__ __forceinline__ uint32_t coal_packet(uint32_t lane) { return 16u * (lane & 3u) + (lane >> 2); }
 
@@ -376,9 +406,10 @@ __device__ __forceinline__ uint32_t classify_indexed(const T &tab, const Indexed
         const uint32_t shift = v6 ? s6.shift : s4.shift;
         const uint32_t dir = v6 ? s6.off_dir : s4.off_dir;
         base[s] = v6 ? s6.off_ent : s4.off_ent;
-        const uint32_t t = key[s] >> shift;
-        c[s] = tab.ld(dir + t);
-        e[s] = mine ? tab.ld(dir + t + 1) : c[s];
+        const uint32_t t = key[s] >> shift;  // < n_buckets for any key: both reads in range
+        const uint32_t lo = tab.ld(dir + t), hi = tab.ld(dir + t + 1);  // one ds_read2
+        c[s] = lo;
+        e[s] = mine ? hi : lo;
     }
     uint32_t best = kNone, out = 0;
     while (true) {
@@ -457,21 +488,30 @@ k_indexed_slots(const uint8_t *__restrict__ slots, uint32_t stride, uint64_t n, 
     const uint32_t wpb = blockDim.x >> 6;
     const uint64_t wave0 = uint64_t(blockIdx.x) * wpb + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t step = uint64_t(gridDim.x) * wpb * 64;
-    constexpr bool COAL = MODE != 0;
+    constexpr bool RS = MODE == 4;            // lane-contiguous loads + permlane row swaps
+    constexpr bool COAL = MODE != 0 && !RS;   // lane-contiguous loads + quad DPP transpose
     constexpr bool NT = MODE >= 2;
     constexpr bool PF = MODE == 3;  // coalesced + next-batch register prefetch
     const uint32_t mine = COAL ? coal_packet(lane) : lane;  // packet of this lane within the batch
     uint64_t base = wave0 * 64;
     uint32_t d[16];
     u32x4 nv[4];
-    if (!COAL && base < n) load16(slots + (base + lane < n ? base + lane : 0) * stride, d);
+    if (!COAL && !RS && base < n) load16(slots + (base + lane < n ? base + lane : 0) * stride, d);
     if (PF && base + 64 <= n) load_coal<NT>(slots + base * 64, lane, nv);
     for (; base < n; base += step) {
         const uint64_t idx = base + mine;
         const bool live = idx < n;
         const uint8_t *pkt = slots + (live ? idx : 0) * stride;
         uint32_t cur[16];
-        if (COAL) {
+        if (RS) {
+            if (base + 64 <= n) {
+                u32x4 cv[4];
+                load_rowswap<NT>(slots + base * 64, lane, cv);
+                rowswap_batch(cv, cur);
+            } else {
+                load16(pkt, cur);
+            }
+        } else if (COAL) {
             if (base + 64 <= n) {
                 u32x4 cv[4];
                 if (PF) {
@@ -635,7 +675,8 @@ int prepare_kernels() {
     static std::once_flag once;
     static hipError_t err = hipSuccess;
     std::call_once(once, [] {
-        const hipError_t e[10] = {allow_lds(dev::k_indexed_slots<2, true, 0>), allow_lds(dev::k_indexed_slots<4, true, 0>),
+        const hipError_t e[12] = {allow_lds(dev::k_indexed_slots<2, true, 4>), allow_lds(dev::k_indexed_slots<4, true, 4>),
+                                 allow_lds(dev::k_indexed_slots<2, true, 0>), allow_lds(dev::k_indexed_slots<4, true, 0>),
                                  allow_lds(dev::k_indexed_slots<2, true, 1>), allow_lds(dev::k_indexed_slots<4, true, 1>),
                                  allow_lds(dev::k_indexed_slots<2, true, 2>), allow_lds(dev::k_indexed_slots<4, true, 2>),
                                  allow_lds(dev::k_indexed_slots<2, true, 3>), allow_lds(dev::k_indexed_slots<4, true, 3>),
@@ -659,15 +700,17 @@ int launch_slots(nffacl_engine *eng, const DevTable *t, const uint8_t *d_slots, 
         const IndexedLaunch L = indexed_launch(t);
         const uint32_t grid = grid_for(eng, n, L.block, L.per_cu);
         const dim3 g(grid), b(L.block);
-        // load mode: 0 one row per lane, 1 lane-contiguous + transpose (64-byte
-        // slots only), 2 = 1 with non-temporal loads (default: C2 0.220 ms vs
-        // 0.246 / 0.249 for modes 1 / 0, interleaved A/B in one process,
-        // profiles/r1_ab/ab_c2.json)
-        const int mode = stride == 64 ? std::min(3, std::max(0, tune_env("NFFACL_TUNE_COAL", 2))) : 0;
+        // load mode (64-byte slots): 0 one row per lane; 1 lane-contiguous +
+        // quad DPP transpose; 2 = 1 with non-temporal loads; 3 = 2 + register
+        // prefetch; 4 lane-contiguous non-temporal + permlane row-swap
+        // transpose (default).  Interleaved A/B in one process
+        // (profiles/r1_ab/): mode 4 0.2195 ms, 2 0.2203, 0 0.2475 (C2).
+        const int mode = stride == 64 ? std::min(4, std::max(0, tune_env("NFFACL_TUNE_COAL", 4))) : 0;
 #define NFFACL_SLOTS(NS_, LDS_, M_) \
     hipLaunchKernelGGL((dev::k_indexed_slots<NS_, LDS_, M_>), g, b, LDS_ ? L.lds_bytes : 0, stream, d_slots, stride, n, a, d_port, d_permit)
 #define NFFACL_SLOTS_M(NS_, LDS_) \
-    do { if (mode == 3) NFFACL_SLOTS(NS_, LDS_, 3); else if (mode == 2) NFFACL_SLOTS(NS_, LDS_, 2); \
+    do { if (mode == 4) NFFACL_SLOTS(NS_, LDS_, 4); else if (mode == 3) NFFACL_SLOTS(NS_, LDS_, 3); \
+         else if (mode == 2) NFFACL_SLOTS(NS_, LDS_, 2); \
          else if (mode == 1) NFFACL_SLOTS(NS_, LDS_, 1); else NFFACL_SLOTS(NS_, LDS_, 0); } while (0)
         if (L.lds && L.ns == 2) NFFACL_SLOTS_M(2, true);
         else if (L.lds) NFFACL_SLOTS_M(4, true);

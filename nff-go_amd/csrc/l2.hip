@@ -90,21 +90,25 @@ L2Compiled compile_l2(const std::vector<nffacl_l2_rule> &eth, int algo) {
             L2Shape &S = c.shapes[s];
             std::copy(shapes[s].begin(), shapes[s].end(), S.m);
             S.off = static_cast<uint32_t>(c.blob.size());
+            S.off_key = S.off + cap * kL2ProbeDwords;
             S.cap_mask = cap - 1;
             S.first = members[s].front();
-            c.blob.resize(c.blob.size() + size_t(cap) * kL2EntDwords, 0);
+            c.blob.resize(c.blob.size() + size_t(cap) * (kL2ProbeDwords + kL2KeyDwords), 0);
             for (uint32_t i : members[s]) {  // ascending rule index: the first key owner wins
                 const auto &v = rules[i].v;
-                uint32_t h = l2_hash(v[0], v[1], v[2], v[3]) & S.cap_mask;
+                const uint32_t hv = l2_hash(v[0], v[1], v[2], v[3]);
+                uint32_t h = hv & S.cap_mask;
                 while (true) {
-                    uint32_t *e = &c.blob[S.off + size_t(h) * kL2EntDwords];
-                    if (e[4] == 0) {
-                        e[0] = v[0]; e[1] = v[1]; e[2] = v[2]; e[3] = v[3];
-                        e[4] = i + 1;
-                        e[5] = eth[i].output_number;
+                    uint32_t *pw = &c.blob[S.off + size_t(h) * kL2ProbeDwords];
+                    uint32_t *kr = &c.blob[S.off_key + size_t(h) * kL2KeyDwords];
+                    if (pw[1] == 0) {
+                        pw[0] = hv;
+                        pw[1] = i + 1;
+                        kr[0] = v[0]; kr[1] = v[1]; kr[2] = v[2]; kr[3] = v[3];
+                        kr[4] = eth[i].output_number;
                         break;
                     }
-                    if (e[0] == v[0] && e[1] == v[1] && e[2] == v[2] && e[3] == v[3]) break;  // shadowed
+                    if (kr[0] == v[0] && kr[1] == v[1] && kr[2] == v[2] && kr[3] == v[3]) break;  // shadowed
                     h = (h + 1) & S.cap_mask;
                 }
             }
@@ -165,35 +169,58 @@ __device__ __forceinline__ uint32_t classify_l2_linear(const uint32_t (&p)[4], b
     return res;
 }
 
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
 template <bool LDS>
 __device__ __forceinline__ u32x4 l2_ld4(const uint32_t *__restrict__ g, uint32_t i) {
     return LDS ? *reinterpret_cast<const u32x4 *>(&l2_lds[i]) : *reinterpret_cast<const u32x4 *>(g + i);
+}
+template <bool LDS>
+__device__ __forceinline__ u32x2 l2_ld2(const uint32_t *__restrict__ g, uint32_t i) {
+    return LDS ? *reinterpret_cast<const u32x2 *>(&l2_lds[i]) : *reinterpret_cast<const u32x2 *>(g + i);
+}
+template <bool LDS>
+__device__ __forceinline__ uint32_t l2_ld1(const uint32_t *__restrict__ g, uint32_t i) {
+    return LDS ? l2_lds[i] : g[i];
+}
+
+// One hashed probe sequence of shape S for the active lanes: the first probe
+// runs straight-line, the (rare, load factor <= 1/2) continuation in a
+// ballot-uniform loop.
+template <bool LDS>
+__device__ __forceinline__ void l2_probe(const L2Shape &S, const uint32_t (&p)[4], bool active, const uint32_t *tab,
+                                         uint32_t &best, uint32_t &res) {
+    const uint32_t k0 = p[0] & S.m[0], k1 = p[1] & S.m[1], k2 = p[2] & S.m[2], k3 = p[3] & S.m[3];
+    const uint32_t hv = l2_hash(k0, k1, k2, k3);
+    uint32_t h = hv & S.cap_mask;
+    do {
+        if (active) {
+            const u32x2 pw = l2_ld2<LDS>(tab, S.off + h * kL2ProbeDwords);
+            bool hit = false;
+            if (pw.y == 0u) {
+                active = false;  // empty slot: key absent
+            } else if (pw.x == hv) {  // hash match: verify the key
+                const uint32_t at = S.off_key + h * kL2KeyDwords;
+                const u32x4 e = l2_ld4<LDS>(tab, at);
+                hit = e.x == k0 && e.y == k1 && e.z == k2 && e.w == k3;
+                if (hit) {
+                    if (pw.y - 1u < best) { best = pw.y - 1u; res = l2_ld1<LDS>(tab, at + 4); }
+                    active = false;
+                }
+            }
+            if (active && !hit) h = (h + 1u) & S.cap_mask;
+        }
+    } while (ballot(active));
 }
 
 template <bool LDS>
 __device__ __forceinline__ uint32_t classify_l2_hash(const uint32_t (&p)[4], bool live, const L2Args &a) {
     uint32_t best = 0xFFFFFFFFu, res = 0;
-    for (uint32_t s = 0; s < a.n; ++s) {
-        const L2Shape &S = a.shapes[s];
-        bool active = live && S.first < best;  // shapes ascend by first rule index
+#pragma unroll 1
+    for (uint32_t s = 0; s < a.n; ++s) {  // shape fields: scalar loads from the kernel arguments
+        const bool active = live && a.shapes[s].first < best;  // shapes ascend by first rule index
         if (!ballot(active)) break;
-        const uint32_t k0 = p[0] & S.m[0], k1 = p[1] & S.m[1], k2 = p[2] & S.m[2], k3 = p[3] & S.m[3];
-        uint32_t h = l2_hash(k0, k1, k2, k3) & S.cap_mask;
-        while (ballot(active)) {
-            if (active) {
-                const uint32_t at = S.off + h * kL2EntDwords;
-                const u32x4 e = l2_ld4<LDS>(a.tab, at);
-                const u32x4 f = l2_ld4<LDS>(a.tab, at + 4);
-                if (f.x == 0u) {
-                    active = false;  // empty slot: key absent
-                } else if (e.x == k0 && e.y == k1 && e.z == k2 && e.w == k3) {
-                    if (f.x - 1u < best) { best = f.x - 1u; res = f.y; }
-                    active = false;
-                } else {
-                    h = (h + 1u) & S.cap_mask;
-                }
-            }
-        }
+        l2_probe<LDS>(a.shapes[s], p, active, a.tab, best, res);
     }
     return res;
 }
@@ -213,8 +240,11 @@ __device__ __forceinline__ void l2_stage(const L2Args &a) {
     __syncthreads();
 }
 
+// Two 1024-thread workgroups per CU (LDS mode) need 8 waves per SIMD: at most
+// 64 VGPRs and 80 SGPRs (MI355X_MICROARCH.md: blocks per CU <=
+// 800 / (ceil(sgpr/16)*16 + 16)).
 template <int ALGO, bool LDS>
-__global__ void __launch_bounds__(1024)
+__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8)))
 k_l2_slots(const uint8_t *__restrict__ slots, uint32_t stride, uint64_t n, L2Args a,
            uint32_t *__restrict__ port_out, uint64_t *__restrict__ permit_out) {
     l2_stage<LDS>(a);
@@ -229,7 +259,7 @@ k_l2_slots(const uint8_t *__restrict__ slots, uint32_t stride, uint64_t n, L2Arg
 
 // Packed frames: desc = offset << 16 | length; bytes >= length read as 0.
 template <int ALGO, bool LDS>
-__global__ void __launch_bounds__(1024)
+__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8)))
 k_l2_frames(const uint8_t *__restrict__ frames, const uint64_t *__restrict__ desc, uint64_t n, L2Args a,
             uint32_t *__restrict__ port_out, uint64_t *__restrict__ permit_out) {
     l2_stage<LDS>(a);

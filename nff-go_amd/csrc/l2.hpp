@@ -15,7 +15,10 @@
 //          first (lowest-index) rule with that key.  A packet probes every
 //          shape whose first rule precedes its best match so far; the answer
 //          is the lowest rule index found — the reference's first match.
-//          Entry (8 dwords): k0..k3, rule index + 1 (0 = empty), OutputNumber, 0, 0.
+//          Per slot: a 2-dword probe word {32-bit key hash, rule index + 1}
+//          (0 = empty) — one 8-byte read per probe — and, in a parallel
+//          array, the 8-dword key record {k0..k3, OutputNumber, 0, 0, 0}
+//          read only when the hash matches.
 // Rules after the first unconstrained rule (matches everything) are dropped.
 #pragma once
 
@@ -31,15 +34,16 @@
 namespace nffacl {
 
 constexpr uint32_t kL2RecDwords = 8;
-constexpr uint32_t kL2EntDwords = 8;
+constexpr uint32_t kL2ProbeDwords = 2;
+constexpr uint32_t kL2KeyDwords = 8;
 constexpr uint32_t kL2MaxShapes = 8;
 
 struct L2Shape {
     uint32_t m[4];     // header masks of this shape
-    uint32_t off;      // dword offset of its table in the blob
+    uint32_t off;      // dword offset of its probe words (2 dwords per slot)
     uint32_t cap_mask; // table capacity - 1 (power of two)
     uint32_t first;    // lowest rule index of the shape
-    uint32_t pad;
+    uint32_t off_key;  // dword offset of its key records (8 dwords per slot)
 };
 
 struct L2Compiled {

@@ -20,6 +20,7 @@
 // through ACLVectorSeparator / Aggregator for throughput.
 #pragma once
 
+#include <algorithm>
 #include <array>
 #include <cstdint>
 #include <cstring>
@@ -328,6 +329,64 @@ inline VectorSplitFunction ACLVectorSplitter(std::shared_ptr<const packet::L3Rul
         uint32_t ports[vBurstSize] = {0};
         packet::L3ACLPortBatch(sel, n, ports, *rules);
         for (size_t k = 0; k < n; ++k) answers[idx[k]] = static_cast<uint8_t>(ports[k]);
+    };
+}
+
+// One nffacl_batcher per GPU, shared by every flow-function clone: the
+// clones' bursts ride in common GPU batches.
+class SharedBatcher {
+public:
+    SharedBatcher(std::shared_ptr<const packet::L3Rules> rules, uint32_t max_batch = 1 << 16,
+                  uint32_t max_delay_us = 100, uint32_t nbuf = 4)
+        : rules_(std::move(rules)) {
+        const int st = nffacl_batcher_create(rules_->engine(), packet::kSlot, max_batch, max_delay_us, nbuf, &b_);
+        if (st != NFFACL_OK)
+            throw std::runtime_error(std::string("nffacl_batcher_create: ") + nffacl_strerror(st));
+    }
+    SharedBatcher(const SharedBatcher &) = delete;
+    SharedBatcher &operator=(const SharedBatcher &) = delete;
+    ~SharedBatcher() { nffacl_batcher_destroy(b_); }
+
+    // L3ACLPort of n packets (blocks until their batch is back).
+    void Classify(const packet::Packet *const *pkts, size_t n, uint32_t *ports) {
+        const uint8_t *frames[vBurstSize];
+        uint32_t lens[vBurstSize];
+        for (size_t off = 0; off < n; off += vBurstSize) {
+            const size_t m = std::min<size_t>(vBurstSize, n - off);
+            for (size_t i = 0; i < m; ++i) {
+                frames[i] = pkts[off + i]->Ether;
+                lens[i] = pkts[off + i]->Len;
+            }
+            const int st = nffacl_batcher_classify(b_, frames, lens, static_cast<uint32_t>(m), ports + off);
+            if (st != NFFACL_OK)
+                throw std::runtime_error(std::string("nffacl_batcher_classify: ") + nffacl_strerror(st) + " " +
+                                         nffacl_last_error());
+        }
+    }
+    nffacl_batcher_stats Stats() const {
+        nffacl_batcher_stats s{};
+        nffacl_batcher_get_stats(b_, &s);
+        return s;
+    }
+
+private:
+    std::shared_ptr<const packet::L3Rules> rules_;  // keeps the engine alive
+    nffacl_batcher *b_ = nullptr;
+};
+
+// The vector separator of every clone, backed by one shared batcher.
+inline VectorSeparateFunction ACLVectorSeparator(std::shared_ptr<SharedBatcher> batcher) {
+    return [batcher](packet::Packet *const *pkts, const bool *mask, bool *answers) {
+        const packet::Packet *sel[vBurstSize];
+        int idx[vBurstSize];
+        size_t n = 0;
+        for (int i = 0; i < vBurstSize; ++i) {
+            answers[i] = false;
+            if (mask[i] && pkts[i]) { sel[n] = pkts[i]; idx[n++] = i; }
+        }
+        uint32_t ports[vBurstSize] = {0};
+        batcher->Classify(sel, n, ports);
+        for (size_t k = 0; k < n; ++k) answers[idx[k]] = ports[k] > 0;
     };
 }
 

@@ -120,3 +120,25 @@ def gather_verdicts(port: torch.Tensor, n_total: int, device: torch.device | Non
     if c:
         dist.send(port.to(cd).contiguous(), dst)
     return None
+
+
+def scatter_classify_gather(slots_root, n_total: int, stride: int, classify, device, src: int = 0):
+    """The root-scattered deployment end to end (SURVEY.md §8e curve 2): rank
+    `src` holds all n_total slots, every rank receives its 64-aligned shard,
+    runs `classify(shard_slots, count) -> u32/i32 port tensor` on it, and the
+    verdicts come back to `src`.  Returns (full verdict vector on src / None,
+    seconds between the opening and closing barriers, max over ranks)."""
+    import time
+    dev = comm_device(device)
+    dist.barrier()
+    if dev is not None and dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    mine = scatter_slots(slots_root, n_total, stride, device, src)
+    _, cnt = shard(n_total, dist.get_rank(), dist.get_world_size())
+    port = classify(mine, cnt) if cnt else torch.empty(0, dtype=torch.int32, device=dev)
+    full = gather_verdicts(port, n_total, device, src)
+    if dev is not None and dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    dist.barrier()
+    return full, max_over_ranks(time.perf_counter() - t0, device)

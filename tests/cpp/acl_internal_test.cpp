@@ -20,6 +20,8 @@
 #include <cstring>
 #include <string>
 #include <vector>
+#include <atomic>
+#include <thread>
 
 #include "nffgo.hpp"
 
@@ -547,6 +549,50 @@ static void TestInternal_l2ACL_packetARP(T &t) {
     l2Table(t, arpRequestPacket(), idMsk, srcMac, dstMac);
 }
 
+// Many flow-function clones (threads) sharing one batcher: every burst's
+// answers must equal the single-clone separator's (acl.go semantics).
+static void TestVectorSeparatorSharedBatcher(T &t) {
+    const char *dir = std::getenv("NFFACL_GOLDEN");
+    const std::string g = dir ? dir : "tests/golden";
+    auto sep = packet::GetL3ACLFromTextTable(g + "/rules/test-separate-l3rules.conf");
+    if (sep.second) { t.Errorf("cannot load rules"); return; }
+    std::vector<TestPacket> tp;
+    for (int i = 0; i < flow::vBurstSize; ++i) {
+        TestPacket p{ipv4Packet(types::UDPNumber, types::UDPLen, true)};
+        const uint16_t dport = (i % 3 == 0) ? 111 : (i % 3 == 1) ? 222 : 333;
+        p.bytes[36] = uint8_t(dport >> 8);
+        p.bytes[37] = uint8_t(dport);
+        tp.push_back(p);
+    }
+    std::vector<packet::Packet> pk;
+    for (auto &p : tp) pk.push_back(p.pkt());
+    auto batcher = std::make_shared<flow::SharedBatcher>(sep.first, 4096, 50, 4);
+    auto fn = flow::ACLVectorSeparator(batcher);
+    constexpr int kClones = 8, kBursts = 200;
+    std::atomic<int> bad{0};
+    std::vector<std::thread> clones;
+    for (int c = 0; c < kClones; ++c)
+        clones.emplace_back([&, c] {
+            packet::Packet *ptrs[flow::vBurstSize];
+            bool mask[flow::vBurstSize], answers[flow::vBurstSize];
+            for (int b = 0; b < kBursts; ++b) {
+                for (int i = 0; i < flow::vBurstSize; ++i) {
+                    ptrs[i] = &pk[i];
+                    mask[i] = ((i + b + c) % 5) != 0;
+                }
+                fn(ptrs, mask, answers);
+                for (int i = 0; i < flow::vBurstSize; ++i)
+                    if (answers[i] != (mask[i] && i % 3 == 0)) ++bad;
+            }
+        });
+    for (auto &th : clones) th.join();
+    const auto st = batcher->Stats();
+    if (bad) t.Errorf("%d wrong answers", bad.load());
+    if (st.bursts != uint64_t(kClones) * kBursts) t.Errorf("bursts %llu", (unsigned long long)st.bursts);
+    if (st.batches >= st.bursts) t.Errorf("no aggregation: %llu batches for %llu bursts",
+                                          (unsigned long long)st.batches, (unsigned long long)st.bursts);
+}
+
 int main(int argc, char **argv) {
     const std::string which = argc > 1 ? argv[1] : "parse";
     if (which == "parse" || which == "all") {
@@ -567,6 +613,7 @@ int main(int argc, char **argv) {
         run("TestVectorSeparatorStability", TestVectorSeparatorStability);
         run("TestInternal_l2ACL_packetIPv4", TestInternal_l2ACL_packetIPv4);
         run("TestInternal_l2ACL_packetARP", TestInternal_l2ACL_packetARP);
+        run("TestVectorSeparatorSharedBatcher", TestVectorSeparatorSharedBatcher);
     }
     std::printf(g_failed ? "FAIL\n" : "ok\n");
     return g_failed ? 1 : 0;

@@ -47,6 +47,14 @@ def _worker(rank, world_size, port, q):
         if rank == 0:
             want = oracle.classify_slots(full, 64, n_total, a4, a6).view(np.int32)
             ok_gather = bool((gathered.numpy() == want).all())
+        # the same through scatter_classify_gather (bench.py's N>1 scatter-inclusive line)
+        def classify(sl, cnt):
+            return torch.from_numpy(oracle.classify_slots(sl.numpy(), 64, cnt, a4, a6).view(np.int32))
+        full_v, secs = nd.scatter_classify_gather(slots, n_total, 64, classify, None)
+        if rank == 0:
+            ok_gather = ok_gather and bool((full_v.numpy() == want).all()) and secs > 0
+        else:
+            ok_gather = ok_gather and full_v is None
         t = nd.max_over_ranks(float(rank + 1), None)
         dist.barrier()
         dist.destroy_process_group()

@@ -22,9 +22,10 @@ rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 10
 VARIANTS = {
     "rows": {"NFFACL_TUNE_COAL": "0"},
     "coal_nt": {"NFFACL_TUNE_COAL": "2"},
-    "pf_768": {"NFFACL_TUNE_COAL": "3", "NFFACL_TUNE_BLOCK": "768"},
-    "pf_896": {"NFFACL_TUNE_COAL": "3", "NFFACL_TUNE_BLOCK": "896"},
-    "pf_1024x1": {"NFFACL_TUNE_COAL": "3", "NFFACL_TUNE_PER_CU": "1"},
+    "rowswap_nt": {"NFFACL_TUNE_COAL": "4"},
+    # speed-of-light kernels of tools/sol.hip on the same buffer (no classify):
+    "sol_coalesced_nt": {"SOL": "3"},
+    "sol_rows": {"SOL": "1"},
 }
 n = 1 << 24
 if cfg == "c1":
@@ -41,16 +42,41 @@ stream = torch.cuda.current_stream()
 eng = nffacl.Engine(rules)
 
 
+_sol = None
+
+
+def sol_lib():
+    global _sol
+    if _sol is None:
+        import ctypes
+        import subprocess
+        lib_path = ROOT / "tools" / "libsol.so"
+        if not lib_path.exists():
+            subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-shared", "-fPIC",
+                            str(ROOT / "tools" / "sol.hip"), "-o", str(lib_path)], check=True)
+        _sol = ctypes.CDLL(str(lib_path))
+        _sol.sol_run.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+                                 ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    return _sol
+
+
 def run(env, reps=10):
-    saved = {k: os.environ.get(k) for k in env}
-    os.environ.update(env)
+    if "SOL" in env:
+        which = int(env["SOL"])
+        per_cu, block = (4, 256) if which == 3 else (8, 256)
+        launch = lambda: sol_lib().sol_run(which, slots.data_ptr(), n, port.data_ptr(), bits.data_ptr(),  # noqa: E731
+                                           None, per_cu, block, stream.cuda_stream)
+    else:
+        launch = lambda: eng.classify_device(slots, 64, n, port, bits, stream)  # noqa: E731
+    saved = {k: os.environ.get(k) for k in env if k != "SOL"}
+    os.environ.update({k: v for k, v in env.items() if k != "SOL"})
     try:
         for _ in range(2):
-            eng.classify_device(slots, 64, n, port, bits, stream)
+            launch()
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
         for a, b in evs:
             a.record(stream)
-            eng.classify_device(slots, 64, n, port, bits, stream)
+            launch()
             b.record(stream)
         torch.cuda.synchronize()
         return [a.elapsed_time(b) for a, b in evs], port.clone(), bits.clone()
@@ -68,6 +94,8 @@ for r in range(rounds):
     for name, env in VARIANTS.items():
         ts, p, b = run(env)
         times[name] += ts
+        if "SOL" in env:
+            continue
         if ref is None:
             ref = (p, b)
         else:
