@@ -355,17 +355,20 @@ struct IndexedArgs {
 extern __shared__ __attribute__((aligned(16))) uint32_t lds_tab[];
 
 // Table accessors: the whole table staged in LDS, or read through L1/L2.
+// ld4(i): i is a multiple of 4 (entries are 16-byte aligned, table.hpp) and is
+// indexed in vector units so the compiler can emit one ds_read_b128 /
+// global_load_dwordx4 (a byte-offset cast only gets split ds_read2_b32 pairs).
 struct LdsTab {
     __device__ __forceinline__ uint32_t ld(uint32_t i) const { return lds_tab[i]; }
     __device__ __forceinline__ u32x4 ld4(uint32_t i) const {
-        return *reinterpret_cast<const u32x4 *>(&lds_tab[i]);
+        return reinterpret_cast<const u32x4 *>(lds_tab)[i >> 2];
     }
 };
 struct GlobalTab {
     const uint32_t *__restrict__ p;
     __device__ __forceinline__ uint32_t ld(uint32_t i) const { return p[i]; }
     __device__ __forceinline__ u32x4 ld4(uint32_t i) const {
-        return *reinterpret_cast<const u32x4 *>(p + i);
+        return reinterpret_cast<const u32x4 *>(p)[i >> 2];
     }
 };
 

@@ -143,7 +143,7 @@ int upload_l2(int device, const nffacl_l2rules &rules, int algo, L2Table *&out) 
 
 namespace dev {
 
-extern __shared__ uint32_t l2_lds[];
+extern __shared__ __attribute__((aligned(16))) uint32_t l2_lds[];
 
 struct L2Args {
     const uint32_t *tab;
@@ -171,46 +171,35 @@ __device__ __forceinline__ uint32_t classify_l2_linear(const uint32_t (&p)[4], b
 
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
+// i: dword index, a multiple of 4 (ld4) / 2 (ld2) — indexed in vector units
+// so the compiler emits one ds_read_b128 / ds_read_b64
 template <bool LDS>
 __device__ __forceinline__ u32x4 l2_ld4(const uint32_t *__restrict__ g, uint32_t i) {
-    return LDS ? *reinterpret_cast<const u32x4 *>(&l2_lds[i]) : *reinterpret_cast<const u32x4 *>(g + i);
+    return LDS ? reinterpret_cast<const u32x4 *>(l2_lds)[i >> 2] : reinterpret_cast<const u32x4 *>(g)[i >> 2];
 }
 template <bool LDS>
 __device__ __forceinline__ u32x2 l2_ld2(const uint32_t *__restrict__ g, uint32_t i) {
-    return LDS ? *reinterpret_cast<const u32x2 *>(&l2_lds[i]) : *reinterpret_cast<const u32x2 *>(g + i);
+    return LDS ? reinterpret_cast<const u32x2 *>(l2_lds)[i >> 1] : reinterpret_cast<const u32x2 *>(g)[i >> 1];
 }
 template <bool LDS>
 __device__ __forceinline__ uint32_t l2_ld1(const uint32_t *__restrict__ g, uint32_t i) {
     return LDS ? l2_lds[i] : g[i];
 }
 
-// One hashed probe sequence of shape S for the active lanes: the first probe
-// runs straight-line, the (rare, load factor <= 1/2) continuation in a
-// ballot-uniform loop.
+// Shape probes.  The first probe of every shape is straight-line and
+// predicated by selects (inactive lanes read slot 0: a broadcast, no bank
+// conflict); only lanes whose first slot holds another key continue, in a
+// rare ballot-uniform loop (load factor <= 1/2).
 template <bool LDS>
-__device__ __forceinline__ void l2_probe(const L2Shape &S, const uint32_t (&p)[4], bool active, const uint32_t *tab,
-                                         uint32_t &best, uint32_t &res) {
-    const uint32_t k0 = p[0] & S.m[0], k1 = p[1] & S.m[1], k2 = p[2] & S.m[2], k3 = p[3] & S.m[3];
-    const uint32_t hv = l2_hash(k0, k1, k2, k3);
-    uint32_t h = hv & S.cap_mask;
-    do {
-        if (active) {
-            const u32x2 pw = l2_ld2<LDS>(tab, S.off + h * kL2ProbeDwords);
-            bool hit = false;
-            if (pw.y == 0u) {
-                active = false;  // empty slot: key absent
-            } else if (pw.x == hv) {  // hash match: verify the key
-                const uint32_t at = S.off_key + h * kL2KeyDwords;
-                const u32x4 e = l2_ld4<LDS>(tab, at);
-                hit = e.x == k0 && e.y == k1 && e.z == k2 && e.w == k3;
-                if (hit) {
-                    if (pw.y - 1u < best) { best = pw.y - 1u; res = l2_ld1<LDS>(tab, at + 4); }
-                    active = false;
-                }
-            }
-            if (active && !hit) h = (h + 1u) & S.cap_mask;
-        }
-    } while (ballot(active));
+__device__ __forceinline__ u32x2 l2_probe_word(const uint32_t *tab, uint32_t off, uint32_t h) {
+    return l2_ld2<LDS>(tab, off + h * kL2ProbeDwords);
+}
+
+template <bool LDS>
+__device__ __forceinline__ bool l2_key_eq(const uint32_t *tab, uint32_t at, uint32_t k0, uint32_t k1, uint32_t k2,
+                                          uint32_t k3) {
+    const u32x4 e = l2_ld4<LDS>(tab, at);  // `at` is a multiple of 8 dwords
+    return ((e.x ^ k0) | (e.y ^ k1) | (e.z ^ k2) | (e.w ^ k3)) == 0u;
 }
 
 template <bool LDS>
@@ -218,9 +207,25 @@ __device__ __forceinline__ uint32_t classify_l2_hash(const uint32_t (&p)[4], boo
     uint32_t best = 0xFFFFFFFFu, res = 0;
 #pragma unroll 1
     for (uint32_t s = 0; s < a.n; ++s) {  // shape fields: scalar loads from the kernel arguments
-        const bool active = live && a.shapes[s].first < best;  // shapes ascend by first rule index
+        const L2Shape S = a.shapes[s];
+        bool active = live && S.first < best;  // shapes ascend by first rule index
         if (!ballot(active)) break;
-        l2_probe<LDS>(a.shapes[s], p, active, a.tab, best, res);
+        const uint32_t k0 = p[0] & S.m[0], k1 = p[1] & S.m[1], k2 = p[2] & S.m[2], k3 = p[3] & S.m[3];
+        const uint32_t hv = l2_hash(k0, k1, k2, k3);
+        uint32_t h = active ? hv & S.cap_mask : 0u;
+        while (true) {
+            const u32x2 pw = l2_probe_word<LDS>(a.tab, S.off, h);
+            const bool cand = active && pw.y != 0u && pw.x == hv;
+            const bool hit = l2_key_eq<LDS>(a.tab, S.off_key + (cand ? h : 0u) * kL2KeyDwords, k0, k1, k2, k3) && cand;
+            const uint32_t idx = pw.y - 1u;
+            if (hit && idx < best) {  // rare: a first match so far
+                best = idx;
+                res = l2_ld1<LDS>(a.tab, S.off_key + h * kL2KeyDwords + 4);
+            }
+            active = active && pw.y != 0u && !hit;  // another key in this slot: probe on
+            if (!ballot(active)) break;
+            h = active ? (h + 1u) & S.cap_mask : 0u;
+        }
     }
     return res;
 }

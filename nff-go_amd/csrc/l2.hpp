@@ -58,11 +58,14 @@ struct L2Compiled {
 L2Compiled compile_l2(const std::vector<nffacl_l2_rule> &eth, int algo);
 
 // Header hash shared by the host compiler and the kernel.
+// (one multiply: rotations fold the four header dwords, the multiply and
+// shifts mix; collisions cost probes, never correctness)
+__host__ __device__ inline uint32_t l2_rotl(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
 __host__ __device__ inline uint32_t l2_hash(uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
-    uint32_t h = k0 * 0x9E3779B1u ^ k1 * 0x85EBCA77u ^ k2 * 0xC2B2AE3Du ^ k3 * 0x27D4EB2Fu;
+    uint32_t h = k0 ^ l2_rotl(k1, 11) ^ l2_rotl(k2, 19) ^ l2_rotl(k3, 27);
+    h ^= h >> 16;
+    h *= 0x7FEB352Du;
     h ^= h >> 15;
-    h *= 0x2C1B3C6Du;
-    h ^= h >> 13;
     return h;
 }
 
