@@ -85,31 +85,37 @@ L2Compiled compile_l2(const std::vector<nffacl_l2_rule> &eth, int algo) {
         c.algo = NFFACL_ALGO_INDEXED;
         c.n_shapes = static_cast<uint32_t>(shapes.size());
         for (uint32_t s = 0; s < shapes.size(); ++s) {
-            uint32_t cap = 4;
-            while (cap < 2 * members[s].size()) cap <<= 1;
+            uint32_t buckets = 1;  // four slots each, at most half full
+            while (buckets * kL2BucketSlots < 2 * members[s].size()) buckets <<= 1;
+            const uint32_t slots = buckets * kL2BucketSlots;
             L2Shape &S = c.shapes[s];
             std::copy(shapes[s].begin(), shapes[s].end(), S.m);
             S.off = static_cast<uint32_t>(c.blob.size());
-            S.off_key = S.off + cap * kL2ProbeDwords;
-            S.cap_mask = cap - 1;
+            S.off_key = S.off + slots;
+            S.cap_mask = buckets - 1;
             S.first = members[s].front();
-            c.blob.resize(c.blob.size() + size_t(cap) * (kL2ProbeDwords + kL2KeyDwords), 0);
+            c.blob.resize(c.blob.size() + size_t(slots) * (1 + kL2KeyDwords), 0);
             for (uint32_t i : members[s]) {  // ascending rule index: the first key owner wins
                 const auto &v = rules[i].v;
                 const uint32_t hv = l2_hash(v[0], v[1], v[2], v[3]);
-                uint32_t h = hv & S.cap_mask;
-                while (true) {
-                    uint32_t *pw = &c.blob[S.off + size_t(h) * kL2ProbeDwords];
-                    uint32_t *kr = &c.blob[S.off_key + size_t(h) * kL2KeyDwords];
-                    if (pw[1] == 0) {
-                        pw[0] = hv;
-                        pw[1] = i + 1;
-                        kr[0] = v[0]; kr[1] = v[1]; kr[2] = v[2]; kr[3] = v[3];
-                        kr[4] = eth[i].output_number;
-                        break;
+                uint32_t bkt = hv & S.cap_mask;
+                bool placed = false;
+                while (!placed) {
+                    for (uint32_t j = 0; j < kL2BucketSlots && !placed; ++j) {
+                        const uint32_t slot = bkt * kL2BucketSlots + j;
+                        uint32_t *fp = &c.blob[S.off + slot];
+                        uint32_t *kr = &c.blob[S.off_key + size_t(slot) * kL2KeyDwords];
+                        if (*fp == 0) {
+                            *fp = hv | 1u;
+                            kr[0] = v[0]; kr[1] = v[1]; kr[2] = v[2]; kr[3] = v[3];
+                            kr[4] = i;
+                            kr[5] = eth[i].output_number;
+                            placed = true;
+                        } else if (kr[0] == v[0] && kr[1] == v[1] && kr[2] == v[2] && kr[3] == v[3]) {
+                            placed = true;  // shadowed by an earlier rule with the same key
+                        }
                     }
-                    if (kr[0] == v[0] && kr[1] == v[1] && kr[2] == v[2] && kr[3] == v[3]) break;  // shadowed
-                    h = (h + 1) & S.cap_mask;
+                    bkt = (bkt + 1) & S.cap_mask;
                 }
             }
         }
@@ -186,20 +192,39 @@ __device__ __forceinline__ uint32_t l2_ld1(const uint32_t *__restrict__ g, uint3
     return LDS ? l2_lds[i] : g[i];
 }
 
-// Shape probes.  The first probe of every shape is straight-line and
-// predicated by selects (inactive lanes read slot 0: a broadcast, no bank
-// conflict); only lanes whose first slot holds another key continue, in a
-// rare ballot-uniform loop (load factor <= 1/2).
+// Shape lookups: one 16-byte fingerprint-bucket read per shape; a key record
+// only on a fingerprint match; the next bucket only when this one is full and
+// missed (rare at load <= 1/2).  Inactive lanes read bucket 0 (a broadcast).
 template <bool LDS>
-__device__ __forceinline__ u32x2 l2_probe_word(const uint32_t *tab, uint32_t off, uint32_t h) {
-    return l2_ld2<LDS>(tab, off + h * kL2ProbeDwords);
-}
-
-template <bool LDS>
-__device__ __forceinline__ bool l2_key_eq(const uint32_t *tab, uint32_t at, uint32_t k0, uint32_t k1, uint32_t k2,
-                                          uint32_t k3) {
-    const u32x4 e = l2_ld4<LDS>(tab, at);  // `at` is a multiple of 8 dwords
-    return ((e.x ^ k0) | (e.y ^ k1) | (e.z ^ k2) | (e.w ^ k3)) == 0u;
+__device__ __forceinline__ void l2_lookup(const L2Shape &S, const uint32_t (&p)[4], bool go, const uint32_t *tab,
+                                          uint32_t &best, uint32_t &res) {
+    const uint32_t k0 = p[0] & S.m[0], k1 = p[1] & S.m[1], k2 = p[2] & S.m[2], k3 = p[3] & S.m[3];
+    const uint32_t hv = l2_hash(k0, k1, k2, k3);
+    const uint32_t f = hv | 1u;
+    uint32_t bkt = go ? hv & S.cap_mask : 0u;
+    while (true) {
+        const u32x4 fp = l2_ld4<LDS>(tab, S.off + bkt * kL2BucketSlots);
+        uint32_t mm = go ? (uint32_t(fp.x == f) | uint32_t(fp.y == f) << 1 | uint32_t(fp.z == f) << 2 |
+                            uint32_t(fp.w == f) << 3)
+                         : 0u;
+        const bool has_free = (fp.x == 0u) | (fp.y == 0u) | (fp.z == 0u) | (fp.w == 0u);
+        bool hit = false;
+        while (ballot(mm != 0u)) {  // fingerprint matches (almost always one at most)
+            const uint32_t j = mm ? static_cast<uint32_t>(__builtin_ctz(mm)) : 0u;
+            const uint32_t at = S.off_key + (mm ? bkt * kL2BucketSlots + j : 0u) * kL2KeyDwords;
+            const u32x4 e = l2_ld4<LDS>(tab, at);
+            const bool eq = mm != 0u && ((e.x ^ k0) | (e.y ^ k1) | (e.z ^ k2) | (e.w ^ k3)) == 0u;
+            if (eq) {
+                const u32x2 io = l2_ld2<LDS>(tab, at + 4);  // rule index, OutputNumber
+                if (io.x < best) { best = io.x; res = io.y; }
+                hit = true;
+            }
+            mm = eq ? 0u : (mm & (mm - 1u));
+        }
+        go = go && !hit && !has_free;
+        if (!ballot(go)) break;
+        bkt = go ? (bkt + 1u) & S.cap_mask : 0u;
+    }
 }
 
 template <bool LDS>
@@ -208,24 +233,9 @@ __device__ __forceinline__ uint32_t classify_l2_hash(const uint32_t (&p)[4], boo
 #pragma unroll 1
     for (uint32_t s = 0; s < a.n; ++s) {  // shape fields: scalar loads from the kernel arguments
         const L2Shape S = a.shapes[s];
-        bool active = live && S.first < best;  // shapes ascend by first rule index
-        if (!ballot(active)) break;
-        const uint32_t k0 = p[0] & S.m[0], k1 = p[1] & S.m[1], k2 = p[2] & S.m[2], k3 = p[3] & S.m[3];
-        const uint32_t hv = l2_hash(k0, k1, k2, k3);
-        uint32_t h = active ? hv & S.cap_mask : 0u;
-        while (true) {
-            const u32x2 pw = l2_probe_word<LDS>(a.tab, S.off, h);
-            const bool cand = active && pw.y != 0u && pw.x == hv;
-            const bool hit = l2_key_eq<LDS>(a.tab, S.off_key + (cand ? h : 0u) * kL2KeyDwords, k0, k1, k2, k3) && cand;
-            const uint32_t idx = pw.y - 1u;
-            if (hit && idx < best) {  // rare: a first match so far
-                best = idx;
-                res = l2_ld1<LDS>(a.tab, S.off_key + h * kL2KeyDwords + 4);
-            }
-            active = active && pw.y != 0u && !hit;  // another key in this slot: probe on
-            if (!ballot(active)) break;
-            h = active ? (h + 1u) & S.cap_mask : 0u;
-        }
+        const bool go = live && S.first < best;  // shapes ascend by first rule index
+        if (!ballot(go)) break;
+        l2_lookup<LDS>(S, p, go, a.tab, best, res);
     }
     return res;
 }

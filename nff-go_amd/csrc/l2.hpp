@@ -15,10 +15,12 @@
 //          first (lowest-index) rule with that key.  A packet probes every
 //          shape whose first rule precedes its best match so far; the answer
 //          is the lowest rule index found — the reference's first match.
-//          Per slot: a 2-dword probe word {32-bit key hash, rule index + 1}
-//          (0 = empty) — one 8-byte read per probe — and, in a parallel
-//          array, the 8-dword key record {k0..k3, OutputNumber, 0, 0, 0}
-//          read only when the hash matches.
+//          Buckets of four slots (load <= 1/2): a bucket is four 32-bit
+//          fingerprints (key hash | 1; 0 = empty) read with one 16-byte load,
+//          and in a parallel array one 8-dword key record per slot
+//          {k0..k3, rule index, OutputNumber, 0, 0} read only on a
+//          fingerprint match.  A lookup almost always ends in its first
+//          bucket (a match, or a free slot proving absence).
 // Rules after the first unconstrained rule (matches everything) are dropped.
 #pragma once
 
@@ -34,14 +36,14 @@
 namespace nffacl {
 
 constexpr uint32_t kL2RecDwords = 8;
-constexpr uint32_t kL2ProbeDwords = 2;
+constexpr uint32_t kL2BucketSlots = 4;
 constexpr uint32_t kL2KeyDwords = 8;
 constexpr uint32_t kL2MaxShapes = 8;
 
 struct L2Shape {
     uint32_t m[4];     // header masks of this shape
-    uint32_t off;      // dword offset of its probe words (2 dwords per slot)
-    uint32_t cap_mask; // table capacity - 1 (power of two)
+    uint32_t off;      // dword offset of its fingerprint buckets (4 dwords each)
+    uint32_t cap_mask; // buckets - 1 (power of two)
     uint32_t first;    // lowest rule index of the shape
     uint32_t off_key;  // dword offset of its key records (8 dwords per slot)
 };

@@ -305,6 +305,21 @@ def test_stability_separate_split_proportions(torch_cuda, golden):
     with nffacl.Engine(split) as eng:
         p, _ = classify(torch_cuda, eng, slots, 64, n)
     assert (p[0::3] == 1).all() and (p[1::3] == 2).all() and (p[2::3] == 3).all()
+    # dhandle (test-handle-l3rules.conf): the kept third
+    handle = nffacl.L3Rules.from_text_file(golden / "rules" / "test-handle-l3rules.conf")
+    with nffacl.Engine(handle) as eng:
+        p, _ = classify(torch_cuda, eng, slots, 64, n)
+    assert (p != 0).sum() == n // 3 and (p[0::3] == 1).all()
+    # split scenario generator (generatePacket, :425-431): every 5th packet to
+    # dst port 111, the rest to 222 -> outputs 1 / 2 at exactly 20 / 80 %
+    frames5 = []
+    for i in range(n):
+        f = bytearray(frames[i])
+        f[36:38] = (111 if i % 5 == 0 else 222).to_bytes(2, "big")
+        frames5.append(bytes(f))
+    with nffacl.Engine(split) as eng:
+        p, _ = classify(torch_cuda, eng, slot_buffer(frames5, 64), 64, n)
+    assert (p == 1).sum() * 5 == n and (p == 2).sum() * 5 == 4 * n
 
 
 # ---- BASELINE-size properties (2^24 packets, C2) ------------------------------------
