@@ -53,6 +53,7 @@ WORKLOADS = {
     "c5": "C5 100k-rule L3+L4 ACL with port ranges, 64B packets, device-resident",
     "l2": "L2 ACL (acl.go l2ACL), 256 MAC/EtherType rules, 64B packets, device-resident",
 }
+ALGO_NAMES = {1: "linear", 2: "indexed", 3: "hybrid"}  # nffacl.ALGO_*
 L2_RULES = 256
 # L2 reads the 16-byte line holding the Ethernet header and writes 4 B
 BYTES_PER_PACKET_L2 = 20
@@ -212,7 +213,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "l2"])
-    ap.add_argument("--algo", default="auto", choices=["auto", "linear", "indexed"])
+    ap.add_argument("--algo", default="auto", choices=["auto", "linear", "indexed", "hybrid"])
     ap.add_argument("--packets", type=int, default=1 << 24, help="packets per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -240,7 +241,8 @@ def main():
 
     cfg = args.config
     n = args.packets
-    algo_id = {"auto": nffacl.ALGO_AUTO, "linear": nffacl.ALGO_LINEAR, "indexed": nffacl.ALGO_INDEXED}[args.algo]
+    algo_id = {"auto": nffacl.ALGO_AUTO, "linear": nffacl.ALGO_LINEAR, "indexed": nffacl.ALGO_INDEXED,
+               "hybrid": nffacl.ALGO_HYBRID}[args.algo]
 
     # ---- rules: rank 0 generates, RCCL broadcast of the rule file bytes ----
     text, gen = build_rules(cfg)
@@ -250,12 +252,12 @@ def main():
         rules = nffacl.L2Rules.parse_text(text)
         n4, n6 = rules.count(), 0
         eng = nffacl.L2Engine(rules, device=local, algo=algo_id)
-        algo_name = {nffacl.ALGO_LINEAR: "linear", nffacl.ALGO_INDEXED: "indexed"}[eng.algo]
+        algo_name = ALGO_NAMES[eng.algo]
     else:
         rules = nffacl.L3Rules.parse_text(text)
         n4, n6 = rules.counts()
         eng = nffacl.Engine(rules, device=local, algo=algo_id)
-        algo_name = {nffacl.ALGO_LINEAR: "linear", nffacl.ALGO_INDEXED: "indexed"}[eng.algo]
+        algo_name = ALGO_NAMES[eng.algo]
 
     # ---- packets: per-rank shard, resident in HBM before timing ----
     from nffacl import synth

@@ -157,7 +157,11 @@ NFFACL_API int nffacl_rules_get6(const nffacl_rules *rules, size_t i, nffacl_rul
 enum nffacl_algo {
     NFFACL_ALGO_AUTO = 0,   /* library picks (indexed when the rule set allows) */
     NFFACL_ALGO_LINEAR = 1, /* wave-uniform first-match scan (acl.go's loop order) */
-    NFFACL_ALGO_INDEXED = 2 /* host-compiled interval index + ordered candidate lists */
+    NFFACL_ALGO_INDEXED = 2, /* host-compiled interval index + ordered candidate lists */
+    NFFACL_ALGO_HYBRID = 3   /* the same index for tables larger than LDS: bucket
+                                directories in LDS, compact 16-byte candidates and
+                                per-rule records in HBM (CIDR rule sets; AUTO picks
+                                it when the INDEXED table outgrows LDS) */
 };
 
 /* Compile `rules` for HIP device `hip_device` and upload the table. */
@@ -168,7 +172,7 @@ NFFACL_API int nffacl_engine_create_ex(int hip_device, const nffacl_rules *rules
  * Launches issued before the call keep using the previous table. */
 NFFACL_API int nffacl_engine_swap_rules(nffacl_engine *eng, const nffacl_rules *rules);
 NFFACL_API void nffacl_engine_destroy(nffacl_engine *eng);
-/* Algorithm actually compiled into the active table (NFFACL_ALGO_LINEAR/INDEXED). */
+/* Algorithm actually compiled into the active table (NFFACL_ALGO_LINEAR/INDEXED/HYBRID). */
 NFFACL_API int nffacl_engine_algo(const nffacl_engine *eng);
 /* Bytes of the active device table (rule records + index), for reporting. */
 NFFACL_API int nffacl_engine_table_bytes(const nffacl_engine *eng, uint64_t *bytes);
@@ -191,15 +195,16 @@ typedef struct nffacl_dim_info {
 
 typedef struct nffacl_family_info {
     uint32_t n_rec;        /* live rules of the family */
-    uint32_t off_rec;      /* LINEAR: dword offset of the rule records (8 dwords IPv4, 20 IPv6) */
-    uint32_t entry_dwords; /* INDEXED: dwords per entry (8 IPv4, 20 IPv6) */
+    uint32_t off_rec;      /* LINEAR: dword offset of the rule records (8 dwords IPv4, 20 IPv6);
+                              HYBRID: of the cold records (4 dwords IPv4, 16 IPv6) */
+    uint32_t entry_dwords; /* INDEXED: dwords per entry (8 IPv4, 20 IPv6); HYBRID: 4 */
     uint32_t off_resid, n_resid; /* INDEXED: entries scanned linearly (no selective key) */
     nffacl_dim_info dims[4];     /* INDEXED: [dst addr, src addr, dst port, src port] */
 } nffacl_family_info;
 
 typedef struct nffacl_table_info {
-    int32_t algo;        /* NFFACL_ALGO_LINEAR or NFFACL_ALGO_INDEXED */
-    uint32_t reserved;
+    int32_t algo;        /* NFFACL_ALGO_LINEAR, _INDEXED or _HYBRID */
+    uint32_t lds_dwords; /* HYBRID: blob[0, lds_dwords) = the directories staged in LDS */
     uint64_t blob_dwords;
     nffacl_family_info fam[2]; /* [0] IPv4, [1] IPv6 */
 } nffacl_table_info;

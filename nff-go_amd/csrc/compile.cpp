@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <cmath>
 #include <array>
+#include <cstdlib>
 #include <cstring>
 
 namespace nffacl {
@@ -128,6 +129,9 @@ uint32_t pick_rb(size_t n, uint32_t key_bits) {
 
 uint64_t budget_for(size_t n) { return 8ull * n + 65536ull; }
 
+// Fewest rules worth a source-port slot of their own (see assign_family).
+constexpr size_t kMinSportRules = 128;
+
 // Pick the radix width and count the replicated entries of the dimension's
 // bucket lists: start at ~4 buckets per rule and narrow the radix while wide
 // rules would replicate past the budget.
@@ -193,15 +197,22 @@ void emit_entry(const uint32_t *rec, bool v6, uint32_t r, std::vector<uint32_t> 
     }
 }
 
-// Assign the live records of one family to key slots and emit the slots'
-// directories + inline entries and the residual entries.
-void build_family(const std::vector<uint32_t> &recs, uint32_t rw, bool v6, uint32_t n,
-                  std::vector<uint32_t> &blob, FamilyIndex &fi) {
-    static const uint32_t kinds4[4] = {kKeyDst4, kKeySrc4, kKeyDport, kKeySport};
-    static const uint32_t kinds6[4] = {kKeyDst6, kKeySrc6, kKeyDport, kKeySport};
+// Assign the live records of one family to key slots: each rule goes to the
+// slot where its key range covers the least of the key domain; past a slot's
+// replication budget the widest rules move to their next-best slot (or to the
+// residual scan, choice -1).
+struct FamilyPlan {
     DimBuild dims[4];
     std::vector<uint32_t> resid;
-    std::vector<std::array<KeyRange, 4>> rr(n);
+    std::vector<std::array<KeyRange, 4>> rr;
+};
+
+void assign_family(const std::vector<uint32_t> &recs, uint32_t rw, bool v6, uint32_t n, FamilyPlan &plan) {
+    static const uint32_t kinds4[4] = {kKeyDst4, kKeySrc4, kKeyDport, kKeySport};
+    static const uint32_t kinds6[4] = {kKeyDst6, kKeySrc6, kKeyDport, kKeySport};
+    DimBuild *dims = plan.dims;
+    auto &rr = plan.rr;
+    rr.assign(n, {});
     for (int k = 0; k < 4; ++k) {
         dims[k].kind = v6 ? kinds6[k] : kinds4[k];
         dims[k].key_bits = k < 2 ? 32 : 16;
@@ -218,9 +229,26 @@ void build_family(const std::vector<uint32_t> &recs, uint32_t rw, bool v6, uint3
         pref[r] = o;
         choice[r] = kr[o[0]].cover < 1.0 ? o[0] : -1;
     }
+    std::vector<int> rank(n, 0);
+    // A sparsely used source-port slot costs every packet a directory lookup
+    // for few candidates: its rules move to their next-best slot, and the
+    // kernels then run with three slots.
+    size_t n_sport = 0;
+    for (uint32_t r = 0; r < n; ++r) n_sport += choice[r] == 3;
+    const bool no_sport = n_sport > 0 && n_sport < std::max<size_t>(kMinSportRules, n / 256);
+    if (no_sport) {
+        for (uint32_t r = 0; r < n; ++r) {
+            if (choice[r] != 3) continue;
+            int next = -1;
+            while (++rank[r] < 4) {
+                const int cand = pref[r][rank[r]];
+                if (cand != 3 && rr[r][cand].cover < 1.0) { next = cand; break; }
+            }
+            choice[r] = next;
+        }
+    }
     // Bound replication: a slot may hold at most `budget` entries; past it,
     // the widest rules move to their next-best slot (or to the residual scan).
-    std::vector<int> rank(n, 0);
     for (int round = 0; round < 8; ++round) {
         for (int k = 0; k < 4; ++k) {
             dims[k].rules.clear();
@@ -248,7 +276,7 @@ void build_family(const std::vector<uint32_t> &recs, uint32_t rw, bool v6, uint3
                 int next = -1;
                 while (++rank[r] < 4) {
                     const int cand = pref[r][rank[r]];
-                    if (rr[r][cand].cover < 1.0) { next = cand; break; }
+                    if (rr[r][cand].cover < 1.0 && !(no_sport && cand == 3)) { next = cand; break; }
                 }
                 choice[r] = next;
                 moved = true;
@@ -256,12 +284,20 @@ void build_family(const std::vector<uint32_t> &recs, uint32_t rw, bool v6, uint3
         }
         if (!moved) break;
     }
+    plan.resid.clear();
     for (uint32_t r = 0; r < n; ++r)
-        if (choice[r] < 0) resid.push_back(r);
+        if (choice[r] < 0) plan.resid.push_back(r);
+}
+
+// INDEXED: emit the slots' directories + inline entries and the residual entries.
+void build_family(const std::vector<uint32_t> &recs, uint32_t rw, bool v6, uint32_t n,
+                  std::vector<uint32_t> &blob, FamilyIndex &fi) {
+    FamilyPlan plan;
+    assign_family(recs, rw, v6, n, plan);
     const uint32_t ew = v6 ? kEnt6Dwords : kEnt4Dwords;
     fi.entry_dwords = ew;
     for (int k = 0; k < 4; ++k) {
-        DimBuild &d = dims[k];
+        DimBuild &d = plan.dims[k];
         finish_dim(d);
         DimInfo &di = fi.dims[k];
         di.kind = d.kind;
@@ -276,12 +312,262 @@ void build_family(const std::vector<uint32_t> &recs, uint32_t rw, bool v6, uint3
         di.off_ent = static_cast<uint32_t>(blob.size());
         for (uint32_t r : d.ents) emit_entry(recs.data() + size_t(r) * rw, v6, r, blob);
         if (d.ents.empty()) blob.insert(blob.end(), ew, 0u);  // keep entry 0 addressable
-        if (k >= 2 && !d.rules.empty()) fi.port_dims = true;
+        if (!d.rules.empty()) fi.used_slots = k + 1;
     }
     fi.off_resid = static_cast<uint32_t>(blob.size());
-    fi.n_resid = static_cast<uint32_t>(resid.size());
-    for (uint32_t r : resid) emit_entry(recs.data() + size_t(r) * rw, v6, r, blob);
+    fi.n_resid = static_cast<uint32_t>(plan.resid.size());
+    for (uint32_t r : plan.resid) emit_entry(recs.data() + size_t(r) * rw, v6, r, blob);
     while (blob.size() % 4) blob.push_back(0);
+}
+
+// ---------------------------------------------------------------------------
+// Hybrid table (table.hpp): directories sized to an LDS budget, compact
+// 16-byte candidate entries + per-rule cold records in global memory.
+// ---------------------------------------------------------------------------
+
+// A big-endian mask is a prefix iff its complement is 0...01...1.
+bool prefix32(uint32_t m_be) {
+    const uint32_t c = ~m_be;
+    return (c & (c + 1u)) == 0u;
+}
+
+// Prefix length of a 16-byte wire-order mask, or -1 if it is not a prefix.
+int prefix128(const uint32_t *m_le) {
+    int len = 0;
+    bool ended = false;
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t w = bswap32(m_le[k]);
+        if (ended) {
+            if (w) return -1;
+            continue;
+        }
+        if (!prefix32(w)) return -1;
+        const int l = __builtin_popcount(w);
+        len += l;
+        if (l < 32) ended = true;
+    }
+    return len;
+}
+
+// Rules the compact format encodes exactly: CIDR masks (what both parsers
+// produce) and id_mask in {0, 0xff}.
+bool hybrid_encodable(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vector<uint32_t> &rec6,
+                      uint32_t n6) {
+    if (n4 >= kMaxIndexedRules || n6 >= kMaxIndexedRules) return false;
+    for (uint32_t r = 0; r < n4; ++r) {
+        const uint32_t *R = rec4.data() + size_t(r) * kRec4Dwords;
+        const uint32_t idm = (R[4] >> 8) & 0xFFu;
+        if ((idm != 0 && idm != 0xFF) || !prefix32(bswap32(R[1])) || !prefix32(bswap32(R[3]))) return false;
+    }
+    for (uint32_t r = 0; r < n6; ++r) {
+        const uint32_t *R = rec6.data() + size_t(r) * kRec6Dwords;
+        const uint32_t idm = (R[16] >> 8) & 0xFFu;
+        if ((idm != 0 && idm != 0xFF) || prefix128(R + 4) < 0 || prefix128(R + 12) < 0) return false;
+    }
+    return true;
+}
+
+// Port-block bitmap of [mn, mx]: bit b set iff the range meets block b
+// (8192 ports per block); `exact` iff the range is a union of whole blocks.
+uint32_t port_blocks(uint32_t mn, uint32_t mx, bool &exact) {
+    const uint32_t b0 = mn >> kHybPortBlockShift, b1 = mx >> kHybPortBlockShift;
+    exact = (mn & kHybPortBlockMask) == 0 && (mx & kHybPortBlockMask) == kHybPortBlockMask;
+    return ((2u << b1) - 1u) & ~((1u << b0) - 1u);
+}
+
+// Compact entry of record r (table.hpp, "hybrid entry").
+void emit_hyb_entry(const uint32_t *rec, bool v6, uint32_t r, std::vector<uint32_t> &blob) {
+    const uint32_t *m = v6 ? rec + 16 : rec + 4;  // meta, lo, hi
+    uint32_t sa, da, sl, dl;
+    bool cold = false;
+    if (v6) {
+        const int s = prefix128(rec + 4), d = prefix128(rec + 12);
+        sa = bswap32(rec[0]);
+        da = bswap32(rec[8]);
+        sl = static_cast<uint32_t>(std::min(s, 32));
+        dl = static_cast<uint32_t>(std::min(d, 32));
+        cold = s > 32 || d > 32;
+    } else {
+        sa = bswap32(rec[0]);
+        da = bswap32(rec[2]);
+        sl = static_cast<uint32_t>(__builtin_popcount(rec[1]));
+        dl = static_cast<uint32_t>(__builtin_popcount(rec[3]));
+    }
+    const bool pc = (m[0] & kMetaPortCheck) != 0;
+    const uint32_t lo = pc ? m[1] : 0u, hi = pc ? m[2] : 0xFFFFFFFFu;
+    bool es, ed;
+    const uint32_t sbm = port_blocks(lo & 0xFFFFu, hi & 0xFFFFu, es);
+    const uint32_t dbm = port_blocks(lo >> 16, hi >> 16, ed);
+    cold = cold || !es || !ed;
+    const uint32_t exact = ((m[0] >> 8) & 0xFFu) ? kEntExact : 0u;
+    blob.insert(blob.end(), {sa, da, (m[0] & 0xFFu) | exact | (r << kEntIndexShift),
+                             sl | dl << 6 | (cold ? kHybCold : 0u) | sbm << 16 | dbm << 24});
+}
+
+// Cold record of record r: {lo, hi, output, 0} (+ IPv6 extension words).
+void emit_cold(const uint32_t *rec, bool v6, std::vector<uint32_t> &blob) {
+    const uint32_t *m = v6 ? rec + 16 : rec + 4;
+    const bool pc = (m[0] & kMetaPortCheck) != 0;
+    blob.insert(blob.end(), {pc ? m[1] : 0u, pc ? m[2] : 0xFFFFFFFFu, v6 ? rec[19] : rec[7], 0u});
+    if (v6)  // s1 s2 s3 sm1 | sm2 sm3 t1 t2 | t3 tm1 tm2 tm3 (entry_miss_ext layout)
+        blob.insert(blob.end(), {rec[1], rec[2], rec[3], rec[5], rec[6], rec[7],
+                                 rec[9], rec[10], rec[11], rec[13], rec[14], rec[15]});
+}
+
+uint64_t entries_at(const DimBuild &d, uint32_t rb) {
+    const uint32_t shift = d.key_bits - rb;
+    uint64_t total = 0;
+    for (const KeyRange &r : d.ranges) total += uint64_t(r.hi >> shift) - (r.lo >> shift) + 1;
+    return total;
+}
+
+// Radix widths of all eight slots (both families) so that their directories
+// fit `budget` bytes: start every slot at ~4 buckets per rule, then narrow,
+// one bit at a time, the slot whose mean list grows least per byte saved
+// (weighted by its family's share of the rules, a proxy for its share of
+// the traffic).
+void size_directories(DimBuild *const *all, const double *weight, int nd, size_t budget) {
+    std::vector<uint32_t> rb(nd);
+    std::vector<std::vector<double>> mean(nd);
+    auto bytes = [&](int i, uint32_t b) { return all[i]->rules.empty() ? 12.0 : 4.0 * ((1u << b) + 1); };
+    for (int i = 0; i < nd; ++i) {
+        const DimBuild &d = *all[i];
+        if (d.rules.empty()) { rb[i] = 1; continue; }
+        rb[i] = pick_rb(d.rules.size(), d.key_bits);
+        mean[i].assign(rb[i] + 1, 0.0);
+        for (uint32_t b = 1; b <= rb[i]; ++b) mean[i][b] = double(entries_at(d, b)) / double(1u << b);
+    }
+    double total = 0;
+    for (int i = 0; i < nd; ++i) total += bytes(i, rb[i]);
+    while (total > double(budget)) {
+        int best = -1;
+        double best_cost = 0;
+        for (int i = 0; i < nd; ++i) {
+            if (all[i]->rules.empty() || rb[i] <= 1) continue;
+            const double saved = bytes(i, rb[i]) - bytes(i, rb[i] - 1);
+            const double cost = weight[i] * (mean[i][rb[i] - 1] - mean[i][rb[i]]) / saved;
+            if (best < 0 || cost < best_cost) { best = i; best_cost = cost; }
+        }
+        if (best < 0) break;
+        total -= bytes(best, rb[best]) - bytes(best, rb[best] - 1);
+        --rb[best];
+    }
+    for (int i = 0; i < nd; ++i) {
+        DimBuild &d = *all[i];
+        d.rb = rb[i];
+        d.shift = d.key_bits - rb[i];
+    }
+}
+
+// Bucket lists of a slot at its chosen radix width (ascending rule order).
+void fill_lists(DimBuild &d) {
+    const size_t nb = size_t(1) << d.rb;
+    std::vector<uint32_t> len(nb, 0);
+    for (const KeyRange &r : d.ranges)
+        for (uint64_t t = r.lo >> d.shift; t <= (r.hi >> d.shift); ++t) ++len[t];
+    d.dir.assign(nb + 1, 0);
+    d.max_list = 0;
+    for (size_t t = 0; t < nb; ++t) {
+        d.dir[t + 1] = d.dir[t] + len[t];
+        d.max_list = std::max(d.max_list, len[t]);
+    }
+    d.ents.assign(d.dir[nb], 0);
+    std::vector<uint32_t> fill(d.dir.begin(), d.dir.end() - 1);
+    for (size_t i = 0; i < d.rules.size(); ++i)
+        for (uint64_t t = d.ranges[i].lo >> d.shift; t <= (d.ranges[i].hi >> d.shift); ++t)
+            d.ents[fill[t]++] = d.rules[i];
+}
+
+// Directory budget override (tuning experiments); 0 = the default policy.
+size_t tuned_dir_budget() {
+    const char *v = std::getenv("NFFACL_TUNE_DIR_KB");
+    const long kb = v && *v ? std::atol(v) : 0;
+    return kb > 0 ? size_t(kb) * 1024 : 0;
+}
+
+// Radix widths for `budget` bytes of directories, then the bucket lists;
+// returns the expected candidates per packet (mean list length summed over
+// the slots, families weighted by their share of the rules).
+double size_and_fill(DimBuild *const *all, const double *weight, size_t budget) {
+    size_directories(all, weight, 8, budget);
+    double expect = 0;
+    for (int i = 0; i < 8; ++i) {
+        DimBuild &d = *all[i];
+        if (d.rules.empty()) {
+            d.rb = 1;
+            d.shift = d.key_bits - 1;
+            d.dir.assign(3, 0);
+            d.ents.clear();
+            d.max_list = 0;
+        } else {
+            fill_lists(d);
+            expect += weight[i] * double(d.ents.size()) / double(size_t(1) << d.rb);
+        }
+    }
+    return expect;
+}
+
+void build_hybrid(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vector<uint32_t> &rec6, uint32_t n6,
+                  CompiledTable &out) {
+    FamilyPlan plan[2];
+    assign_family(rec4, kRec4Dwords, false, n4, plan[0]);
+    assign_family(rec6, kRec6Dwords, true, n6, plan[1]);
+    DimBuild *all[8];
+    for (int f = 0; f < 2; ++f)
+        for (int k = 0; k < 4; ++k) all[4 * f + k] = &plan[f].dims[k];
+    double weight[8];
+    for (int i = 0; i < 8; ++i) weight[i] = double(i < 4 ? n4 : n6) / double(std::max<uint32_t>(1, n4 + n6));
+    // Policy (profiles/r1_hybrid/): directories in LDS with per-lane walks
+    // while that keeps the expected candidates per packet short; past that,
+    // wide directories in global memory and the wave-flattened candidates.
+    const size_t tuned = tuned_dir_budget();
+    bool flat;
+    if (tuned) {
+        size_and_fill(all, weight, tuned);
+        flat = tuned > kLdsTableBytes;
+    } else {
+        flat = size_and_fill(all, weight, kHybLaneDirBytes) > kHybFlatCandidates;
+        if (flat) size_and_fill(all, weight, kHybFlatDirBytes);
+    }
+    std::vector<uint32_t> &blob = out.blob;
+    FamilyIndex *fi[2] = {&out.idx4, &out.idx6};
+    // LDS image: the eight directories (values patched to absolute entry numbers below)
+    for (int f = 0; f < 2; ++f)
+        for (int k = 0; k < 4; ++k) {
+            fi[f]->dims[k].off_dir = static_cast<uint32_t>(blob.size());
+            blob.insert(blob.end(), all[4 * f + k]->dir.begin(), all[4 * f + k]->dir.end());
+        }
+    while (blob.size() % 4) blob.push_back(0);
+    out.lds_dwords = flat ? 0u : static_cast<uint32_t>(blob.size());
+    // global part: candidate lists, residual lists, cold records
+    const std::vector<uint32_t> *recs[2] = {&rec4, &rec6};
+    const uint32_t rw[2] = {kRec4Dwords, kRec6Dwords};
+    for (int f = 0; f < 2; ++f) {
+        const bool v6 = f == 1;
+        fi[f]->entry_dwords = kHybEntDwords;
+        for (int k = 0; k < 4; ++k) {
+            DimBuild &d = *all[4 * f + k];
+            DimInfo &di = fi[f]->dims[k];
+            di.kind = d.kind;
+            di.shift = d.shift;
+            di.n_buckets = 1u << d.rb;
+            di.n_rules = static_cast<uint32_t>(d.rules.size());
+            di.n_ent = d.ents.size();
+            di.max_list = d.max_list;
+            di.off_ent = static_cast<uint32_t>(blob.size());
+            const uint32_t first = di.off_ent / kHybEntDwords;
+            for (size_t t = 0; t <= di.n_buckets; ++t) blob[di.off_dir + t] += first;
+            for (uint32_t r : d.ents) emit_hyb_entry(recs[f]->data() + size_t(r) * rw[f], v6, r, blob);
+            if (!d.rules.empty()) fi[f]->used_slots = k + 1;
+        }
+        fi[f]->off_resid = static_cast<uint32_t>(blob.size());
+        fi[f]->n_resid = static_cast<uint32_t>(plan[f].resid.size());
+        for (uint32_t r : plan[f].resid) emit_hyb_entry(recs[f]->data() + size_t(r) * rw[f], v6, r, blob);
+    }
+    out.off_rec4 = static_cast<uint32_t>(blob.size());
+    for (uint32_t r = 0; r < n4; ++r) emit_cold(rec4.data() + size_t(r) * kRec4Dwords, false, blob);
+    out.off_rec6 = static_cast<uint32_t>(blob.size());
+    for (uint32_t r = 0; r < n6; ++r) emit_cold(rec6.data() + size_t(r) * kRec6Dwords, true, blob);
 }
 
 // Indexed tables encode id_mask as one bit and the rule index in 23 bits.
@@ -297,7 +583,8 @@ bool indexable(const nffacl_rules &rules) {
 }  // namespace
 
 bool compile_table(const nffacl_rules &rules, int algo, CompiledTable &out, std::string &err) {
-    if (algo != NFFACL_ALGO_AUTO && algo != NFFACL_ALGO_LINEAR && algo != NFFACL_ALGO_INDEXED) {
+    if (algo != NFFACL_ALGO_AUTO && algo != NFFACL_ALGO_LINEAR && algo != NFFACL_ALGO_INDEXED &&
+        algo != NFFACL_ALGO_HYBRID) {
         err = "unknown algorithm";
         return false;
     }
@@ -311,17 +598,31 @@ bool compile_table(const nffacl_rules &rules, int algo, CompiledTable &out, std:
         if (emit_rec6(r, rec6)) ++out.n6;
     // AUTO = INDEXED whenever encodable: with the lane-contiguous loads even
     // 5 rules classify faster indexed (C1: 70.2 vs 67.3 Gpps LINEAR,
-    // profiles/r1_configs_k/).
-    const bool indexed = algo != NFFACL_ALGO_LINEAR && indexable(rules);
-    out.algo = indexed ? NFFACL_ALGO_INDEXED : NFFACL_ALGO_LINEAR;
-    if (!indexed) {
+    // profiles/r1_configs_k/) — unless its inline table outgrows LDS, where
+    // HYBRID keeps the directories in LDS and the lists compact in HBM.
+    if (algo == NFFACL_ALGO_HYBRID && !hybrid_encodable(rec4, out.n4, rec6, out.n6)) algo = NFFACL_ALGO_INDEXED;
+    if (algo == NFFACL_ALGO_HYBRID) {
+        out.algo = NFFACL_ALGO_HYBRID;
+        build_hybrid(rec4, out.n4, rec6, out.n6, out);
+    } else if (algo != NFFACL_ALGO_LINEAR && indexable(rules)) {
+        out.algo = NFFACL_ALGO_INDEXED;
+        build_family(rec4, kRec4Dwords, false, out.n4, out.blob, out.idx4);
+        build_family(rec6, kRec6Dwords, true, out.n6, out.blob, out.idx6);
+        if (algo == NFFACL_ALGO_AUTO && out.blob.size() * 4 > kLdsTableBytes &&
+            hybrid_encodable(rec4, out.n4, rec6, out.n6)) {
+            const uint32_t n4 = out.n4, n6 = out.n6;
+            out = CompiledTable{};
+            out.n4 = n4;
+            out.n6 = n6;
+            out.algo = NFFACL_ALGO_HYBRID;
+            build_hybrid(rec4, n4, rec6, n6, out);
+        }
+    } else {
+        out.algo = NFFACL_ALGO_LINEAR;
         out.off_rec4 = 0;
         out.off_rec6 = static_cast<uint32_t>(rec4.size());
         out.blob = rec4;
         out.blob.insert(out.blob.end(), rec6.begin(), rec6.end());
-    } else {
-        build_family(rec4, kRec4Dwords, false, out.n4, out.blob, out.idx4);
-        build_family(rec6, kRec6Dwords, true, out.n6, out.blob, out.idx6);
     }
     if (out.blob.empty()) out.blob.push_back(0);  // keep a valid allocation
     while (out.blob.size() % 4) out.blob.push_back(0);

@@ -29,7 +29,7 @@ struct FamilyIndex {
     uint32_t entry_dwords = 0;  // 8 (IPv4) or 20 (IPv6)
     DimInfo dims[4];
     uint32_t off_resid = 0, n_resid = 0;  // residual entries (scanned linearly)
-    bool port_dims = false;               // slot 2 or 3 non-empty
+    uint32_t used_slots = 0;              // 1 + last non-empty slot (kernels walk that many)
 };
 
 struct CompiledTable {
@@ -39,11 +39,14 @@ struct CompiledTable {
     // LINEAR: rule records (dword offsets into blob) and live record counts.
     uint32_t off_rec4 = 0, n4 = 0;
     uint32_t off_rec6 = 0, n6 = 0;
-    // INDEXED: per family key slots + residual entries.
+    // INDEXED / HYBRID: per family key slots + residual entries.
+    // HYBRID: off_rec4/off_rec6 = the cold records; blob[0, lds_dwords) = the
+    // directories staged in LDS.
     FamilyIndex idx4, idx6;
+    uint32_t lds_dwords = 0;
 };
 
-// Compile `rules`.  algo: NFFACL_ALGO_LINEAR, NFFACL_ALGO_INDEXED or AUTO.
+// Compile `rules`.  algo: NFFACL_ALGO_LINEAR, _INDEXED, _HYBRID or AUTO.
 bool compile_table(const nffacl_rules &rules, int algo, CompiledTable &out, std::string &err);
 
 }  // namespace nffacl

@@ -25,6 +25,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <type_traits>
 
 #include "compile.hpp"
 #include "devutil.hpp"
@@ -344,12 +345,26 @@ struct SlotArgs {
 struct FamArgs {
     SlotArgs slot[4];  // [dst addr, src addr, dst port, src port]
     uint32_t off_resid, n_resid;
+    uint32_t off_cold;  // HYBRID: cold records
 };
 struct IndexedArgs {
-    const uint32_t *tab;  // device table (global memory)
-    uint32_t tab_dwords;  // multiple of 4
-    uint32_t flags;       // NFFACL_PARSE_*
+    const uint32_t *tab;    // device table (global memory)
+    uint32_t stage_dwords;  // leading dwords staged in LDS (multiple of 4)
+    uint32_t flags;         // NFFACL_PARSE_*
     FamArgs f4, f6;
+};
+
+// Table placement (kernel template argument).
+enum TableMode : int {
+    kTabGlobal = 0,  // INDEXED, read through L1/L2/MALL
+    kTabLds = 1,     // INDEXED, staged whole in LDS
+    kTabHybrid = 2,  // HYBRID: directories in LDS, lists + cold records global
+    kTabHybrid2 = 3, // HYBRID, two list entries per slot per loop trip
+    kTabHybrid4 = 6, // HYBRID, four
+    kTabFlat = 4,    // HYBRID table, directories read from global memory, the
+                     // candidates of a wave's 64 packets tested 64 at a time,
+                     // 2 rounds of loads in flight
+    kTabFlat4 = 5,   // the same, 4 rounds in flight
 };
 
 extern __shared__ __attribute__((aligned(16))) uint32_t lds_tab[];
@@ -465,13 +480,300 @@ __device__ __forceinline__ uint32_t classify_indexed(const T &tab, const Indexed
 __device__ __forceinline__ void stage_table(const IndexedArgs &a) {
     const u32x4 *src = reinterpret_cast<const u32x4 *>(a.tab);
     u32x4 *dst = reinterpret_cast<u32x4 *>(lds_tab);
-    for (uint32_t i = threadIdx.x; i < a.tab_dwords / 4; i += blockDim.x) dst[i] = src[i];
+    for (uint32_t i = threadIdx.x; i < a.stage_dwords / 4; i += blockDim.x) dst[i] = src[i];
     __syncthreads();
 }
 
-template <int NS, bool LDS>
+// ---- HYBRID (table.hpp "hybrid table") --------------------------------------
+
+// Top-L-bits mask of a big-endian word, L in 0..32 (one 64-bit shift).
+__device__ __forceinline__ uint32_t prefix_mask(uint32_t L) {
+    return static_cast<uint32_t>(0xFFFFFFFF00000000ull >> L);
+}
+
+// Common test of a compact entry: addresses under their prefix lengths,
+// protocol, port blocks.  ks/kd: big-endian src/dst (top) words; pb: the
+// packet's port-block bits (1 << 16 + sport/8192 | 1 << 24 + dport/8192).
+__device__ __forceinline__ bool hyb_pass(const u32x4 &E, uint32_t ks, uint32_t kd, uint32_t proto, uint32_t pb) {
+    const uint32_t w = E.w;
+    const uint32_t pm = ((proto ^ E.z) & 0xFFu) & (0u - ((E.z >> 8) & 1u));
+    const uint32_t m = ((ks ^ E.x) & prefix_mask(w & 63u)) | ((kd ^ E.y) & prefix_mask((w >> 6) & 63u)) | pm;
+    const uint32_t q = w & pb;
+    return m == 0u && (q & 0x00FF0000u) != 0u && (q & 0xFF000000u) != 0u;
+}
+
+// Exact confirmation on the cold record of rule `idx`: ports (l4ACL) and,
+// for IPv6, address words 1..3.
+__device__ __forceinline__ bool hyb_cold_ok(const IndexedArgs &a, bool v6, uint32_t idx, const Fields &f) {
+    const GlobalTab g{a.tab};
+    const uint32_t off = v6 ? a.f6.off_cold + idx * kHybCold6Dwords : a.f4.off_cold + idx * kHybCold4Dwords;
+    const u32x4 C = g.ld4(off);
+    uint32_t m = port_miss(f.ports, C.x, C.y);
+    if (v6) m |= entry_miss_ext(g, off + 4, f);
+    return m == 0u;
+}
+
+// One candidate of a slot list: the common test, confirmed on the cold
+// record when the entry says so (ballot-gated: only waves with such a lane
+// pay the cold read).  Returns true while the walk must go on.
+__device__ __forceinline__ bool hyb_step(const IndexedArgs &a, const Fields &f, bool act, const u32x4 &E,
+                                         uint32_t ks, uint32_t kd, uint32_t pb, uint32_t &best) {
+    const uint32_t idx = E.z >> kEntIndexShift;
+    const bool earlier = act && idx < best;
+    bool pass = hyb_pass(E, ks, kd, f.proto, pb);
+    const bool cold = earlier && pass && (E.w & kHybCold);
+    if (ballot(cold)) {
+        if (cold) pass = hyb_cold_ok(a, f.is6, idx, f);
+    }
+    const bool take = earlier && pass;
+    best = take ? idx : best;
+    // stop at a hit, or once the ascending list has passed `best`
+    return earlier && !pass;
+}
+
+// U = list entries per slot per loop trip (both loads issued together).
+template <int NS, int U>
+__device__ __forceinline__ uint32_t classify_hybrid(const IndexedArgs &a, const Fields &f) {
+    const bool v6 = f.is6;
+    const bool mine = f.is4 || f.is6;
+    const uint32_t ks = __builtin_bswap32(f.s[0]), kd = __builtin_bswap32(f.t[0]);
+    const uint32_t sport = f.ports & 0xFFFFu, dport = f.ports >> 16;
+    const uint32_t key[4] = {kd, ks, dport, sport};
+    const uint32_t pb = (1u << (16 + (sport >> kHybPortBlockShift))) | (1u << (24 + (dport >> kHybPortBlockShift)));
+    const u32x4 *G = reinterpret_cast<const u32x4 *>(a.tab);
+    uint32_t c[NS], e[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        const SlotArgs &s4 = a.f4.slot[s], &s6 = a.f6.slot[s];
+        const uint32_t shift = v6 ? s6.shift : s4.shift;
+        const uint32_t dir = v6 ? s6.off_dir : s4.off_dir;
+        const uint32_t t = key[s] >> shift;
+        const uint32_t lo = lds_tab[dir + t], hi = lds_tab[dir + t + 1];  // one ds_read2
+        c[s] = lo;
+        e[s] = mine ? hi : lo;
+    }
+    uint32_t best = kNone;
+    while (true) {
+        bool any = false;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) any |= c[s] < e[s];
+        if (!ballot(any)) break;
+        u32x4 E[NS][U];
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+#pragma unroll
+            for (int u = 0; u < U; ++u) E[s][u] = G[c[s] + u < e[s] ? c[s] + u : 0u];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            bool go = true;
+#pragma unroll
+            for (int u = 0; u < U; ++u) go = hyb_step(a, f, go && c[s] + u < e[s], E[s][u], ks, kd, pb, best);
+            c[s] = go ? c[s] + U : e[s];
+        }
+    }
+    // rules with no selective key: wave-uniform scan in rule order per family
+#pragma unroll
+    for (int fam = 0; fam < 2; ++fam) {
+        const FamArgs &fa = fam ? a.f6 : a.f4;
+        const bool in_fam = fam ? f.is6 : f.is4;
+        for (uint32_t i = 0; i < fa.n_resid; ++i) {
+            const u32x4 E = G[(fa.off_resid >> 2) + i];
+            const uint32_t idx = E.z >> kEntIndexShift;
+            const bool want = in_fam && idx < best;
+            if (!ballot(want)) break;  // residual list ascends too
+            bool pass = want && hyb_pass(E, ks, kd, f.proto, pb);
+            const bool cold = pass && (E.w & kHybCold);
+            if (ballot(cold)) {
+                if (cold) pass = hyb_cold_ok(a, fam == 1, idx, f);
+            }
+            best = pass ? idx : best;
+        }
+    }
+    // the winner's output number, from its cold record
+    const bool hit = best != kNone;
+    uint32_t out = 0;
+    if (ballot(hit)) {
+        if (hit) out = a.tab[v6 ? a.f6.off_cold + best * kHybCold6Dwords + 2 : a.f4.off_cold + best * kHybCold4Dwords + 2];
+    }
+    return out;
+}
+
+// ---- FLAT: a wave's candidates, 64 at a time --------------------------------
+//
+// The list walks above cost one dependent table round trip per loop trip, and
+// a wave takes as many trips as its longest walk.  For tables that live in
+// L2/MALL that latency, not bandwidth, bounds the kernel (C5: 13 trips of
+// ~3 us per 64 packets).  Here every lane first looks up the list bounds of
+// its packet in each slot (one round trip), the wave lays all (packet, slot,
+// entry) candidates end to end (exclusive scan of the list lengths), and
+// round r gives lane l candidate 64 r + l: one table load per lane per round,
+// all 64 lanes busy, ceil(total / 64) rounds.  A lane finds its candidate's
+// list through an LDS window: every list overlapping the round's 64
+// positions marks its first position there, a prefix max over the window
+// carries the mark forward.  Each passing candidate posts its rule index to
+// the packet's LDS minimum (ds_min_u32): the minimum over every candidate is
+// the first match of the ordered lists, no early exit needed.
+constexpr int kFlatMaxRounds = 4;
+struct FlatScratch {
+    uint32_t mark[64 * kFlatMaxRounds];   // window position -> (list id << 8 | position) + 1, 0 = none
+    uint32_t delta[64 * kFlatMaxRounds];  // window position -> entry number - candidate number
+    uint32_t best[64];                    // per packet (lane): lowest passing rule index
+};
+
+// Order this wave's LDS writes before its following LDS reads of other lanes'
+// words (one wave: program order on the LDS queue; this keeps the compiler
+// from reordering across it).
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ uint32_t bperm(uint32_t v, uint32_t src_lane) {
+    return static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(static_cast<int>(src_lane << 2), static_cast<int>(v)));
+}
+
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x, uint32_t lane) {
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t y = bperm(x, lane >= d ? lane - d : lane);
+        x += lane >= d ? y : 0u;
+    }
+    return x;
+}
+
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x, uint32_t lane) {
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t y = bperm(x, lane >= d ? lane - d : lane);
+        x = max(x, y);
+    }
+    return x;
+}
+
+template <int NS, int R>
+__device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fields &f, FlatScratch &W,
+                                                  uint32_t lane) {
+    const bool v6 = f.is6;
+    const bool mine = f.is4 || f.is6;
+    const uint32_t ks = __builtin_bswap32(f.s[0]), kd = __builtin_bswap32(f.t[0]);
+    const uint32_t sport = f.ports & 0xFFFFu, dport = f.ports >> 16;
+    const uint32_t key[4] = {kd, ks, dport, sport};
+    const u32x4 *G = reinterpret_cast<const u32x4 *>(a.tab);
+    // list bounds of this packet in every slot (directories in global memory)
+    uint32_t st[NS], ln[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        const SlotArgs &s4 = a.f4.slot[s], &s6 = a.f6.slot[s];
+        const uint32_t shift = v6 ? s6.shift : s4.shift;
+        const uint32_t dir = v6 ? s6.off_dir : s4.off_dir;
+        const uint32_t t = key[s] >> shift;
+        st[s] = a.tab[dir + t];
+        ln[s] = mine ? a.tab[dir + t + 1] - st[s] : 0u;
+    }
+    uint32_t total = 0;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) total += ln[s];
+    const uint32_t incl = wave_incl_sum(total, lane);
+    const uint32_t off = incl - total;  // first candidate number of this packet
+    const uint32_t T = __builtin_amdgcn_readlane(incl, 63);
+    W.best[lane] = kNone;
+    const uint32_t proto_fam = f.proto | (v6 ? 0x100u : 0u);
+    for (uint32_t win = 0; win < T; win += 64 * R) {
+#pragma unroll
+        for (int j = 0; j < R; ++j) W.mark[64 * j + lane] = 0u;
+        wave_lds_sync();
+        uint32_t so = off;  // candidate number of list s's first entry
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            if (ln[s] != 0u && so < win + 64u * R && so + ln[s] > win) {
+                const uint32_t pos = so > win ? so - win : 0u;
+                W.mark[pos] = (((lane * NS + s) << 8) | pos) + 1u;
+                W.delta[pos] = st[s] - so;
+            }
+            so += ln[s];
+        }
+        wave_lds_sync();
+        // R rounds: locate every candidate's list, then issue all R loads
+        uint32_t owner[R];
+        bool valid[R];
+        u32x4 E[R];
+        uint32_t carry = 0;
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            const uint32_t m = max(wave_incl_max(W.mark[64 * j + lane], lane), carry);
+            carry = __builtin_amdgcn_readlane(m, 63);
+            const uint32_t k = win + 64u * j + lane;
+            valid[j] = k < T;
+            owner[j] = ((m - 1u) >> 8) / NS;
+            const uint32_t ent = k + W.delta[(m - 1u) & 0xFFu];
+            E[j] = G[valid[j] ? ent : 0u];
+        }
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            // the owner packet's fields
+            const uint32_t o = owner[j];
+            const uint32_t oks = bperm(ks, o), okd = bperm(kd, o);
+            const uint32_t opf = bperm(proto_fam, o), opt = bperm(f.ports, o);
+            const uint32_t osp = opt & 0xFFFFu, odp = opt >> 16;
+            const uint32_t pb = (1u << (16 + (osp >> kHybPortBlockShift))) | (1u << (24 + (odp >> kHybPortBlockShift)));
+            const uint32_t idx = E[j].z >> kEntIndexShift;
+            bool pass = valid[j] && hyb_pass(E[j], oks, okd, opf & 0xFFu, pb);
+            const bool cold = pass && (E[j].w & kHybCold);
+            if (ballot(cold)) {
+                // owner's IPv6 address words 1..3 (whole wave: bpermute reads every lane)
+                Fields of;
+                of.ports = opt;
+                of.is6 = (opf & 0x100u) != 0u;
+#pragma unroll
+                for (int q = 1; q < 4; ++q) {
+                    of.s[q] = bperm(f.s[q], o);
+                    of.t[q] = bperm(f.t[q], o);
+                }
+                if (cold) pass = hyb_cold_ok(a, of.is6, idx, of);
+            }
+            if (pass) atomicMin(&W.best[o], idx);
+        }
+        wave_lds_sync();
+    }
+    uint32_t best = W.best[lane];
+    // rules with no selective key: wave-uniform scan in rule order per family
+    const uint32_t pb = (1u << (16 + (sport >> kHybPortBlockShift))) | (1u << (24 + (dport >> kHybPortBlockShift)));
+#pragma unroll
+    for (int fam = 0; fam < 2; ++fam) {
+        const FamArgs &fa = fam ? a.f6 : a.f4;
+        const bool in_fam = fam ? f.is6 : f.is4;
+        for (uint32_t i = 0; i < fa.n_resid; ++i) {
+            const u32x4 E = G[(fa.off_resid >> 2) + i];
+            const uint32_t idx = E.z >> kEntIndexShift;
+            const bool want = in_fam && idx < best;
+            if (!ballot(want)) break;  // residual list ascends too
+            bool pass = want && hyb_pass(E, ks, kd, f.proto, pb);
+            const bool cold = pass && (E.w & kHybCold);
+            if (ballot(cold)) {
+                if (cold) pass = hyb_cold_ok(a, fam == 1, idx, f);
+            }
+            best = pass ? idx : best;
+        }
+    }
+    const bool hit = best != kNone;
+    uint32_t out = 0;
+    if (ballot(hit)) {
+        if (hit) out = a.tab[v6 ? a.f6.off_cold + best * kHybCold6Dwords + 2 : a.f4.off_cold + best * kHybCold4Dwords + 2];
+    }
+    return out;
+}
+
+template <int NS, int TM>
 __device__ __forceinline__ uint32_t classify_any(const IndexedArgs &a, const Fields &f) {
-    if (LDS) return classify_indexed<NS>(LdsTab{}, a, f);
+    if (TM == kTabFlat || TM == kTabFlat4) {
+        FlatScratch *W = reinterpret_cast<FlatScratch *>(lds_tab);
+        const uint32_t lane = lane_id();
+        return classify_flat<NS, TM == kTabFlat4 ? 4 : 2>(a, f, W[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)], lane);
+    }
+    if (TM == kTabLds) return classify_indexed<NS>(LdsTab{}, a, f);
+    if (TM == kTabHybrid) return classify_hybrid<NS, 1>(a, f);
+    if (TM == kTabHybrid2) return classify_hybrid<NS, 2>(a, f);
+    if (TM == kTabHybrid4) return classify_hybrid<NS, 4>(a, f);
     return classify_indexed<NS>(GlobalTab{a.tab}, a, f);
 }
 
@@ -482,11 +784,11 @@ __device__ __forceinline__ uint32_t classify_any(const IndexedArgs &a, const Fie
 //    classifying packet coal_packet(l) of its wave's batch; no register
 //    prefetch (it would push the kernel past 64 VGPRs, i.e. below 8 waves per
 //    SIMD) — 32 resident waves per CU keep 128 KiB of loads in flight.
-template <int NS, bool LDS, int MODE>
+template <int NS, int TM, int MODE>
 __global__ void __launch_bounds__(1024)
 k_indexed_slots(const uint8_t *__restrict__ slots, uint32_t stride, uint64_t n, IndexedArgs a,
                 uint32_t *__restrict__ port_out, uint64_t *__restrict__ permit_out) {
-    if (LDS) stage_table(a);
+    if (TM == kTabLds || TM == kTabHybrid || TM == kTabHybrid2 || TM == kTabHybrid4) stage_table(a);
     const uint32_t lane = lane_id();
     const uint32_t wpb = blockDim.x >> 6;
     const uint64_t wave0 = uint64_t(blockIdx.x) * wpb + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -539,7 +841,7 @@ k_indexed_slots(const uint8_t *__restrict__ slots, uint32_t stride, uint64_t n, 
         parse_fields(cur, live, f, [&](uint32_t k, uint32_t &lo, uint32_t &hi) {
             far_dwords(pkt, stride, k, lo, hi);
         }, a.flags & NFFACL_PARSE_VLAN);
-        const uint32_t res = classify_any<NS, LDS>(a, f);
+        const uint32_t res = classify_any<NS, TM>(a, f);
         if (live && port_out) port_out[idx] = res;
         if (permit_out) {
             // permit bit p belongs to packet p: fetch packet `lane`'s verdict from the lane holding it
@@ -553,25 +855,56 @@ k_indexed_slots(const uint8_t *__restrict__ slots, uint32_t stride, uint64_t n, 
     }
 }
 
-template <int NS, bool LDS>
+template <int NS, int TM>
 __global__ void __launch_bounds__(1024)
 k_indexed_frames(const uint8_t *__restrict__ frames, const uint64_t *__restrict__ desc, uint64_t n,
                  IndexedArgs a, uint32_t *__restrict__ port_out, uint64_t *__restrict__ permit_out) {
-    if (LDS) stage_table(a);
+    if (TM == kTabLds || TM == kTabHybrid || TM == kTabHybrid2 || TM == kTabHybrid4) stage_table(a);
+    // Software pipeline.  Always: the next batch's descriptors load while this
+    // batch is classified (the frame load depends on them).  PF (per-lane
+    // HYBRID walks, whose LDS directories hold the CU to 16 waves and so leave
+    // VGPRs to spare): also the next batch's 64-byte frame lines, and the
+    // descriptors of the batch after.
+    constexpr bool PF = TM == kTabHybrid2 || TM == kTabHybrid4;
+    uint64_t ds_n1 = 0;  // descriptor of this lane's packet in the next batch
+    uint64_t ds_n2 = 0;  // PF: ... in the batch after
+    uint32_t f_n1[16];   // PF: first 64 bytes of the next batch's packet
+    bool first = true;
     NFFACL_WAVE_LOOP(n) {
         const uint64_t idx = base + lane;
         const bool live = idx < n;
-        const uint64_t ds = live ? desc[idx] : 0;
+        const uint64_t S = nwaves * 64;
+        uint64_t ds;
+        uint32_t d[16];
+        if (first) {
+            ds = live ? desc[idx] : 0;
+            load16(frames + (ds >> 16), d);
+            ds_n1 = idx + S < n ? desc[idx + S] : 0;
+            if (PF) {
+                if (base + S < n) load16(frames + (ds_n1 >> 16), f_n1);
+                ds_n2 = idx + 2 * S < n ? desc[idx + 2 * S] : 0;
+            }
+        } else if (PF) {
+            ds = ds_n1;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) d[k] = f_n1[k];
+            ds_n1 = ds_n2;
+            if (base + S < n) load16(frames + (ds_n1 >> 16), f_n1);
+            ds_n2 = idx + 2 * S < n ? desc[idx + 2 * S] : 0;
+        } else {
+            ds = ds_n1;
+            load16(frames + (ds >> 16), d);
+            ds_n1 = idx + S < n ? desc[idx + S] : 0;
+        }
+        first = false;
         const uint32_t len = static_cast<uint32_t>(ds & 0xFFFFu);
         const uint8_t *pkt = frames + (ds >> 16);
-        uint32_t d[16];
-        load16(pkt, d);
         clip16(d, len);
         Fields f;
         parse_fields(d, live, f, [&](uint32_t k, uint32_t &lo, uint32_t &hi) {
             far_dwords(pkt, len, k, lo, hi);
         }, a.flags & NFFACL_PARSE_VLAN);
-        const uint32_t res = classify_any<NS, LDS>(a, f);
+        const uint32_t res = classify_any<NS, TM>(a, f);
         store_verdicts(base, lane, live, res, port_out, permit_out);
     }
 }
@@ -623,17 +956,19 @@ static uint32_t grid_for(const nffacl_engine *eng, uint64_t n, uint32_t block, u
 static dev::IndexedArgs indexed_args(const DevTable *t) {
     dev::IndexedArgs a{};
     a.tab = t->d_blob;
-    a.tab_dwords = static_cast<uint32_t>(t->meta.blob.size());
-    auto fam = [&](const FamilyIndex &fi, dev::FamArgs &fa) {
+    const bool hyb = t->meta.algo == NFFACL_ALGO_HYBRID;
+    a.stage_dwords = hyb ? t->meta.lds_dwords : static_cast<uint32_t>(t->meta.blob.size());
+    auto fam = [&](const FamilyIndex &fi, uint32_t off_cold, dev::FamArgs &fa) {
         for (uint32_t k = 0; k < 4; ++k) {
             const DimInfo &d = fi.dims[k];
             fa.slot[k] = dev::SlotArgs{d.shift, d.off_dir, d.off_ent, 0};
         }
         fa.off_resid = fi.off_resid;
         fa.n_resid = fi.n_resid;
+        fa.off_cold = off_cold;
     };
-    fam(t->meta.idx4, a.f4);
-    fam(t->meta.idx6, a.f6);
+    fam(t->meta.idx4, t->meta.off_rec4, a.f4);
+    fam(t->meta.idx6, t->meta.off_rec6, a.f6);
     return a;
 }
 
@@ -641,7 +976,7 @@ static dev::IndexedArgs indexed_args(const DevTable *t) {
 constexpr size_t kLdsBytes = 160 * 1024;
 
 struct IndexedLaunch {
-    bool lds;
+    int tm;  // dev::TableMode
     int ns;
     uint32_t block, per_cu;
     size_t lds_bytes;
@@ -654,14 +989,35 @@ static int tune_env(const char *name, int dflt) {
 }
 
 static IndexedLaunch indexed_launch(const DevTable *t) {
-    const size_t bytes = t->meta.blob.size() * sizeof(uint32_t);
-    const int ns = (t->meta.idx4.port_dims || t->meta.idx6.port_dims) ? 4 : 2;
-    const bool lds = bytes <= kLdsBytes - 1024 && tune_env("NFFACL_TUNE_LDS", 1) != 0;
-    IndexedLaunch L{lds, ns, 256u, 8u, 0};
-    if (lds) {
+    const uint32_t used = std::max(t->meta.idx4.used_slots, t->meta.idx6.used_slots);
+    const int ns = used <= 2 ? 2 : static_cast<int>(used);
+    IndexedLaunch L{dev::kTabGlobal, ns, 256u, 8u, 0};
+    size_t staged = 0;
+    // HYBRID: directories staged in LDS and walked per lane, or (directories
+    // too large for LDS, or forced) read from global memory, candidates flat.
+    const bool hyb_flat = t->meta.lds_dwords == 0 || tune_env("NFFACL_TUNE_FLAT", 0) != 0;
+    if (t->meta.algo == NFFACL_ALGO_HYBRID && hyb_flat) {
+        L.tm = tune_env("NFFACL_TUNE_ROUNDS", 4) == 2 ? dev::kTabFlat : dev::kTabFlat4;
+        L.block = static_cast<uint32_t>(tune_env("NFFACL_TUNE_BLOCK", 256));
+        L.per_cu = static_cast<uint32_t>(tune_env("NFFACL_TUNE_PER_CU", 8));
+        L.lds_bytes = sizeof(dev::FlatScratch) * (L.block / 64);
+        return L;
+    }
+    if (t->meta.algo == NFFACL_ALGO_HYBRID) {
+        const int u = tune_env("NFFACL_TUNE_UNROLL", 2);
+        L.tm = u == 1 ? dev::kTabHybrid : u == 4 ? dev::kTabHybrid4 : dev::kTabHybrid2;
+        staged = size_t(t->meta.lds_dwords) * sizeof(uint32_t);
+    } else {
+        const size_t bytes = t->meta.blob.size() * sizeof(uint32_t);
+        if (bytes <= kLdsTableBytes && tune_env("NFFACL_TUNE_LDS", 1) != 0) {
+            L.tm = dev::kTabLds;
+            staged = bytes;
+        }
+    }
+    if (L.tm != dev::kTabGlobal) {
         L.block = 1024u;
-        L.per_cu = static_cast<uint32_t>(std::min<size_t>(2, kLdsBytes / bytes));
-        L.lds_bytes = bytes;
+        L.per_cu = static_cast<uint32_t>(std::max<size_t>(1, std::min<size_t>(2, kLdsBytes / std::max<size_t>(staged, 16))));
+        L.lds_bytes = std::max<size_t>(staged, 16);
     }
     L.block = static_cast<uint32_t>(tune_env("NFFACL_TUNE_BLOCK", static_cast<int>(L.block)));
     L.per_cu = static_cast<uint32_t>(tune_env("NFFACL_TUNE_PER_CU", static_cast<int>(L.per_cu)));
@@ -674,18 +1030,54 @@ static hipError_t allow_lds(K kernel) {
                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kLdsBytes));
 }
 
+// Load modes (64-byte slots): 0 one row per lane (+ next-batch register
+// prefetch; any stride); 1 lane-contiguous + quad DPP transpose; 2 = 1 with
+// non-temporal loads; 3 = 2 + register prefetch; 4 lane-contiguous
+// non-temporal + permlane row-swap transpose (default).  Interleaved A/B in
+// one process (profiles/r1_ab/): mode 4 0.2195 ms, 2 0.2203, 0 0.2475 (C2).
+// Modes 1-3 are built for the LDS-staged table only (the A/B experiments).
+template <int NS, int TM>
+static hipError_t allow_lds_modes() {
+    hipError_t e = allow_lds(dev::k_indexed_slots<NS, TM, 0>);
+    if (e == hipSuccess) e = allow_lds(dev::k_indexed_slots<NS, TM, 4>);
+    if (TM == dev::kTabLds) {
+        if (e == hipSuccess) e = allow_lds(dev::k_indexed_slots<NS, dev::kTabLds, 1>);
+        if (e == hipSuccess) e = allow_lds(dev::k_indexed_slots<NS, dev::kTabLds, 2>);
+        if (e == hipSuccess) e = allow_lds(dev::k_indexed_slots<NS, dev::kTabLds, 3>);
+    }
+    if (e == hipSuccess) e = allow_lds(dev::k_indexed_frames<NS, TM>);
+    return e;
+}
+
+// Calls f(integral_constant<NS>, integral_constant<TM>) for the runtime pair.
+template <class F>
+static void dispatch_indexed(int ns, int tm, F &&f) {
+    auto with_ns = [&](auto nsc) {
+        switch (tm) {
+        case dev::kTabLds: f(nsc, std::integral_constant<int, dev::kTabLds>{}); break;
+        case dev::kTabHybrid: f(nsc, std::integral_constant<int, dev::kTabHybrid>{}); break;
+        case dev::kTabHybrid2: f(nsc, std::integral_constant<int, dev::kTabHybrid2>{}); break;
+        case dev::kTabHybrid4: f(nsc, std::integral_constant<int, dev::kTabHybrid4>{}); break;
+        case dev::kTabFlat: f(nsc, std::integral_constant<int, dev::kTabFlat>{}); break;
+        case dev::kTabFlat4: f(nsc, std::integral_constant<int, dev::kTabFlat4>{}); break;
+        default: f(nsc, std::integral_constant<int, dev::kTabGlobal>{}); break;
+        }
+    };
+    if (ns == 2) with_ns(std::integral_constant<int, 2>{});
+    else if (ns == 3) with_ns(std::integral_constant<int, 3>{});
+    else with_ns(std::integral_constant<int, 4>{});
+}
+
 int prepare_kernels() {
     static std::once_flag once;
     static hipError_t err = hipSuccess;
     std::call_once(once, [] {
-        const hipError_t e[12] = {allow_lds(dev::k_indexed_slots<2, true, 4>), allow_lds(dev::k_indexed_slots<4, true, 4>),
-                                 allow_lds(dev::k_indexed_slots<2, true, 0>), allow_lds(dev::k_indexed_slots<4, true, 0>),
-                                 allow_lds(dev::k_indexed_slots<2, true, 1>), allow_lds(dev::k_indexed_slots<4, true, 1>),
-                                 allow_lds(dev::k_indexed_slots<2, true, 2>), allow_lds(dev::k_indexed_slots<4, true, 2>),
-                                 allow_lds(dev::k_indexed_slots<2, true, 3>), allow_lds(dev::k_indexed_slots<4, true, 3>),
-                                 allow_lds(dev::k_indexed_frames<2, true>), allow_lds(dev::k_indexed_frames<4, true>)};
-        for (hipError_t x : e)
-            if (x != hipSuccess) err = x;
+        for (int ns = 2; ns <= 4; ++ns)
+            for (int tm : {int(dev::kTabLds), int(dev::kTabHybrid), int(dev::kTabHybrid2), int(dev::kTabHybrid4)})
+                dispatch_indexed(ns, tm, [&](auto nsc, auto tmc) {
+                    const hipError_t e = allow_lds_modes<decltype(nsc)::value, decltype(tmc)::value>();
+                    if (e != hipSuccess) err = e;
+                });
     });
     if (err != hipSuccess) {
         set_last_error(std::string("hipFuncSetAttribute(LDS): ") + hipGetErrorString(err));
@@ -694,33 +1086,53 @@ int prepare_kernels() {
     return NFFACL_OK;
 }
 
+template <int NS, int TM>
+static void launch_slots_tm(int mode, const IndexedLaunch &L, uint32_t grid, hipStream_t stream,
+                            const uint8_t *d_slots, uint32_t stride, uint64_t n, const dev::IndexedArgs &a,
+                            uint32_t *d_port, uint64_t *d_permit) {
+    const dim3 g(grid), b(L.block);
+    const size_t lds = TM == dev::kTabGlobal ? 0 : L.lds_bytes;
+    if (TM == dev::kTabFlat || TM == dev::kTabFlat4) {  // built with load modes 0 and 4 only
+        if (mode == 0)
+            hipLaunchKernelGGL((dev::k_indexed_slots<NS, TM, 0>), g, b, lds, stream, d_slots, stride, n, a, d_port, d_permit);
+        else
+            hipLaunchKernelGGL((dev::k_indexed_slots<NS, TM, 4>), g, b, lds, stream, d_slots, stride, n, a, d_port, d_permit);
+    } else if (TM == dev::kTabLds && mode >= 1 && mode <= 3) {
+        if (mode == 1)
+            hipLaunchKernelGGL((dev::k_indexed_slots<NS, dev::kTabLds, 1>), g, b, lds, stream, d_slots, stride, n, a, d_port, d_permit);
+        else if (mode == 2)
+            hipLaunchKernelGGL((dev::k_indexed_slots<NS, dev::kTabLds, 2>), g, b, lds, stream, d_slots, stride, n, a, d_port, d_permit);
+        else
+            hipLaunchKernelGGL((dev::k_indexed_slots<NS, dev::kTabLds, 3>), g, b, lds, stream, d_slots, stride, n, a, d_port, d_permit);
+    } else if (mode == 0) {
+        hipLaunchKernelGGL((dev::k_indexed_slots<NS, TM, 0>), g, b, lds, stream, d_slots, stride, n, a, d_port, d_permit);
+    } else {
+        hipLaunchKernelGGL((dev::k_indexed_slots<NS, TM, 4>), g, b, lds, stream, d_slots, stride, n, a, d_port, d_permit);
+    }
+}
+
+template <int NS, int TM>
+static void launch_frames_tm(const IndexedLaunch &L, uint32_t grid, hipStream_t stream, const uint8_t *d_frames,
+                             const uint64_t *d_desc, uint64_t n, const dev::IndexedArgs &a, uint32_t *d_port,
+                             uint64_t *d_permit) {
+    const size_t lds = TM == dev::kTabGlobal ? 0 : L.lds_bytes;
+    hipLaunchKernelGGL((dev::k_indexed_frames<NS, TM>), dim3(grid), dim3(L.block), lds, stream, d_frames, d_desc, n,
+                       a, d_port, d_permit);
+}
+
 int launch_slots(nffacl_engine *eng, const DevTable *t, const uint8_t *d_slots, uint32_t stride,
                  uint64_t n, uint32_t *d_port, uint64_t *d_permit, hipStream_t stream, uint32_t flags) {
     if (n == 0) return NFFACL_OK;
-    if (t->meta.algo == NFFACL_ALGO_INDEXED) {
+    if (t->meta.algo != NFFACL_ALGO_LINEAR) {
         dev::IndexedArgs a = indexed_args(t);
         a.flags = flags;
         const IndexedLaunch L = indexed_launch(t);
         const uint32_t grid = grid_for(eng, n, L.block, L.per_cu);
-        const dim3 g(grid), b(L.block);
-        // load mode (64-byte slots): 0 one row per lane; 1 lane-contiguous +
-        // quad DPP transpose; 2 = 1 with non-temporal loads; 3 = 2 + register
-        // prefetch; 4 lane-contiguous non-temporal + permlane row-swap
-        // transpose (default).  Interleaved A/B in one process
-        // (profiles/r1_ab/): mode 4 0.2195 ms, 2 0.2203, 0 0.2475 (C2).
         const int mode = stride == 64 ? std::min(4, std::max(0, tune_env("NFFACL_TUNE_COAL", 4))) : 0;
-#define NFFACL_SLOTS(NS_, LDS_, M_) \
-    hipLaunchKernelGGL((dev::k_indexed_slots<NS_, LDS_, M_>), g, b, LDS_ ? L.lds_bytes : 0, stream, d_slots, stride, n, a, d_port, d_permit)
-#define NFFACL_SLOTS_M(NS_, LDS_) \
-    do { if (mode == 4) NFFACL_SLOTS(NS_, LDS_, 4); else if (mode == 3) NFFACL_SLOTS(NS_, LDS_, 3); \
-         else if (mode == 2) NFFACL_SLOTS(NS_, LDS_, 2); \
-         else if (mode == 1) NFFACL_SLOTS(NS_, LDS_, 1); else NFFACL_SLOTS(NS_, LDS_, 0); } while (0)
-        if (L.lds && L.ns == 2) NFFACL_SLOTS_M(2, true);
-        else if (L.lds) NFFACL_SLOTS_M(4, true);
-        else if (L.ns == 2) NFFACL_SLOTS_M(2, false);
-        else NFFACL_SLOTS_M(4, false);
-#undef NFFACL_SLOTS_M
-#undef NFFACL_SLOTS
+        dispatch_indexed(L.ns, L.tm, [&](auto nsc, auto tmc) {
+            launch_slots_tm<decltype(nsc)::value, decltype(tmc)::value>(mode, L, grid, stream, d_slots, stride, n, a,
+                                                                      d_port, d_permit);
+        });
     } else {
         const uint32_t block = 256;
         dev::LinearArgs a{t->d_blob + t->meta.off_rec4, t->meta.n4, t->d_blob + t->meta.off_rec6,
@@ -737,20 +1149,15 @@ int launch_frames(nffacl_engine *eng, const DevTable *t, const uint8_t *d_frames
                   const uint64_t *d_desc, uint64_t n, uint32_t *d_port, uint64_t *d_permit,
                   hipStream_t stream, uint32_t flags) {
     if (n == 0) return NFFACL_OK;
-    if (t->meta.algo == NFFACL_ALGO_INDEXED) {
+    if (t->meta.algo != NFFACL_ALGO_LINEAR) {
         dev::IndexedArgs a = indexed_args(t);
         a.flags = flags;
         const IndexedLaunch L = indexed_launch(t);
         const uint32_t grid = grid_for(eng, n, L.block, L.per_cu);
-        const dim3 g(grid), b(L.block);
-        if (L.lds && L.ns == 2)
-            hipLaunchKernelGGL((dev::k_indexed_frames<2, true>), g, b, L.lds_bytes, stream, d_frames, d_desc, n, a, d_port, d_permit);
-        else if (L.lds)
-            hipLaunchKernelGGL((dev::k_indexed_frames<4, true>), g, b, L.lds_bytes, stream, d_frames, d_desc, n, a, d_port, d_permit);
-        else if (L.ns == 2)
-            hipLaunchKernelGGL((dev::k_indexed_frames<2, false>), g, b, 0, stream, d_frames, d_desc, n, a, d_port, d_permit);
-        else
-            hipLaunchKernelGGL((dev::k_indexed_frames<4, false>), g, b, 0, stream, d_frames, d_desc, n, a, d_port, d_permit);
+        dispatch_indexed(L.ns, L.tm, [&](auto nsc, auto tmc) {
+            launch_frames_tm<decltype(nsc)::value, decltype(tmc)::value>(L, grid, stream, d_frames, d_desc, n, a,
+                                                                       d_port, d_permit);
+        });
     } else {
         const uint32_t block = 256;
         dev::LinearArgs a{t->d_blob + t->meta.off_rec4, t->meta.n4, t->d_blob + t->meta.off_rec6,

@@ -62,6 +62,47 @@ constexpr uint32_t kEntIndexShift = 9;
 constexpr uint32_t kEntExact = 1u << 8;
 constexpr uint32_t kMaxIndexedRules = 1u << 23;
 
+// ---- hybrid table (tables whose inline index outgrows LDS) ---------------
+//
+// Same slot assignment and ascending bucket lists as the indexed table, but
+//  * the eight directories (both families) come first in the blob; their
+//    values are absolute entry numbers (16-byte units of the blob).  Either
+//    they are the only part staged in LDS (radix widths chosen to fit
+//    kHybLaneDirBytes; each lane walks its lists), or — when that leaves more
+//    than kHybFlatCandidates expected candidates per packet — they are sized
+//    to kHybFlatDirBytes and read from global memory, and a wave tests its
+//    packets' candidates 64 at a time (lds_dwords = 0 marks this form);
+//  * a list entry is 16 bytes, everything the common test needs:
+//      [0] src word, big-endian value (IPv6: top 32 bits)
+//      [1] dst word, big-endian value
+//      [2] meta = id | exact << 8 | rule_index << 9          (as inline)
+//      [3] src_len | dst_len << 6 | cold << 12 | sport_blocks << 16 | dport_blocks << 24
+//    with prefix lengths (IPv6: capped at 32) and 8-bit port-block bitmaps
+//    (bit b: the rule's range meets ports [8192 b, 8192 b + 8191]);
+//  * cold records, one per rule in rule order, hold what the entry cannot:
+//      IPv4 (4 dwords): lo, hi, output_number, 0
+//      IPv6 (16 dwords): lo, hi, output_number, 0, then the 12 extension words
+//      of the inline entry (src[1..3], src_mask[1..3], dst[1..3], dst_mask[1..3]).
+//    An entry with the cold bit (port ranges not made of whole blocks, IPv6
+//    prefixes longer than 32) is confirmed against its cold record; the
+//    winner's output number is read from its cold record at the end.
+// Only CIDR masks and id_mask in {0, 0xff} are encodable (what the parsers
+// produce); other rule sets compile INDEXED.
+constexpr uint32_t kHybEntDwords = 4;
+constexpr uint32_t kHybCold = 1u << 12;
+constexpr uint32_t kHybPortBlockShift = 13;
+constexpr uint32_t kHybPortBlockMask = (1u << kHybPortBlockShift) - 1u;
+constexpr uint32_t kHybCold4Dwords = 4;
+constexpr uint32_t kHybCold6Dwords = 16;
+// Directory budgets (both families), see above.  128 KiB of LDS directories
+// leave one 1024-thread workgroup per CU; measured faster than 64 KiB with
+// two (C3: 0.64 vs 0.69 ms, profiles/r1_hybrid/).
+constexpr size_t kHybLaneDirBytes = 128 * 1024;
+constexpr size_t kHybFlatDirBytes = 1024 * 1024;
+constexpr double kHybFlatCandidates = 6.0;
+// Largest table staged whole in LDS (gfx950: 160 KiB per CU, 1 KiB headroom).
+constexpr size_t kLdsTableBytes = 159 * 1024;
+
 enum KeyKind : uint32_t {
     kKeySrc4 = 0,   // IPv4 source address (host-order value of the wire bytes)
     kKeyDst4 = 1,   // IPv4 destination address

@@ -54,7 +54,7 @@ ERR_HIP = -102
 ERR_NO_DEVICE = -103
 ERR_UNSUPPORTED = -104
 
-ALGO_AUTO, ALGO_LINEAR, ALGO_INDEXED = 0, 1, 2
+ALGO_AUTO, ALGO_LINEAR, ALGO_INDEXED, ALGO_HYBRID = 0, 1, 2, 3
 PARSE_VLAN = 1  # ParseAllKnownL3CheckVLAN (packet/vlan.go:104-117) instead of ParseAllKnownL3
 
 # ---- record layouts ------------------------------------------------------------

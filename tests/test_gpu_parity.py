@@ -15,7 +15,7 @@ from oracle import oracle, rules_oracle as ro
 
 pytestmark = pytest.mark.gpu
 
-ALGOS = [nffacl.ALGO_LINEAR, nffacl.ALGO_INDEXED]
+ALGOS = [nffacl.ALGO_LINEAR, nffacl.ALGO_INDEXED, nffacl.ALGO_HYBRID]
 THREADS = 16
 
 
@@ -348,9 +348,66 @@ def test_full_size_c2_properties(torch_cuda):
             assert torch.equal(port, half)
             outs[algo] = port
     assert torch.equal(outs[nffacl.ALGO_LINEAR], outs[nffacl.ALGO_INDEXED])
+    assert torch.equal(outs[nffacl.ALGO_LINEAR], outs[nffacl.ALGO_HYBRID])
     rng = np.random.default_rng(5)
     idx = np.sort(rng.choice(n, 1 << 16, replace=False))
     sample = d_slots.view(n, 64)[torch.from_numpy(idx).to("cuda")].cpu().numpy().reshape(-1)
     want = oracle.classify_slots(sample, 64, len(idx), a4, a6, threads=THREADS)
     got = outs[nffacl.ALGO_LINEAR].cpu().numpy().view(np.uint32)[idx]
     np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.parametrize("flat", [0, 1])
+def test_full_size_c5_hybrid(torch_cuda, monkeypatch, flat):
+    """C5 (100k rules with port ranges) at 2^22 packets: HYBRID (AUTO's choice)
+    == INDEXED read from global memory on every packet, and a 2^14 random
+    sample equals the oracle."""
+    torch = torch_cuda
+    monkeypatch.setenv("NFFACL_TUNE_FLAT", str(flat))
+    g = synth.gen_rules(synth.SPECS["c5"], synth.RULE_SEEDS["c5"])
+    rules, (a4, a6) = _rules_and_arrays(g.text)
+    n = 1 << 22
+    slots = synth.gen_slots(g, n, synth.PACKET_SEEDS["c5"])
+    d_slots = to_dev(torch, slots)
+    del slots
+    outs = {}
+    for algo in (nffacl.ALGO_AUTO, nffacl.ALGO_INDEXED):
+        with nffacl.Engine(rules, algo=algo) as eng:
+            assert eng.algo == (nffacl.ALGO_HYBRID if algo == nffacl.ALGO_AUTO else nffacl.ALGO_INDEXED)
+            port = torch.zeros(n, dtype=torch.int32, device="cuda")
+            eng.classify_device(d_slots, 64, n, port)
+            torch.cuda.synchronize()
+            outs[algo] = port
+    assert torch.equal(outs[nffacl.ALGO_AUTO], outs[nffacl.ALGO_INDEXED])
+    rng = np.random.default_rng(7)
+    idx = np.sort(rng.choice(n, 1 << 14, replace=False))
+    sample = d_slots.view(n, 64)[torch.from_numpy(idx).to("cuda")].cpu().numpy().reshape(-1)
+    want = oracle.classify_slots(sample, 64, len(idx), a4, a6, threads=THREADS)
+    np.testing.assert_array_equal(outs[nffacl.ALGO_AUTO].cpu().numpy().view(np.uint32)[idx], want)
+
+
+@pytest.mark.parametrize("flat", [0, 1])
+@pytest.mark.parametrize("dir_kb", [1, 16, 1024])
+def test_hybrid_directory_budgets(torch_cuda, monkeypatch, dir_kb, flat):
+    """Narrow directories (long candidate lists) and wide ones stay exact,
+    walked per lane or flattened per wave: C3-style rules on slots and on
+    IMIX frames."""
+    torch = torch_cuda
+    monkeypatch.setenv("NFFACL_TUNE_DIR_KB", str(dir_kb))
+    monkeypatch.setenv("NFFACL_TUNE_FLAT", str(flat))
+    g = synth.gen_rules(synth.SPECS["c3"], synth.RULE_SEEDS["c3"])
+    rules, (a4, a6) = _rules_and_arrays(g.text)
+    n = (1 << 15) + 5
+    slots = synth.gen_slots(g, n, 21)
+    with nffacl.Engine(rules, algo=nffacl.ALGO_HYBRID) as eng:
+        assert eng.algo == nffacl.ALGO_HYBRID
+        p, b = classify(torch, eng, slots, 64, n)
+        want = oracle.classify_slots(slots, 64, n, a4, a6, threads=THREADS)
+        np.testing.assert_array_equal(p, want)
+        np.testing.assert_array_equal(b, permit_bits(want))
+        frames, desc = synth.gen_imix(g, 1 << 14, 22)
+        port = torch.zeros(1 << 14, dtype=torch.int32, device="cuda")
+        eng.classify_frames_device(to_dev(torch, frames), to_dev(torch, desc.view(np.int64)), 1 << 14, port)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(port.cpu().numpy().view(np.uint32),
+                                      oracle.classify_frames(frames, desc, a4, a6, threads=THREADS))

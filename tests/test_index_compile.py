@@ -27,7 +27,7 @@ class FamInfo(ctypes.Structure):
 
 
 class TableInfo(ctypes.Structure):
-    _fields_ = [("algo", ctypes.c_int32), ("reserved", ctypes.c_uint32), ("blob_dwords", ctypes.c_uint64),
+    _fields_ = [("algo", ctypes.c_int32), ("lds_dwords", ctypes.c_uint32), ("blob_dwords", ctypes.c_uint64),
                 ("fam", FamInfo * 2)]
 
 
@@ -200,3 +200,159 @@ def test_non_indexable_rules_compile_linear():
     r["id_mask"] = 0x0F
     _, info = compile_table(nffacl.L3Rules.from_arrays(r), nffacl.ALGO_INDEXED)
     assert info.algo == nffacl.ALGO_LINEAR
+
+
+# ---- HYBRID (table.hpp "hybrid table") --------------------------------------
+
+def pmask(L):
+    """Top-L-bits mask of a big-endian word, L in 0..32."""
+    L = L.astype(np.uint64)
+    return ((np.uint64(0xFFFFFFFF00000000) >> L) & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+
+
+def hyb_test(blob, info, offs, v6, F, sel):
+    """Common test of the compact entries at dword offsets offs[i] against
+    packet sel[i], confirmed on the cold record where the cold bit is set;
+    returns (ok, rule index)."""
+    e = blob[offs[:, None] + np.arange(4)[None, :]]
+    ks, kd = bswap(F["s"][0][sel]), bswap(F["t"][0][sel])
+    w = e[:, 3]
+    m = ((ks ^ e[:, 0]) & pmask(w & 63)) | ((kd ^ e[:, 1]) & pmask((w >> 6) & 63))
+    meta = e[:, 2]
+    m |= np.where((meta >> 8) & 1 == 1, (F["proto"][sel] ^ meta) & 0xFF, 0)
+    sp, dp = F["sp"][sel].astype(np.uint32), F["dp"][sel].astype(np.uint32)
+    pb = (np.uint32(1) << (16 + (sp >> 13))) | (np.uint32(1) << (24 + (dp >> 13)))
+    q = w & pb
+    ok = (m == 0) & ((q & 0x00FF0000) != 0) & ((q & 0xFF000000) != 0)
+    idx = (meta >> 9).astype(np.uint64)
+    cold = ok & ((w >> 12) & 1 == 1)
+    if cold.any():
+        c = np.nonzero(cold)[0]
+        cw = 16 if v6 else 4
+        off = info.fam[int(v6)].off_rec + idx[c].astype(np.int64) * cw
+        C = blob[off[:, None] + np.arange(cw)[None, :]]
+        lo, hi = C[:, 0], C[:, 1]
+        s2, d2 = sp[c], dp[c]
+        okc = (s2 >= (lo & 0xFFFF)) & (s2 <= (hi & 0xFFFF)) & (d2 >= (lo >> 16)) & (d2 <= (hi >> 16))
+        if v6:  # s1 s2 s3 sm1 sm2 sm3 t1 t2 t3 tm1 tm2 tm3
+            sc = sel[c]
+            x = np.zeros(len(c), np.uint32)
+            for k in range(3):
+                x |= (F["s"][k + 1][sc] ^ C[:, 4 + k]) & C[:, 7 + k]
+                x |= (F["t"][k + 1][sc] ^ C[:, 10 + k]) & C[:, 13 + k]
+            okc &= x == 0
+        ok[c] = okc
+    return ok, idx
+
+
+def emulate_hybrid(blob, info, F, n):
+    best = np.full(n, 0xFFFFFFFF, np.uint64)
+    for fam, v6 in ((0, False), (1, True)):
+        fi = info.fam[fam]
+        mine = F["is6"] if v6 else F["is4"]
+        for d in range(4):
+            di = fi.dims[d]
+            if di.n_rules == 0:
+                continue
+            key = KEYS[di.kind](F).astype(np.uint64)
+            dirv = blob[di.off_dir:di.off_dir + di.n_buckets + 1].astype(np.int64)
+            assert info.lds_dwords == 0 or di.off_dir + di.n_buckets + 1 <= info.lds_dwords
+            t = (key >> np.uint64(di.shift)).astype(np.int64)
+            start, end = dirv[t], dirv[t + 1]
+            for k in range(di.max_list):
+                live = mine & (start < end)
+                if not live.any():
+                    break
+                sel = np.nonzero(live)[0]
+                ok, idx = hyb_test(blob, info, start[sel] * 4, v6, F, sel)
+                keep = idx < best[sel]
+                ok &= keep
+                best[sel[ok]] = idx[ok]
+                stop = ok | ~keep
+                start[sel] += 1
+                start[sel[stop]] = end[sel[stop]]
+        for i in range(fi.n_resid):
+            sel = np.nonzero(mine)[0]
+            ok, idx = hyb_test(blob, info, np.full(len(sel), fi.off_resid + 4 * i), v6, F, sel)
+            ok &= idx < best[sel]
+            best[sel[ok]] = idx[ok]
+    out = np.zeros(n, np.uint32)
+    for fam, v6 in ((0, False), (1, True)):
+        mine = (F["is6"] if v6 else F["is4"]) & (best != 0xFFFFFFFF)
+        cw = 16 if v6 else 4
+        out[mine] = blob[info.fam[fam].off_rec + best[mine].astype(np.int64) * cw + 2]
+    return best, out
+
+
+def check_hybrid(text: str, slots: np.ndarray, n: int, dir_kb=None, monkeypatch=None):
+    rules = nffacl.L3Rules.parse_text(text)
+    if dir_kb is not None:
+        monkeypatch.setenv("NFFACL_TUNE_DIR_KB", str(dir_kb))
+    blob, info = compile_table(rules, nffacl.ALGO_HYBRID)
+    assert info.algo == nffacl.ALGO_HYBRID
+    a4, a6 = ro.parse_text_table(text.encode()).arrays()
+    want, _ = oracle.classify_slots_which(slots, 64, n, a4, a6)
+    F = fields(slots, n)
+    best, out = emulate_hybrid(blob, info, F, n)
+    sel = ~F["skip"]
+    got = np.where(best != 0xFFFFFFFF, out, 0)
+    np.testing.assert_array_equal(got[sel], want[sel])
+    return info
+
+
+@pytest.mark.parametrize("cfg", ["c2", "c3"])
+def test_hybrid_matches_oracle_synthetic(cfg):
+    g = synth.gen_rules(synth.SPECS[cfg], synth.RULE_SEEDS[cfg])
+    n = 1 << 15
+    info = check_hybrid(g.text, synth.gen_slots(g, n, synth.PACKET_SEEDS[cfg]), n)
+    assert 0 < info.lds_dwords * 4 <= 128 * 1024  # LDS directories, per-lane walks
+
+
+def test_hybrid_small_directory_budget(monkeypatch):
+    """A 4 KiB directory budget forces long lists; still the first match."""
+    g = synth.gen_rules(synth.SPECS["c3"], synth.RULE_SEEDS["c3"])
+    n = 1 << 13
+    info = check_hybrid(g.text, synth.gen_slots(g, n, 11), n, dir_kb=4, monkeypatch=monkeypatch)
+    assert info.lds_dwords * 4 <= 4 * 1024 + 64
+
+
+def test_hybrid_firewall_and_nested(golden):
+    text = (golden / "rules" / "firewall.conf").read_text()
+    n = 1 << 13
+    check_hybrid(text, synth.gen_slots(synth.firewall_rules(text), n, 5), n)
+    lines = []
+    rng = np.random.default_rng(10)
+    for i in range(400):
+        plen = int(rng.integers(0, 33))
+        a = int(rng.integers(0, 1 << 32)) & (0xFFFFFFFF << (32 - plen) if plen else 0) & 0xFFFFFFFF
+        src = f"{a >> 24}.{a >> 16 & 255}.{a >> 8 & 255}.{a & 255}/{plen}" if i % 5 else "ANY"
+        dst = "ANY" if i % 3 else f"10.{i % 256}.0.0/16"
+        proto = ["ANY", "TCP", "UDP", "ICMP"][i % 4]
+        lo = int(rng.integers(0, 60000))
+        sp = "ANY" if i % 2 or proto == "ICMP" else f"{lo & ~8191}:{(lo & ~8191) + 8191}"  # whole blocks
+        dp = "ANY" if i % 4 == 0 or proto == "ICMP" else f"{lo}:{lo + int(rng.integers(0, 5000))}"
+        lines.append(f"{src} {dst} {proto} {sp} {dp} {i % 7}")
+        if i % 50 == 0:
+            lines.append(f"ANY 2001:db8:{i:x}::/{48 + i % 80} TCP ANY {lo} {i}")
+    lines.append("ANY ANY UDP ANY ANY 9")
+    text = "\n".join(lines) + "\n"
+    check_hybrid(text, synth.gen_slots(synth.firewall_rules(text), n, 6), n)
+
+
+def test_hybrid_falls_back_on_non_cidr_masks():
+    r = np.zeros(1, nffacl.RULE4)
+    r["src_mask"] = 0x00FF00FF  # not a prefix
+    r["output_number"] = 1
+    _, info = compile_table(nffacl.L3Rules.from_arrays(r), nffacl.ALGO_HYBRID)
+    assert info.algo == nffacl.ALGO_INDEXED
+
+
+def test_hybrid_policy_c5_flat():
+    """C5 (100k rules): LDS-sized directories would leave long lists, so the
+    compiler picks wide global directories (the wave-flattened form,
+    lds_dwords == 0); the structure still gives the oracle's first match."""
+    g = synth.gen_rules(synth.SPECS["c5"], synth.RULE_SEEDS["c5"])
+    n = 1 << 12
+    info = check_hybrid(g.text, synth.gen_slots(g, n, synth.PACKET_SEEDS["c5"]), n)
+    assert info.lds_dwords == 0
+    assert info.fam[0].dims[3].n_rules == 0  # sparse source-port slot folded away

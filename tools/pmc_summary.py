@@ -10,7 +10,7 @@ from pathlib import Path
 d = Path(sys.argv[1])
 key = sys.argv[2] if len(sys.argv) > 2 and not sys.argv[2].startswith("--") else "k_indexed_slots"
 out = {}
-for sub in ("fetch", "write", "sq", "sq2"):
+for sub in ("fetch", "write", "sq", "sq2", "tcc"):
     f = d / sub / "run_counter_collection.csv"
     if not f.exists():
         continue
@@ -30,6 +30,8 @@ if f.exists():
 res = {"kernel": key, "trace": stats, "counters_mean_per_dispatch": out}
 if "FETCH_SIZE" in out and "WRITE_SIZE" in out:
     res["hbm_bytes_per_launch"] = (2 * out["FETCH_SIZE"] + out["WRITE_SIZE"]) * 1024
+if out.get("TCC_HIT_sum") is not None and out.get("TCC_MISS_sum") is not None:
+    res["l2_hit_rate"] = out["TCC_HIT_sum"] / max(1.0, out["TCC_HIT_sum"] + out["TCC_MISS_sum"])
 waves = out.get("SQ_WAVES")
 if waves and "SQ_INSTS_VALU" in out:
     batches = None
