@@ -400,8 +400,10 @@ void emit_hyb_entry(const uint32_t *rec, bool v6, uint32_t r, std::vector<uint32
     const uint32_t dbm = port_blocks(lo >> 16, hi >> 16, ed);
     cold = cold || !es || !ed;
     const uint32_t exact = ((m[0] >> 8) & 0xFFu) ? kEntExact : 0u;
+    const uint32_t output = v6 ? rec[19] : rec[7];
+    const uint32_t ocode = std::min(output, kHybOutCold);
     blob.insert(blob.end(), {sa, da, (m[0] & 0xFFu) | exact | (r << kEntIndexShift),
-                             sl | dl << 6 | (cold ? kHybCold : 0u) | sbm << 16 | dbm << 24});
+                             sl | dl << 6 | (cold ? kHybCold : 0u) | ocode << kHybOutShift | sbm << 16 | dbm << 24});
 }
 
 // Cold record of record r: {lo, hi, output, 0} (+ IPv6 extension words).
@@ -520,18 +522,28 @@ void build_hybrid(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vec
     // Policy (profiles/r1_hybrid/): directories in LDS with per-lane walks
     // while that keeps the expected candidates per packet short; past that,
     // wide directories in global memory and the wave-flattened candidates.
+    // Tuning overrides (experiments, tests; unset in production):
+    // NFFACL_TUNE_DIR_KB sets the directory budget, NFFACL_TUNE_FLAT=0/1
+    // forces the form (directories past LDS size always give the flat form).
     const size_t tuned = tuned_dir_budget();
+    const char *fv = std::getenv("NFFACL_TUNE_FLAT");
+    const int force = fv && *fv ? std::atoi(fv) : -1;
     bool flat;
     if (tuned) {
         size_and_fill(all, weight, tuned);
-        flat = tuned > kLdsTableBytes;
+        flat = force == 1 || tuned > kLdsTableBytes;
+    } else if (force >= 0) {
+        flat = force == 1;
+        size_and_fill(all, weight, flat ? kHybFlatDirBytes : kHybLaneDirBytes);
     } else {
         flat = size_and_fill(all, weight, kHybLaneDirBytes) > kHybFlatCandidates;
         if (flat) size_and_fill(all, weight, kHybFlatDirBytes);
     }
     std::vector<uint32_t> &blob = out.blob;
     FamilyIndex *fi[2] = {&out.idx4, &out.idx6};
-    // LDS image: the eight directories (values patched to absolute entry numbers below)
+    const std::vector<uint32_t> *recs[2] = {&rec4, &rec6};
+    const uint32_t rw[2] = {kRec4Dwords, kRec6Dwords};
+    // the eight directories first: the LDS image of the lane form
     for (int f = 0; f < 2; ++f)
         for (int k = 0; k < 4; ++k) {
             fi[f]->dims[k].off_dir = static_cast<uint32_t>(blob.size());
@@ -539,12 +551,12 @@ void build_hybrid(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vec
         }
     while (blob.size() % 4) blob.push_back(0);
     out.lds_dwords = flat ? 0u : static_cast<uint32_t>(blob.size());
-    // global part: candidate lists, residual lists, cold records
-    const std::vector<uint32_t> *recs[2] = {&rec4, &rec6};
-    const uint32_t rw[2] = {kRec4Dwords, kRec6Dwords};
     for (int f = 0; f < 2; ++f) {
         const bool v6 = f == 1;
-        fi[f]->entry_dwords = kHybEntDwords;
+        // lane form: INDEXED's inline entries (exact, output inline — a hit
+        // costs no further read); flat form: compact entries + cold records
+        const uint32_t ew = flat ? kHybEntDwords : (v6 ? kEnt6Dwords : kEnt4Dwords);
+        fi[f]->entry_dwords = ew;
         for (int k = 0; k < 4; ++k) {
             DimBuild &d = *all[4 * f + k];
             DimInfo &di = fi[f]->dims[k];
@@ -555,19 +567,30 @@ void build_hybrid(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vec
             di.n_ent = d.ents.size();
             di.max_list = d.max_list;
             di.off_ent = static_cast<uint32_t>(blob.size());
-            const uint32_t first = di.off_ent / kHybEntDwords;
-            for (size_t t = 0; t <= di.n_buckets; ++t) blob[di.off_dir + t] += first;
-            for (uint32_t r : d.ents) emit_hyb_entry(recs[f]->data() + size_t(r) * rw[f], v6, r, blob);
+            if (flat) {  // directory values: absolute entry numbers (16-byte units)
+                const uint32_t first = di.off_ent / kHybEntDwords;
+                for (size_t t = 0; t <= di.n_buckets; ++t) blob[di.off_dir + t] += first;
+                for (uint32_t r : d.ents) emit_hyb_entry(recs[f]->data() + size_t(r) * rw[f], v6, r, blob);
+            } else {     // relative to off_ent, as INDEXED
+                for (uint32_t r : d.ents) emit_entry(recs[f]->data() + size_t(r) * rw[f], v6, r, blob);
+                if (d.ents.empty()) blob.insert(blob.end(), ew, 0u);  // keep entry 0 addressable
+            }
             if (!d.rules.empty()) fi[f]->used_slots = k + 1;
         }
         fi[f]->off_resid = static_cast<uint32_t>(blob.size());
         fi[f]->n_resid = static_cast<uint32_t>(plan[f].resid.size());
-        for (uint32_t r : plan[f].resid) emit_hyb_entry(recs[f]->data() + size_t(r) * rw[f], v6, r, blob);
+        for (uint32_t r : plan[f].resid) {
+            if (flat) emit_hyb_entry(recs[f]->data() + size_t(r) * rw[f], v6, r, blob);
+            else emit_entry(recs[f]->data() + size_t(r) * rw[f], v6, r, blob);
+        }
+        while (blob.size() % 4) blob.push_back(0);
     }
-    out.off_rec4 = static_cast<uint32_t>(blob.size());
-    for (uint32_t r = 0; r < n4; ++r) emit_cold(rec4.data() + size_t(r) * kRec4Dwords, false, blob);
-    out.off_rec6 = static_cast<uint32_t>(blob.size());
-    for (uint32_t r = 0; r < n6; ++r) emit_cold(rec6.data() + size_t(r) * kRec6Dwords, true, blob);
+    if (flat) {
+        out.off_rec4 = static_cast<uint32_t>(blob.size());
+        for (uint32_t r = 0; r < n4; ++r) emit_cold(rec4.data() + size_t(r) * kRec4Dwords, false, blob);
+        out.off_rec6 = static_cast<uint32_t>(blob.size());
+        for (uint32_t r = 0; r < n6; ++r) emit_cold(rec6.data() + size_t(r) * kRec6Dwords, true, blob);
+    }
 }
 
 // Indexed tables encode id_mask as one bit and the rule index in 23 bits.

@@ -358,9 +358,9 @@ struct IndexedArgs {
 enum TableMode : int {
     kTabGlobal = 0,  // INDEXED, read through L1/L2/MALL
     kTabLds = 1,     // INDEXED, staged whole in LDS
-    kTabHybrid = 2,  // HYBRID: directories in LDS, lists + cold records global
-    kTabHybrid2 = 3, // HYBRID, two list entries per slot per loop trip
-    kTabHybrid4 = 6, // HYBRID, four
+    kTabSplit = 2,   // HYBRID lane form: INDEXED entries in global memory,
+                     // directories staged in LDS, 2 entries per slot per trip
+    kTabSplit1 = 3,  // the same, 1 entry per slot per trip
     kTabFlat = 4,    // HYBRID table, directories read from global memory, the
                      // candidates of a wave's 64 packets tested 64 at a time,
                      // 2 rounds of loads in flight
@@ -382,6 +382,14 @@ struct LdsTab {
 struct GlobalTab {
     const uint32_t *__restrict__ p;
     __device__ __forceinline__ uint32_t ld(uint32_t i) const { return p[i]; }
+    __device__ __forceinline__ u32x4 ld4(uint32_t i) const {
+        return reinterpret_cast<const u32x4 *>(p)[i >> 2];
+    }
+};
+// HYBRID lane form: directories (ld) staged in LDS, entries (ld4) global.
+struct SplitTab {
+    const uint32_t *__restrict__ p;
+    __device__ __forceinline__ uint32_t ld(uint32_t i) const { return lds_tab[i]; }
     __device__ __forceinline__ u32x4 ld4(uint32_t i) const {
         return reinterpret_cast<const u32x4 *>(p)[i >> 2];
     }
@@ -410,7 +418,9 @@ __device__ __forceinline__ uint32_t entry_miss_ext(const T &tab, uint32_t off, c
 // every iteration tests the next entry of every slot list, so the wave pays
 // max(list lengths) table round trips, not their sum.  Loops have
 // wave-uniform trip counts (ballots) and predicated bodies.
-template <int NS, class T>
+// U = list entries per slot per loop trip: all NS x U entry loads of a trip
+// are issued before any is tested.
+template <int NS, int U, class T>
 __device__ __forceinline__ uint32_t classify_indexed(const T &tab, const IndexedArgs &a, const Fields &f) {
     const bool v6 = f.is6;
     const bool mine = f.is4 || f.is6;
@@ -435,23 +445,35 @@ __device__ __forceinline__ uint32_t classify_indexed(const T &tab, const Indexed
 #pragma unroll
         for (int s = 0; s < NS; ++s) any |= c[s] < e[s];
         if (!ballot(any)) break;
+        u32x4 A[NS][U], B[NS][U];
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t off = base[s] + (c[s] + u < e[s] ? c[s] + u : 0u) * ew;
+                A[s][u] = tab.ld4(off);
+                B[s][u] = tab.ld4(off + 4);
+            }
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
-            const bool act = c[s] < e[s];
-            const uint32_t off = base[s] + (act ? c[s] : 0u) * ew;
-            const u32x4 A = tab.ld4(off), B = tab.ld4(off + 4);
-            const uint32_t idx = B.x >> kEntIndexShift;
-            const bool earlier = act && idx < best;
-            bool pass = entry_miss(A, B, f) == 0u;
-            const bool ext = v6 && earlier && pass;
-            if (ballot(ext)) {
-                if (ext) pass = entry_miss_ext(tab, off + 8, f) == 0u;
+            bool go = true;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const bool act = go && c[s] + u < e[s];
+                const uint32_t idx = B[s][u].x >> kEntIndexShift;
+                const bool earlier = act && idx < best;
+                bool pass = entry_miss(A[s][u], B[s][u], f) == 0u;
+                const bool ext = v6 && earlier && pass;
+                if (ballot(ext)) {
+                    if (ext) pass = entry_miss_ext(tab, base[s] + (c[s] + u) * ew + 8, f) == 0u;
+                }
+                const bool take = earlier && pass;
+                best = take ? idx : best;
+                out = take ? B[s][u].w : out;
+                // stop at a hit, or once the ascending list has passed `best`
+                go = earlier && !pass;
             }
-            const bool take = earlier && pass;
-            best = take ? idx : best;
-            out = take ? B.w : out;
-            // stop at a hit, or once the ascending list has passed `best`
-            c[s] = (earlier && !pass) ? c[s] + 1 : e[s];
+            c[s] = go ? c[s] + U : e[s];
         }
     }
     // rules with no selective key: wave-uniform scan in rule order per family
@@ -511,91 +533,6 @@ __device__ __forceinline__ bool hyb_cold_ok(const IndexedArgs &a, bool v6, uint3
     uint32_t m = port_miss(f.ports, C.x, C.y);
     if (v6) m |= entry_miss_ext(g, off + 4, f);
     return m == 0u;
-}
-
-// One candidate of a slot list: the common test, confirmed on the cold
-// record when the entry says so (ballot-gated: only waves with such a lane
-// pay the cold read).  Returns true while the walk must go on.
-__device__ __forceinline__ bool hyb_step(const IndexedArgs &a, const Fields &f, bool act, const u32x4 &E,
-                                         uint32_t ks, uint32_t kd, uint32_t pb, uint32_t &best) {
-    const uint32_t idx = E.z >> kEntIndexShift;
-    const bool earlier = act && idx < best;
-    bool pass = hyb_pass(E, ks, kd, f.proto, pb);
-    const bool cold = earlier && pass && (E.w & kHybCold);
-    if (ballot(cold)) {
-        if (cold) pass = hyb_cold_ok(a, f.is6, idx, f);
-    }
-    const bool take = earlier && pass;
-    best = take ? idx : best;
-    // stop at a hit, or once the ascending list has passed `best`
-    return earlier && !pass;
-}
-
-// U = list entries per slot per loop trip (both loads issued together).
-template <int NS, int U>
-__device__ __forceinline__ uint32_t classify_hybrid(const IndexedArgs &a, const Fields &f) {
-    const bool v6 = f.is6;
-    const bool mine = f.is4 || f.is6;
-    const uint32_t ks = __builtin_bswap32(f.s[0]), kd = __builtin_bswap32(f.t[0]);
-    const uint32_t sport = f.ports & 0xFFFFu, dport = f.ports >> 16;
-    const uint32_t key[4] = {kd, ks, dport, sport};
-    const uint32_t pb = (1u << (16 + (sport >> kHybPortBlockShift))) | (1u << (24 + (dport >> kHybPortBlockShift)));
-    const u32x4 *G = reinterpret_cast<const u32x4 *>(a.tab);
-    uint32_t c[NS], e[NS];
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-        const SlotArgs &s4 = a.f4.slot[s], &s6 = a.f6.slot[s];
-        const uint32_t shift = v6 ? s6.shift : s4.shift;
-        const uint32_t dir = v6 ? s6.off_dir : s4.off_dir;
-        const uint32_t t = key[s] >> shift;
-        const uint32_t lo = lds_tab[dir + t], hi = lds_tab[dir + t + 1];  // one ds_read2
-        c[s] = lo;
-        e[s] = mine ? hi : lo;
-    }
-    uint32_t best = kNone;
-    while (true) {
-        bool any = false;
-#pragma unroll
-        for (int s = 0; s < NS; ++s) any |= c[s] < e[s];
-        if (!ballot(any)) break;
-        u32x4 E[NS][U];
-#pragma unroll
-        for (int s = 0; s < NS; ++s)
-#pragma unroll
-            for (int u = 0; u < U; ++u) E[s][u] = G[c[s] + u < e[s] ? c[s] + u : 0u];
-#pragma unroll
-        for (int s = 0; s < NS; ++s) {
-            bool go = true;
-#pragma unroll
-            for (int u = 0; u < U; ++u) go = hyb_step(a, f, go && c[s] + u < e[s], E[s][u], ks, kd, pb, best);
-            c[s] = go ? c[s] + U : e[s];
-        }
-    }
-    // rules with no selective key: wave-uniform scan in rule order per family
-#pragma unroll
-    for (int fam = 0; fam < 2; ++fam) {
-        const FamArgs &fa = fam ? a.f6 : a.f4;
-        const bool in_fam = fam ? f.is6 : f.is4;
-        for (uint32_t i = 0; i < fa.n_resid; ++i) {
-            const u32x4 E = G[(fa.off_resid >> 2) + i];
-            const uint32_t idx = E.z >> kEntIndexShift;
-            const bool want = in_fam && idx < best;
-            if (!ballot(want)) break;  // residual list ascends too
-            bool pass = want && hyb_pass(E, ks, kd, f.proto, pb);
-            const bool cold = pass && (E.w & kHybCold);
-            if (ballot(cold)) {
-                if (cold) pass = hyb_cold_ok(a, fam == 1, idx, f);
-            }
-            best = pass ? idx : best;
-        }
-    }
-    // the winner's output number, from its cold record
-    const bool hit = best != kNone;
-    uint32_t out = 0;
-    if (ballot(hit)) {
-        if (hit) out = a.tab[v6 ? a.f6.off_cold + best * kHybCold6Dwords + 2 : a.f4.off_cold + best * kHybCold4Dwords + 2];
-    }
-    return out;
 }
 
 // ---- FLAT: a wave's candidates, 64 at a time --------------------------------
@@ -731,11 +668,12 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
                 }
                 if (cold) pass = hyb_cold_ok(a, of.is6, idx, of);
             }
-            if (pass) atomicMin(&W.best[o], idx);
+            // rule index << 3 | output code: the minimum carries the winner's output
+            if (pass) atomicMin(&W.best[o], (idx << 3) | ((E[j].w >> kHybOutShift) & 7u));
         }
         wave_lds_sync();
     }
-    uint32_t best = W.best[lane];
+    uint32_t best = W.best[lane];  // kNone or rule index << 3 | output code
     // rules with no selective key: wave-uniform scan in rule order per family
     const uint32_t pb = (1u << (16 + (sport >> kHybPortBlockShift))) | (1u << (24 + (dport >> kHybPortBlockShift)));
 #pragma unroll
@@ -745,20 +683,23 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
         for (uint32_t i = 0; i < fa.n_resid; ++i) {
             const u32x4 E = G[(fa.off_resid >> 2) + i];
             const uint32_t idx = E.z >> kEntIndexShift;
-            const bool want = in_fam && idx < best;
+            const bool want = in_fam && idx < (best >> 3);
             if (!ballot(want)) break;  // residual list ascends too
             bool pass = want && hyb_pass(E, ks, kd, f.proto, pb);
             const bool cold = pass && (E.w & kHybCold);
             if (ballot(cold)) {
                 if (cold) pass = hyb_cold_ok(a, fam == 1, idx, f);
             }
-            best = pass ? idx : best;
+            best = pass ? (idx << 3) | ((E.w >> kHybOutShift) & 7u) : best;
         }
     }
+    // output numbers below 7 travel in the entry; others come from the cold record
     const bool hit = best != kNone;
-    uint32_t out = 0;
-    if (ballot(hit)) {
-        if (hit) out = a.tab[v6 ? a.f6.off_cold + best * kHybCold6Dwords + 2 : a.f4.off_cold + best * kHybCold4Dwords + 2];
+    uint32_t out = hit ? best & 7u : 0u;
+    const bool rd = hit && out == kHybOutCold;
+    if (ballot(rd)) {
+        const uint32_t r = best >> 3;
+        if (rd) out = a.tab[v6 ? a.f6.off_cold + r * kHybCold6Dwords + 2 : a.f4.off_cold + r * kHybCold4Dwords + 2];
     }
     return out;
 }
@@ -770,11 +711,10 @@ __device__ __forceinline__ uint32_t classify_any(const IndexedArgs &a, const Fie
         const uint32_t lane = lane_id();
         return classify_flat<NS, TM == kTabFlat4 ? 4 : 2>(a, f, W[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)], lane);
     }
-    if (TM == kTabLds) return classify_indexed<NS>(LdsTab{}, a, f);
-    if (TM == kTabHybrid) return classify_hybrid<NS, 1>(a, f);
-    if (TM == kTabHybrid2) return classify_hybrid<NS, 2>(a, f);
-    if (TM == kTabHybrid4) return classify_hybrid<NS, 4>(a, f);
-    return classify_indexed<NS>(GlobalTab{a.tab}, a, f);
+    if (TM == kTabLds) return classify_indexed<NS, 1>(LdsTab{}, a, f);
+    if (TM == kTabSplit) return classify_indexed<NS, 2>(SplitTab{a.tab}, a, f);
+    if (TM == kTabSplit1) return classify_indexed<NS, 1>(SplitTab{a.tab}, a, f);
+    return classify_indexed<NS, 1>(GlobalTab{a.tab}, a, f);
 }
 
 // Grid-stride over 64-packet batches.
@@ -788,7 +728,7 @@ template <int NS, int TM, int MODE>
 __global__ void __launch_bounds__(1024)
 k_indexed_slots(const uint8_t *__restrict__ slots, uint32_t stride, uint64_t n, IndexedArgs a,
                 uint32_t *__restrict__ port_out, uint64_t *__restrict__ permit_out) {
-    if (TM == kTabLds || TM == kTabHybrid || TM == kTabHybrid2 || TM == kTabHybrid4) stage_table(a);
+    if (TM == kTabLds || TM == kTabSplit || TM == kTabSplit1) stage_table(a);
     const uint32_t lane = lane_id();
     const uint32_t wpb = blockDim.x >> 6;
     const uint64_t wave0 = uint64_t(blockIdx.x) * wpb + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -859,13 +799,13 @@ template <int NS, int TM>
 __global__ void __launch_bounds__(1024)
 k_indexed_frames(const uint8_t *__restrict__ frames, const uint64_t *__restrict__ desc, uint64_t n,
                  IndexedArgs a, uint32_t *__restrict__ port_out, uint64_t *__restrict__ permit_out) {
-    if (TM == kTabLds || TM == kTabHybrid || TM == kTabHybrid2 || TM == kTabHybrid4) stage_table(a);
+    if (TM == kTabLds || TM == kTabSplit || TM == kTabSplit1) stage_table(a);
     // Software pipeline.  Always: the next batch's descriptors load while this
     // batch is classified (the frame load depends on them).  PF (per-lane
     // HYBRID walks, whose LDS directories hold the CU to 16 waves and so leave
     // VGPRs to spare): also the next batch's 64-byte frame lines, and the
     // descriptors of the batch after.
-    constexpr bool PF = TM == kTabHybrid2 || TM == kTabHybrid4;
+    constexpr bool PF = TM == kTabSplit || TM == kTabSplit1;
     uint64_t ds_n1 = 0;  // descriptor of this lane's packet in the next batch
     uint64_t ds_n2 = 0;  // PF: ... in the batch after
     uint32_t f_n1[16];   // PF: first 64 bytes of the next batch's packet
@@ -988,15 +928,30 @@ static int tune_env(const char *name, int dflt) {
     return v && *v ? std::atoi(v) : dflt;
 }
 
+// The kernel a table gets must match the layout it was compiled to: checked
+// on the host before every indexed launch (a mismatch would read the blob
+// with the wrong offsets).
+static bool table_consistent(const DevTable *t) {
+    const CompiledTable &m = t->meta;
+    const size_t dw = m.blob.size();
+    if (m.algo == NFFACL_ALGO_HYBRID && m.lds_dwords == 0)
+        return m.idx4.entry_dwords == kHybEntDwords && m.idx6.entry_dwords == kHybEntDwords &&
+               m.off_rec4 <= dw && m.off_rec6 <= dw;
+    if (m.algo == NFFACL_ALGO_HYBRID)
+        return size_t(m.lds_dwords) * sizeof(uint32_t) <= kLdsTableBytes && m.lds_dwords <= dw &&
+               m.idx4.entry_dwords == kEnt4Dwords && m.idx6.entry_dwords == kEnt6Dwords;
+    return m.idx4.entry_dwords == kEnt4Dwords && m.idx6.entry_dwords == kEnt6Dwords;
+}
+
 static IndexedLaunch indexed_launch(const DevTable *t) {
     const uint32_t used = std::max(t->meta.idx4.used_slots, t->meta.idx6.used_slots);
     const int ns = used <= 2 ? 2 : static_cast<int>(used);
     IndexedLaunch L{dev::kTabGlobal, ns, 256u, 8u, 0};
     size_t staged = 0;
-    // HYBRID: directories staged in LDS and walked per lane, or (directories
-    // too large for LDS, or forced) read from global memory, candidates flat.
-    const bool hyb_flat = t->meta.lds_dwords == 0 || tune_env("NFFACL_TUNE_FLAT", 0) != 0;
-    if (t->meta.algo == NFFACL_ALGO_HYBRID && hyb_flat) {
+    // HYBRID: the compiled form decides (table.hpp) — lane form: directories
+    // staged in LDS, inline entries walked per lane; flat form (lds_dwords 0):
+    // directories and compact entries in global memory, candidates flat.
+    if (t->meta.algo == NFFACL_ALGO_HYBRID && t->meta.lds_dwords == 0) {
         L.tm = tune_env("NFFACL_TUNE_ROUNDS", 4) == 2 ? dev::kTabFlat : dev::kTabFlat4;
         L.block = static_cast<uint32_t>(tune_env("NFFACL_TUNE_BLOCK", 256));
         L.per_cu = static_cast<uint32_t>(tune_env("NFFACL_TUNE_PER_CU", 8));
@@ -1004,8 +959,7 @@ static IndexedLaunch indexed_launch(const DevTable *t) {
         return L;
     }
     if (t->meta.algo == NFFACL_ALGO_HYBRID) {
-        const int u = tune_env("NFFACL_TUNE_UNROLL", 2);
-        L.tm = u == 1 ? dev::kTabHybrid : u == 4 ? dev::kTabHybrid4 : dev::kTabHybrid2;
+        L.tm = tune_env("NFFACL_TUNE_UNROLL", 1) == 2 ? dev::kTabSplit : dev::kTabSplit1;
         staged = size_t(t->meta.lds_dwords) * sizeof(uint32_t);
     } else {
         const size_t bytes = t->meta.blob.size() * sizeof(uint32_t);
@@ -1055,9 +1009,8 @@ static void dispatch_indexed(int ns, int tm, F &&f) {
     auto with_ns = [&](auto nsc) {
         switch (tm) {
         case dev::kTabLds: f(nsc, std::integral_constant<int, dev::kTabLds>{}); break;
-        case dev::kTabHybrid: f(nsc, std::integral_constant<int, dev::kTabHybrid>{}); break;
-        case dev::kTabHybrid2: f(nsc, std::integral_constant<int, dev::kTabHybrid2>{}); break;
-        case dev::kTabHybrid4: f(nsc, std::integral_constant<int, dev::kTabHybrid4>{}); break;
+        case dev::kTabSplit: f(nsc, std::integral_constant<int, dev::kTabSplit>{}); break;
+        case dev::kTabSplit1: f(nsc, std::integral_constant<int, dev::kTabSplit1>{}); break;
         case dev::kTabFlat: f(nsc, std::integral_constant<int, dev::kTabFlat>{}); break;
         case dev::kTabFlat4: f(nsc, std::integral_constant<int, dev::kTabFlat4>{}); break;
         default: f(nsc, std::integral_constant<int, dev::kTabGlobal>{}); break;
@@ -1073,7 +1026,7 @@ int prepare_kernels() {
     static hipError_t err = hipSuccess;
     std::call_once(once, [] {
         for (int ns = 2; ns <= 4; ++ns)
-            for (int tm : {int(dev::kTabLds), int(dev::kTabHybrid), int(dev::kTabHybrid2), int(dev::kTabHybrid4)})
+            for (int tm : {int(dev::kTabLds), int(dev::kTabSplit), int(dev::kTabSplit1)})
                 dispatch_indexed(ns, tm, [&](auto nsc, auto tmc) {
                     const hipError_t e = allow_lds_modes<decltype(nsc)::value, decltype(tmc)::value>();
                     if (e != hipSuccess) err = e;
@@ -1124,6 +1077,10 @@ int launch_slots(nffacl_engine *eng, const DevTable *t, const uint8_t *d_slots, 
                  uint64_t n, uint32_t *d_port, uint64_t *d_permit, hipStream_t stream, uint32_t flags) {
     if (n == 0) return NFFACL_OK;
     if (t->meta.algo != NFFACL_ALGO_LINEAR) {
+        if (!table_consistent(t)) {
+            set_last_error("compiled table layout does not match its kernel");
+            return NFFACL_ERR_INVALID_ARG;
+        }
         dev::IndexedArgs a = indexed_args(t);
         a.flags = flags;
         const IndexedLaunch L = indexed_launch(t);
@@ -1150,6 +1107,10 @@ int launch_frames(nffacl_engine *eng, const DevTable *t, const uint8_t *d_frames
                   hipStream_t stream, uint32_t flags) {
     if (n == 0) return NFFACL_OK;
     if (t->meta.algo != NFFACL_ALGO_LINEAR) {
+        if (!table_consistent(t)) {
+            set_last_error("compiled table layout does not match its kernel");
+            return NFFACL_ERR_INVALID_ARG;
+        }
         dev::IndexedArgs a = indexed_args(t);
         a.flags = flags;
         const IndexedLaunch L = indexed_launch(t);

@@ -90,6 +90,8 @@ constexpr uint32_t kMaxIndexedRules = 1u << 23;
 // produce); other rule sets compile INDEXED.
 constexpr uint32_t kHybEntDwords = 4;
 constexpr uint32_t kHybCold = 1u << 12;
+constexpr uint32_t kHybOutShift = 13;
+constexpr uint32_t kHybOutCold = 7;  // output number >= 7: read from the cold record
 constexpr uint32_t kHybPortBlockShift = 13;
 constexpr uint32_t kHybPortBlockMask = (1u << kHybPortBlockShift) - 1u;
 constexpr uint32_t kHybCold4Dwords = 4;

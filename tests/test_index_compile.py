@@ -246,7 +246,17 @@ def hyb_test(blob, info, offs, v6, F, sel):
 
 
 def emulate_hybrid(blob, info, F, n):
+    """Flat form: every candidate of every list (no early exit), the minimum
+    passing rule index wins; its output number from the entry's 3-bit code,
+    or from the cold record when the code is 7."""
     best = np.full(n, 0xFFFFFFFF, np.uint64)
+    code = np.zeros(n, np.uint32)
+
+    def post(sel, ok, idx, w):
+        better = ok & (idx < best[sel])
+        best[sel[better]] = idx[better]
+        code[sel[better]] = (w[better] >> 13) & 7
+
     for fam, v6 in ((0, False), (1, True)):
         fi = info.fam[fam]
         mine = F["is6"] if v6 else F["is4"]
@@ -260,27 +270,25 @@ def emulate_hybrid(blob, info, F, n):
             t = (key >> np.uint64(di.shift)).astype(np.int64)
             start, end = dirv[t], dirv[t + 1]
             for k in range(di.max_list):
-                live = mine & (start < end)
+                live = mine & (start + k < end)
                 if not live.any():
                     break
                 sel = np.nonzero(live)[0]
-                ok, idx = hyb_test(blob, info, start[sel] * 4, v6, F, sel)
-                keep = idx < best[sel]
-                ok &= keep
-                best[sel[ok]] = idx[ok]
-                stop = ok | ~keep
-                start[sel] += 1
-                start[sel[stop]] = end[sel[stop]]
+                offs = (start[sel] + k) * 4
+                ok, idx = hyb_test(blob, info, offs, v6, F, sel)
+                post(sel, ok, idx, blob[offs + 3])
         for i in range(fi.n_resid):
             sel = np.nonzero(mine)[0]
-            ok, idx = hyb_test(blob, info, np.full(len(sel), fi.off_resid + 4 * i), v6, F, sel)
-            ok &= idx < best[sel]
-            best[sel[ok]] = idx[ok]
+            offs = np.full(len(sel), fi.off_resid + 4 * i)
+            ok, idx = hyb_test(blob, info, offs, v6, F, sel)
+            post(sel, ok, idx, blob[offs + 3])
     out = np.zeros(n, np.uint32)
+    hit = best != 0xFFFFFFFF
+    out[hit] = code[hit]
     for fam, v6 in ((0, False), (1, True)):
-        mine = (F["is6"] if v6 else F["is4"]) & (best != 0xFFFFFFFF)
+        rd = (F["is6"] if v6 else F["is4"]) & hit & (code == 7)
         cw = 16 if v6 else 4
-        out[mine] = blob[info.fam[fam].off_rec + best[mine].astype(np.int64) * cw + 2]
+        out[rd] = blob[info.fam[fam].off_rec + best[rd].astype(np.int64) * cw + 2]
     return best, out
 
 
@@ -293,7 +301,8 @@ def check_hybrid(text: str, slots: np.ndarray, n: int, dir_kb=None, monkeypatch=
     a4, a6 = ro.parse_text_table(text.encode()).arrays()
     want, _ = oracle.classify_slots_which(slots, 64, n, a4, a6)
     F = fields(slots, n)
-    best, out = emulate_hybrid(blob, info, F, n)
+    # lane form (directories in LDS): INDEXED's inline entries; flat form: compact + cold
+    best, out = emulate(blob, info, F, n) if info.lds_dwords else emulate_hybrid(blob, info, F, n)
     sel = ~F["skip"]
     got = np.where(best != 0xFFFFFFFF, out, 0)
     np.testing.assert_array_equal(got[sel], want[sel])
@@ -337,6 +346,16 @@ def test_hybrid_firewall_and_nested(golden):
     lines.append("ANY ANY UDP ANY ANY 9")
     text = "\n".join(lines) + "\n"
     check_hybrid(text, synth.gen_slots(synth.firewall_rules(text), n, 6), n)
+
+
+@pytest.mark.parametrize("cfg", ["c2", "c3"])
+def test_hybrid_flat_form_synthetic(cfg, monkeypatch):
+    """Directories past LDS size force the flat form (compact entries + cold
+    records) on the small configs too."""
+    g = synth.gen_rules(synth.SPECS[cfg], synth.RULE_SEEDS[cfg])
+    n = 1 << 14
+    info = check_hybrid(g.text, synth.gen_slots(g, n, 31), n, dir_kb=1024, monkeypatch=monkeypatch)
+    assert info.lds_dwords == 0 and info.fam[0].entry_dwords == 4
 
 
 def test_hybrid_falls_back_on_non_cidr_masks():
