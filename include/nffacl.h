@@ -189,7 +189,8 @@ typedef struct nffacl_dim_info {
     uint32_t off_entries;/* dword offset of the bucket entries (inline rules, ascending per bucket) */
     uint32_t n_rules;    /* rules indexed by this key */
     uint32_t max_list;   /* longest bucket list */
-    uint32_t reserved;
+    uint32_t off_dir16;  /* 0, or (two-level directory) dword offset of u16 offsets dir16[n_buckets + 1];
+                            then off_dir holds u32 group bases and dir[t] = base[t >> 6] + dir16[t] */
     uint64_t n_entries;  /* bucket entries (with replication) */
 } nffacl_dim_info;
 

@@ -206,7 +206,7 @@ int nffacl_table_compile(const nffacl_rules *rules, int algo, uint32_t *blob, ui
         for (int k = 0; k < 4; ++k) {
             const DimInfo &d = fi[f]->dims[k];
             o.dims[k] = nffacl_dim_info{d.kind, d.shift, d.n_buckets, d.off_dir, d.off_ent, d.n_rules,
-                                        d.max_list, 0, d.n_ent};
+                                        d.max_list, d.off_dir16, d.n_ent};
         }
     }
     if (blob) {

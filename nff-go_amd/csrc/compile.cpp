@@ -428,10 +428,14 @@ uint64_t entries_at(const DimBuild &d, uint32_t rb) {
 // one bit at a time, the slot whose mean list grows least per byte saved
 // (weighted by its family's share of the rules, a proxy for its share of
 // the traffic).
-void size_directories(DimBuild *const *all, const double *weight, int nd, size_t budget) {
+void size_directories(DimBuild *const *all, const double *weight, int nd, size_t budget, bool dir16) {
     std::vector<uint32_t> rb(nd);
     std::vector<std::vector<double>> mean(nd);
-    auto bytes = [&](int i, uint32_t b) { return all[i]->rules.empty() ? 12.0 : 4.0 * ((1u << b) + 1); };
+    auto bytes = [&](int i, uint32_t b) {
+        if (all[i]->rules.empty()) return 16.0;
+        const double nb = double(1u << b);
+        return dir16 ? 2.0 * (nb + 4) + 4.0 * (std::floor(nb / (1u << kDir16GroupShift)) + 2) : 4.0 * (nb + 1);
+    };
     for (int i = 0; i < nd; ++i) {
         const DimBuild &d = *all[i];
         if (d.rules.empty()) { rb[i] = 1; continue; }
@@ -490,8 +494,8 @@ size_t tuned_dir_budget() {
 // Radix widths for `budget` bytes of directories, then the bucket lists;
 // returns the expected candidates per packet (mean list length summed over
 // the slots, families weighted by their share of the rules).
-double size_and_fill(DimBuild *const *all, const double *weight, size_t budget) {
-    size_directories(all, weight, 8, budget);
+double size_and_fill(DimBuild *const *all, const double *weight, size_t budget, bool dir16 = false) {
+    size_directories(all, weight, 8, budget, dir16);
     double expect = 0;
     for (int i = 0; i < 8; ++i) {
         DimBuild &d = *all[i];
@@ -528,17 +532,28 @@ void build_hybrid(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vec
     const size_t tuned = tuned_dir_budget();
     const char *fv = std::getenv("NFFACL_TUNE_FLAT");
     const int force = fv && *fv ? std::atoi(fv) : -1;
+    const char *dv = std::getenv("NFFACL_TUNE_DIR16");
+    const bool want16 = !(dv && *dv && std::atoi(dv) == 0);
     bool flat;
     if (tuned) {
-        size_and_fill(all, weight, tuned);
         flat = force == 1 || tuned > kLdsTableBytes;
+        size_and_fill(all, weight, tuned, !flat && want16);
     } else if (force >= 0) {
         flat = force == 1;
-        size_and_fill(all, weight, flat ? kHybFlatDirBytes : kHybLaneDirBytes);
+        size_and_fill(all, weight, flat ? kHybFlatDirBytes : kHybLaneDirBytes, !flat && want16);
     } else {
-        flat = size_and_fill(all, weight, kHybLaneDirBytes) > kHybFlatCandidates;
+        flat = size_and_fill(all, weight, kHybLaneDirBytes, want16) > kHybFlatCandidates;
         if (flat) size_and_fill(all, weight, kHybFlatDirBytes);
     }
+    // lane form: two-level directories unless some 64-bucket group holds
+    // 65536+ entries (then plain u32, re-sized for the same budget)
+    bool dir16 = !flat && want16;
+    for (int i = 0; i < 8 && dir16; ++i) {
+        const std::vector<uint32_t> &dir = all[i]->dir;
+        for (size_t t = 0; t < dir.size(); ++t)
+            if (dir[t] - dir[(t >> kDir16GroupShift) << kDir16GroupShift] > 0xFFFFu) { dir16 = false; break; }
+    }
+    if (!flat && want16 && !dir16) size_and_fill(all, weight, tuned ? tuned : kHybLaneDirBytes, false);
     std::vector<uint32_t> &blob = out.blob;
     FamilyIndex *fi[2] = {&out.idx4, &out.idx6};
     const std::vector<uint32_t> *recs[2] = {&rec4, &rec6};
@@ -546,8 +561,22 @@ void build_hybrid(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vec
     // the eight directories first: the LDS image of the lane form
     for (int f = 0; f < 2; ++f)
         for (int k = 0; k < 4; ++k) {
-            fi[f]->dims[k].off_dir = static_cast<uint32_t>(blob.size());
-            blob.insert(blob.end(), all[4 * f + k]->dir.begin(), all[4 * f + k]->dir.end());
+            const std::vector<uint32_t> &dir = all[4 * f + k]->dir;
+            DimInfo &di = fi[f]->dims[k];
+            di.off_dir = static_cast<uint32_t>(blob.size());
+            if (!dir16) {
+                blob.insert(blob.end(), dir.begin(), dir.end());
+                continue;
+            }
+            const size_t nb = dir.size() - 1;
+            const size_t groups = (nb >> kDir16GroupShift) + 2;  // base[g + 1] stays readable
+            for (size_t g = 0; g < groups; ++g) blob.push_back(dir[std::min(g << kDir16GroupShift, nb)]);
+            di.off_dir16 = static_cast<uint32_t>(blob.size());
+            auto rel = [&](size_t t) -> uint32_t {
+                return t <= nb ? dir[t] - dir[(t >> kDir16GroupShift) << kDir16GroupShift] : 0u;
+            };
+            const size_t words = (nb + 2) / 2 + 1;  // dword (t >> 1) + 1 stays readable
+            for (size_t w = 0; w < words; ++w) blob.push_back(rel(2 * w) | rel(2 * w + 1) << 16);
         }
     while (blob.size() % 4) blob.push_back(0);
     out.lds_dwords = flat ? 0u : static_cast<uint32_t>(blob.size());

@@ -16,7 +16,10 @@ struct DimInfo {
     uint32_t kind = 0;       // KeyKind
     uint32_t shift = 0;      // bucket = key >> shift
     uint32_t n_buckets = 0;  // 2^(key bits - shift)
-    uint32_t off_dir = 0;    // dword offset of dir[n_buckets + 1]
+    uint32_t off_dir = 0;    // dword offset of dir[n_buckets + 1] (or, with off_dir16, of the
+                             // 2-level directory's group bases base[n_buckets / 64 + 2])
+    uint32_t off_dir16 = 0;  // 0, or dword offset of the u16 offsets dir16[n_buckets + 1]:
+                             // dir[t] = base[t >> 6] + dir16[t]
     uint32_t off_ent = 0;    // dword offset of the bucket entries (inline rule entries)
     uint32_t n_rules = 0;    // rules assigned to this dimension
     uint64_t n_ent = 0;      // bucket entries (with replication)

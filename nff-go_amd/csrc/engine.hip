@@ -82,7 +82,8 @@ struct Fields {
 // down by one dword and parses as usual (d[15] is never read afterwards).
 template <class FarDwords>
 __device__ __forceinline__ void parse_fields(uint32_t (&d)[16], bool live, Fields &f, FarDwords far,
-                                             bool vlan) {
+                                             uint32_t flags) {
+    const bool vlan = (flags & NFFACL_PARSE_VLAN) != 0;
     uint32_t l3dw = 3u;  // dword holding the first L3 byte (at byte 2 of it)
     if (vlan) {
         const bool tagged = (d[3] & 0xFFFFu) == 0x0081u;  // 0x8100 on the wire
@@ -101,8 +102,11 @@ __device__ __forceinline__ void parse_fields(uint32_t (&d)[16], bool live, Field
     const uint32_t ihl = (d[3] >> 16) & 0xFu;
     uint32_t pw = f.is6 ? funnel16(d[14], d[13]) : funnel16(d[9], d[8]);
     if (f.is4 && ihl != 5u) {
+        // L4 bytes L3+4*IHL .. +3 = dword l3dw+IHL, byte 2.  (Taking IHL <= 11
+        // from the registers instead, through a select chain, measured 2.6 %
+        // slower on C2 and 1 % faster on C5 in one-process A/B: memory.)
         uint32_t lo, hi;
-        far(l3dw + ihl, lo, hi);  // L4 bytes L3+4*IHL .. +3 = dword l3dw+IHL, byte 2
+        far(l3dw + ihl, lo, hi);
         pw = funnel16(hi, lo);
     }
     f.ports = swap_halves(pw);
@@ -307,7 +311,7 @@ k_linear_slots(const uint8_t *__restrict__ slots, uint32_t stride, uint64_t n, L
         Fields f;
         parse_fields(d, live, f, [&](uint32_t k, uint32_t &lo, uint32_t &hi) {
             far_dwords(pkt, stride, k, lo, hi);
-        }, a.flags & NFFACL_PARSE_VLAN);
+        }, a.flags);
         const uint32_t res = classify_linear(f, a.rec4, a.n4, a.rec6, a.n6);
         store_verdicts(base, lane, live, res, port_out, permit_out);
     }
@@ -329,7 +333,7 @@ k_linear_frames(const uint8_t *__restrict__ frames, const uint64_t *__restrict__
         Fields f;
         parse_fields(d, live, f, [&](uint32_t k, uint32_t &lo, uint32_t &hi) {
             far_dwords(pkt, len, k, lo, hi);
-        }, a.flags & NFFACL_PARSE_VLAN);
+        }, a.flags);
         const uint32_t res = classify_linear(f, a.rec4, a.n4, a.rec6, a.n6);
         store_verdicts(base, lane, live, res, port_out, permit_out);
     }
@@ -340,7 +344,7 @@ k_linear_frames(const uint8_t *__restrict__ frames, const uint64_t *__restrict__
 // ---------------------------------------------------------------------------
 
 struct SlotArgs {
-    uint32_t shift, off_dir, off_ent, pad;
+    uint32_t shift, off_dir, off_ent, off_dir16;  // off_dir16: 0 = plain u32 directory
 };
 struct FamArgs {
     SlotArgs slot[4];  // [dst addr, src addr, dst port, src port]
@@ -359,8 +363,11 @@ enum TableMode : int {
     kTabGlobal = 0,  // INDEXED, read through L1/L2/MALL
     kTabLds = 1,     // INDEXED, staged whole in LDS
     kTabSplit = 2,   // HYBRID lane form: INDEXED entries in global memory,
-                     // directories staged in LDS, 2 entries per slot per trip
-    kTabSplit1 = 3,  // the same, 1 entry per slot per trip
+                     // directories staged in LDS, one workgroup per CU; the
+                     // spare VGPRs buy the frames kernel a two-batch software
+                     // pipeline.  (Two workgroups per CU with <= 78 KiB of
+                     // directories and 64 VGPRs ran 18 % slower on C3:
+                     // longer lists, spills; profiles/r1_hybrid/sw5.)
     kTabFlat = 4,    // HYBRID table, directories read from global memory, the
                      // candidates of a wave's 64 packets tested 64 at a time,
                      // 2 rounds of loads in flight
@@ -373,8 +380,19 @@ extern __shared__ __attribute__((aligned(16))) uint32_t lds_tab[];
 // ld4(i): i is a multiple of 4 (entries are 16-byte aligned, table.hpp) and is
 // indexed in vector units so the compiler can emit one ds_read_b128 /
 // global_load_dwordx4 (a byte-offset cast only gets split ds_read2_b32 pairs).
+// List bounds dir[t], dir[t + 1] of a plain u32 directory (one ds_read2 /
+// two dword loads).
+template <class T>
+__device__ __forceinline__ void bounds32(const T &tab, uint32_t dir, uint32_t t, uint32_t &lo, uint32_t &hi) {
+    lo = tab.ld(dir + t);
+    hi = tab.ld(dir + t + 1);
+}
+
 struct LdsTab {
     __device__ __forceinline__ uint32_t ld(uint32_t i) const { return lds_tab[i]; }
+    __device__ __forceinline__ void bounds(uint32_t dir, uint32_t, uint32_t t, uint32_t &lo, uint32_t &hi) const {
+        bounds32(*this, dir, t, lo, hi);
+    }
     __device__ __forceinline__ u32x4 ld4(uint32_t i) const {
         return reinterpret_cast<const u32x4 *>(lds_tab)[i >> 2];
     }
@@ -382,6 +400,9 @@ struct LdsTab {
 struct GlobalTab {
     const uint32_t *__restrict__ p;
     __device__ __forceinline__ uint32_t ld(uint32_t i) const { return p[i]; }
+    __device__ __forceinline__ void bounds(uint32_t dir, uint32_t, uint32_t t, uint32_t &lo, uint32_t &hi) const {
+        bounds32(*this, dir, t, lo, hi);
+    }
     __device__ __forceinline__ u32x4 ld4(uint32_t i) const {
         return reinterpret_cast<const u32x4 *>(p)[i >> 2];
     }
@@ -390,6 +411,20 @@ struct GlobalTab {
 struct SplitTab {
     const uint32_t *__restrict__ p;
     __device__ __forceinline__ uint32_t ld(uint32_t i) const { return lds_tab[i]; }
+    // two-level directory (table.hpp): dir[t] = base[t >> 6] + dir16[t]
+    __device__ __forceinline__ void bounds(uint32_t dir, uint32_t dir16, uint32_t t, uint32_t &lo,
+                                           uint32_t &hi) const {
+        if (dir16 == 0u) {
+            bounds32(*this, dir, t, lo, hi);
+            return;
+        }
+        const uint32_t g = t >> kDir16GroupShift;
+        const uint32_t b0 = lds_tab[dir + g], b1 = lds_tab[dir + g + 1];                         // ds_read2
+        const uint32_t w0 = lds_tab[dir16 + (t >> 1)], w1 = lds_tab[dir16 + (t >> 1) + 1];      // ds_read2
+        const bool odd = (t & 1u) != 0u;
+        lo = b0 + (odd ? w0 >> 16 : w0 & 0xFFFFu);
+        hi = (((t + 1u) >> kDir16GroupShift) != g ? b1 : b0) + (odd ? w1 & 0xFFFFu : w0 >> 16);
+    }
     __device__ __forceinline__ u32x4 ld4(uint32_t i) const {
         return reinterpret_cast<const u32x4 *>(p)[i >> 2];
     }
@@ -435,7 +470,8 @@ __device__ __forceinline__ uint32_t classify_indexed(const T &tab, const Indexed
         const uint32_t dir = v6 ? s6.off_dir : s4.off_dir;
         base[s] = v6 ? s6.off_ent : s4.off_ent;
         const uint32_t t = key[s] >> shift;  // < n_buckets for any key: both reads in range
-        const uint32_t lo = tab.ld(dir + t), hi = tab.ld(dir + t + 1);  // one ds_read2
+        uint32_t lo, hi;
+        tab.bounds(dir, v6 ? s6.off_dir16 : s4.off_dir16, t, lo, hi);
         c[s] = lo;
         e[s] = mine ? hi : lo;
     }
@@ -569,21 +605,32 @@ __device__ __forceinline__ uint32_t bperm(uint32_t v, uint32_t src_lane) {
     return static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(static_cast<int>(src_lane << 2), static_cast<int>(v)));
 }
 
-__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x, uint32_t lane) {
-#pragma unroll
-    for (uint32_t d = 1; d < 64; d <<= 1) {
-        const uint32_t y = bperm(x, lane >= d ? lane - d : lane);
-        x += lane >= d ? y : 0u;
-    }
+// Wave-wide inclusive scans on DPP (GFX9 controls): row_shr 1, 2, 4, 8 build
+// the prefix inside each 16-lane row, row_bcast:15 (rows 1, 3) and
+// row_bcast:31 (rows 2, 3) carry the row totals.  Lanes without a source read
+// 0 (bound_ctrl), the identity of both + and max over unsigned values.
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ uint32_t dpp0(uint32_t x) {
+    return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), CTRL, ROW_MASK, 0xF, true));
+}
+
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
+    x += dpp0<0x111>(x);
+    x += dpp0<0x112>(x);
+    x += dpp0<0x114>(x);
+    x += dpp0<0x118>(x);
+    x += dpp0<0x142, 0xA>(x);
+    x += dpp0<0x143, 0xC>(x);
     return x;
 }
 
-__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x, uint32_t lane) {
-#pragma unroll
-    for (uint32_t d = 1; d < 64; d <<= 1) {
-        const uint32_t y = bperm(x, lane >= d ? lane - d : lane);
-        x = max(x, y);
-    }
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
+    x = max(x, dpp0<0x111>(x));
+    x = max(x, dpp0<0x112>(x));
+    x = max(x, dpp0<0x114>(x));
+    x = max(x, dpp0<0x118>(x));
+    x = max(x, dpp0<0x142, 0xA>(x));
+    x = max(x, dpp0<0x143, 0xC>(x));
     return x;
 }
 
@@ -610,7 +657,7 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
     uint32_t total = 0;
 #pragma unroll
     for (int s = 0; s < NS; ++s) total += ln[s];
-    const uint32_t incl = wave_incl_sum(total, lane);
+    const uint32_t incl = wave_incl_sum(total);
     const uint32_t off = incl - total;  // first candidate number of this packet
     const uint32_t T = __builtin_amdgcn_readlane(incl, 63);
     W.best[lane] = kNone;
@@ -637,7 +684,7 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
         uint32_t carry = 0;
 #pragma unroll
         for (int j = 0; j < R; ++j) {
-            const uint32_t m = max(wave_incl_max(W.mark[64 * j + lane], lane), carry);
+            const uint32_t m = max(wave_incl_max(W.mark[64 * j + lane]), carry);
             carry = __builtin_amdgcn_readlane(m, 63);
             const uint32_t k = win + 64u * j + lane;
             valid[j] = k < T;
@@ -712,8 +759,7 @@ __device__ __forceinline__ uint32_t classify_any(const IndexedArgs &a, const Fie
         return classify_flat<NS, TM == kTabFlat4 ? 4 : 2>(a, f, W[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)], lane);
     }
     if (TM == kTabLds) return classify_indexed<NS, 1>(LdsTab{}, a, f);
-    if (TM == kTabSplit) return classify_indexed<NS, 2>(SplitTab{a.tab}, a, f);
-    if (TM == kTabSplit1) return classify_indexed<NS, 1>(SplitTab{a.tab}, a, f);
+    if (TM == kTabSplit) return classify_indexed<NS, 1>(SplitTab{a.tab}, a, f);
     return classify_indexed<NS, 1>(GlobalTab{a.tab}, a, f);
 }
 
@@ -728,7 +774,7 @@ template <int NS, int TM, int MODE>
 __global__ void __launch_bounds__(1024)
 k_indexed_slots(const uint8_t *__restrict__ slots, uint32_t stride, uint64_t n, IndexedArgs a,
                 uint32_t *__restrict__ port_out, uint64_t *__restrict__ permit_out) {
-    if (TM == kTabLds || TM == kTabSplit || TM == kTabSplit1) stage_table(a);
+    if (TM == kTabLds || TM == kTabSplit) stage_table(a);
     const uint32_t lane = lane_id();
     const uint32_t wpb = blockDim.x >> 6;
     const uint64_t wave0 = uint64_t(blockIdx.x) * wpb + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -780,7 +826,7 @@ k_indexed_slots(const uint8_t *__restrict__ slots, uint32_t stride, uint64_t n, 
         Fields f;
         parse_fields(cur, live, f, [&](uint32_t k, uint32_t &lo, uint32_t &hi) {
             far_dwords(pkt, stride, k, lo, hi);
-        }, a.flags & NFFACL_PARSE_VLAN);
+        }, a.flags);
         const uint32_t res = classify_any<NS, TM>(a, f);
         if (live && port_out) port_out[idx] = res;
         if (permit_out) {
@@ -799,53 +845,68 @@ template <int NS, int TM>
 __global__ void __launch_bounds__(1024)
 k_indexed_frames(const uint8_t *__restrict__ frames, const uint64_t *__restrict__ desc, uint64_t n,
                  IndexedArgs a, uint32_t *__restrict__ port_out, uint64_t *__restrict__ permit_out) {
-    if (TM == kTabLds || TM == kTabSplit || TM == kTabSplit1) stage_table(a);
-    // Software pipeline.  Always: the next batch's descriptors load while this
-    // batch is classified (the frame load depends on them).  PF (per-lane
-    // HYBRID walks, whose LDS directories hold the CU to 16 waves and so leave
-    // VGPRs to spare): also the next batch's 64-byte frame lines, and the
-    // descriptors of the batch after.
-    constexpr bool PF = TM == kTabSplit || TM == kTabSplit1;
-    uint64_t ds_n1 = 0;  // descriptor of this lane's packet in the next batch
-    uint64_t ds_n2 = 0;  // PF: ... in the batch after
-    uint32_t f_n1[16];   // PF: first 64 bytes of the next batch's packet
-    bool first = true;
-    NFFACL_WAVE_LOOP(n) {
-        const uint64_t idx = base + lane;
-        const bool live = idx < n;
-        const uint64_t S = nwaves * 64;
-        uint64_t ds;
-        uint32_t d[16];
-        if (first) {
-            ds = live ? desc[idx] : 0;
-            load16(frames + (ds >> 16), d);
-            ds_n1 = idx + S < n ? desc[idx + S] : 0;
-            if (PF) {
-                if (base + S < n) load16(frames + (ds_n1 >> 16), f_n1);
-                ds_n2 = idx + 2 * S < n ? desc[idx + 2 * S] : 0;
-            }
-        } else if (PF) {
-            ds = ds_n1;
-#pragma unroll
-            for (int k = 0; k < 16; ++k) d[k] = f_n1[k];
-            ds_n1 = ds_n2;
-            if (base + S < n) load16(frames + (ds_n1 >> 16), f_n1);
-            ds_n2 = idx + 2 * S < n ? desc[idx + 2 * S] : 0;
-        } else {
-            ds = ds_n1;
-            load16(frames + (ds >> 16), d);
-            ds_n1 = idx + S < n ? desc[idx + S] : 0;
-        }
-        first = false;
+    if (TM == kTabLds || TM == kTabSplit) stage_table(a);
+    const uint32_t lane = lane_id();
+    const uint32_t wpb = blockDim.x >> 6;
+    const uint64_t S = uint64_t(gridDim.x) * wpb * 64;  // grid stride in packets
+    uint64_t base = (uint64_t(blockIdx.x) * wpb + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) * 64;
+    if (base >= n) return;
+    auto desc_at = [&](uint64_t b) -> uint64_t { return b + lane < n ? desc[b + lane] : 0; };
+    // classify the batch at b whose descriptor is ds and first 64 bytes d
+    auto classify_batch = [&](uint64_t b, uint64_t ds, uint32_t(&d)[16]) {
+        const bool live = b + lane < n;
         const uint32_t len = static_cast<uint32_t>(ds & 0xFFFFu);
         const uint8_t *pkt = frames + (ds >> 16);
-        clip16(d, len);
+        // bytes past the frame read as 0; IMIX frames are all >= 64 bytes, so
+        // the clip is skipped unless some lane of the wave holds a shorter one
+        if (ballot(live && len < 64u)) clip16(d, len);
         Fields f;
         parse_fields(d, live, f, [&](uint32_t k, uint32_t &lo, uint32_t &hi) {
             far_dwords(pkt, len, k, lo, hi);
-        }, a.flags & NFFACL_PARSE_VLAN);
+        }, a.flags);
         const uint32_t res = classify_any<NS, TM>(a, f);
-        store_verdicts(base, lane, live, res, port_out, permit_out);
+        store_verdicts(b, lane, live, res, port_out, permit_out);
+    };
+    // Software pipeline.  Always: the next batch's descriptors load while this
+    // batch is classified (the frame load depends on them).  PF (per-lane
+    // HYBRID walks, whose LDS directories hold the CU to 16 waves and so leave
+    // VGPRs to spare): also the next batch's 64-byte frame lines, into the
+    // other of two register buffers (ping-pong, no copies), and the
+    // descriptors of the batch after.
+    constexpr bool PF = TM == kTabSplit;
+    if (PF) {
+        uint32_t A[16], B[16];
+        uint64_t dsA = desc_at(base), dsB = 0;
+        load16(frames + (dsA >> 16), A);
+        uint64_t dsN = desc_at(base + S);  // descriptor of the batch after the one in flight
+        while (true) {
+            const uint64_t b1 = base + S;
+            if (b1 < n) {
+                dsB = dsN;
+                load16(frames + (dsB >> 16), B);
+                dsN = desc_at(b1 + S);
+            }
+            classify_batch(base, dsA, A);
+            if (b1 >= n) break;
+            const uint64_t b2 = b1 + S;
+            if (b2 < n) {
+                dsA = dsN;
+                load16(frames + (dsA >> 16), A);
+                dsN = desc_at(b2 + S);
+            }
+            classify_batch(b1, dsB, B);
+            if (b2 >= n) break;
+            base = b2;
+        }
+    } else {
+        uint64_t ds_next = desc_at(base);
+        for (; base < n; base += S) {
+            const uint64_t ds = ds_next;
+            ds_next = desc_at(base + S);
+            uint32_t d[16];
+            load16(frames + (ds >> 16), d);
+            classify_batch(base, ds, d);
+        }
     }
 }
 
@@ -901,7 +962,7 @@ static dev::IndexedArgs indexed_args(const DevTable *t) {
     auto fam = [&](const FamilyIndex &fi, uint32_t off_cold, dev::FamArgs &fa) {
         for (uint32_t k = 0; k < 4; ++k) {
             const DimInfo &d = fi.dims[k];
-            fa.slot[k] = dev::SlotArgs{d.shift, d.off_dir, d.off_ent, 0};
+            fa.slot[k] = dev::SlotArgs{d.shift, d.off_dir, d.off_ent, d.off_dir16};
         }
         fa.off_resid = fi.off_resid;
         fa.n_resid = fi.n_resid;
@@ -959,8 +1020,8 @@ static IndexedLaunch indexed_launch(const DevTable *t) {
         return L;
     }
     if (t->meta.algo == NFFACL_ALGO_HYBRID) {
-        L.tm = tune_env("NFFACL_TUNE_UNROLL", 1) == 2 ? dev::kTabSplit : dev::kTabSplit1;
         staged = size_t(t->meta.lds_dwords) * sizeof(uint32_t);
+        L.tm = dev::kTabSplit;
     } else {
         const size_t bytes = t->meta.blob.size() * sizeof(uint32_t);
         if (bytes <= kLdsTableBytes && tune_env("NFFACL_TUNE_LDS", 1) != 0) {
@@ -970,7 +1031,10 @@ static IndexedLaunch indexed_launch(const DevTable *t) {
     }
     if (L.tm != dev::kTabGlobal) {
         L.block = 1024u;
-        L.per_cu = static_cast<uint32_t>(std::max<size_t>(1, std::min<size_t>(2, kLdsBytes / std::max<size_t>(staged, 16))));
+        // lane form: one workgroup per CU (its VGPRs allow no second one)
+        L.per_cu = L.tm == dev::kTabSplit
+                       ? 1u
+                       : static_cast<uint32_t>(std::max<size_t>(1, std::min<size_t>(2, kLdsBytes / std::max<size_t>(staged, 16))));
         L.lds_bytes = std::max<size_t>(staged, 16);
     }
     L.block = static_cast<uint32_t>(tune_env("NFFACL_TUNE_BLOCK", static_cast<int>(L.block)));
@@ -1010,7 +1074,6 @@ static void dispatch_indexed(int ns, int tm, F &&f) {
         switch (tm) {
         case dev::kTabLds: f(nsc, std::integral_constant<int, dev::kTabLds>{}); break;
         case dev::kTabSplit: f(nsc, std::integral_constant<int, dev::kTabSplit>{}); break;
-        case dev::kTabSplit1: f(nsc, std::integral_constant<int, dev::kTabSplit1>{}); break;
         case dev::kTabFlat: f(nsc, std::integral_constant<int, dev::kTabFlat>{}); break;
         case dev::kTabFlat4: f(nsc, std::integral_constant<int, dev::kTabFlat4>{}); break;
         default: f(nsc, std::integral_constant<int, dev::kTabGlobal>{}); break;
@@ -1026,7 +1089,7 @@ int prepare_kernels() {
     static hipError_t err = hipSuccess;
     std::call_once(once, [] {
         for (int ns = 2; ns <= 4; ++ns)
-            for (int tm : {int(dev::kTabLds), int(dev::kTabSplit), int(dev::kTabSplit1)})
+            for (int tm : {int(dev::kTabLds), int(dev::kTabSplit)})
                 dispatch_indexed(ns, tm, [&](auto nsc, auto tmc) {
                     const hipError_t e = allow_lds_modes<decltype(nsc)::value, decltype(tmc)::value>();
                     if (e != hipSuccess) err = e;

@@ -64,30 +64,33 @@ constexpr uint32_t kMaxIndexedRules = 1u << 23;
 
 // ---- hybrid table (tables whose inline index outgrows LDS) ---------------
 //
-// Same slot assignment and ascending bucket lists as the indexed table, but
-//  * the eight directories (both families) come first in the blob; their
-//    values are absolute entry numbers (16-byte units of the blob).  Either
-//    they are the only part staged in LDS (radix widths chosen to fit
-//    kHybLaneDirBytes; each lane walks its lists), or — when that leaves more
-//    than kHybFlatCandidates expected candidates per packet — they are sized
-//    to kHybFlatDirBytes and read from global memory, and a wave tests its
-//    packets' candidates 64 at a time (lds_dwords = 0 marks this form);
-//  * a list entry is 16 bytes, everything the common test needs:
+// Same slot assignment and ascending bucket lists as the indexed table, with
+// the eight directories (both families) first in the blob, in one of two forms:
+//  * lane form (lds_dwords > 0): the directories, radix widths chosen to fit
+//    kHybLaneDirBytes, are the LDS image — two-level (kDir16GroupShift) when
+//    every group fits u16 offsets; the lists hold INDEXED's inline entries
+//    (directory values relative to the slot's entries, as above) read from
+//    global memory, each lane walking its own lists;
+//  * flat form (lds_dwords == 0) — when LDS-sized directories leave more than
+//    kHybFlatCandidates expected candidates per packet: plain u32 directories
+//    sized to kHybFlatDirBytes, read from global memory, values = absolute
+//    entry numbers (16-byte units of the blob); a wave tests its packets'
+//    candidates 64 at a time, and a list entry is 16 compact bytes:
 //      [0] src word, big-endian value (IPv6: top 32 bits)
 //      [1] dst word, big-endian value
 //      [2] meta = id | exact << 8 | rule_index << 9          (as inline)
-//      [3] src_len | dst_len << 6 | cold << 12 | sport_blocks << 16 | dport_blocks << 24
-//    with prefix lengths (IPv6: capped at 32) and 8-bit port-block bitmaps
-//    (bit b: the rule's range meets ports [8192 b, 8192 b + 8191]);
-//  * cold records, one per rule in rule order, hold what the entry cannot:
+//      [3] src_len | dst_len << 6 | cold << 12 | out << 13 | sport_blocks << 16 | dport_blocks << 24
+//    with prefix lengths (IPv6: capped at 32), the output number when < 7
+//    (7: read it from the cold record) and 8-bit port-block bitmaps (bit b:
+//    the rule's range meets ports [8192 b, 8192 b + 8191]); cold records,
+//    one per rule in rule order, hold what the entry cannot:
 //      IPv4 (4 dwords): lo, hi, output_number, 0
 //      IPv6 (16 dwords): lo, hi, output_number, 0, then the 12 extension words
 //      of the inline entry (src[1..3], src_mask[1..3], dst[1..3], dst_mask[1..3]).
 //    An entry with the cold bit (port ranges not made of whole blocks, IPv6
-//    prefixes longer than 32) is confirmed against its cold record; the
-//    winner's output number is read from its cold record at the end.
-// Only CIDR masks and id_mask in {0, 0xff} are encodable (what the parsers
-// produce); other rule sets compile INDEXED.
+//    prefixes longer than 32) is confirmed against its cold record.
+// The flat form encodes only CIDR masks and id_mask in {0, 0xff} (what the
+// parsers produce); other rule sets compile INDEXED.
 constexpr uint32_t kHybEntDwords = 4;
 constexpr uint32_t kHybCold = 1u << 12;
 constexpr uint32_t kHybOutShift = 13;
@@ -102,6 +105,11 @@ constexpr uint32_t kHybCold6Dwords = 16;
 constexpr size_t kHybLaneDirBytes = 128 * 1024;
 constexpr size_t kHybFlatDirBytes = 1024 * 1024;
 constexpr double kHybFlatCandidates = 6.0;
+// Lane-form directories are two-level: a u32 base per group of 64 buckets +
+// a u16 offset per bucket (2.06 B per bucket instead of 4), so the LDS budget
+// holds twice the buckets.  A group whose lists exceed 65535 entries keeps
+// the whole table on plain u32 directories.
+constexpr uint32_t kDir16GroupShift = 6;
 // Largest table staged whole in LDS (gfx950: 160 KiB per CU, 1 KiB headroom).
 constexpr size_t kLdsTableBytes = 159 * 1024;
 

@@ -18,7 +18,7 @@ from oracle import oracle, rules_oracle as ro
 class DimInfo(ctypes.Structure):
     _fields_ = [("kind", ctypes.c_uint32), ("shift", ctypes.c_uint32), ("n_buckets", ctypes.c_uint32),
                 ("off_dir", ctypes.c_uint32), ("off_entries", ctypes.c_uint32), ("n_rules", ctypes.c_uint32),
-                ("max_list", ctypes.c_uint32), ("reserved", ctypes.c_uint32), ("n_entries", ctypes.c_uint64)]
+                ("max_list", ctypes.c_uint32), ("off_dir16", ctypes.c_uint32), ("n_entries", ctypes.c_uint64)]
 
 
 class FamInfo(ctypes.Structure):
@@ -87,6 +87,19 @@ KEYS = {0: lambda F: bswap(F["s"][0]), 1: lambda F: bswap(F["t"][0]), 2: lambda 
         3: lambda F: bswap(F["t"][0]), 4: lambda F: F["sp"], 5: lambda F: F["dp"]}
 
 
+def dir_values(blob, di):
+    """dir[0..n_buckets] of a slot: plain u32, or two-level (table.hpp:
+    dir[t] = base[t >> 6] + u16 dir16[t])."""
+    nb = di.n_buckets
+    if di.off_dir16 == 0:
+        return blob[di.off_dir:di.off_dir + nb + 1].astype(np.int64)
+    t = np.arange(nb + 1)
+    base = blob[di.off_dir + (t >> 6)].astype(np.int64)
+    w = blob[di.off_dir16 + (t >> 1)].astype(np.int64)
+    rel = np.where(t & 1, w >> 16, w & 0xFFFF)
+    return base + rel
+
+
 def emulate(blob, info, F, n):
     best = np.full(n, 0xFFFFFFFF, np.uint64)
     outv = np.zeros(n, np.uint32)
@@ -99,7 +112,7 @@ def emulate(blob, info, F, n):
             if di.n_rules == 0:
                 continue
             key = KEYS[di.kind](F).astype(np.uint64)
-            dirv = blob[di.off_dir:di.off_dir + di.n_buckets + 1].astype(np.int64)
+            dirv = dir_values(blob, di)
             t = (key >> np.uint64(di.shift)).astype(np.int64)
             assert (t < di.n_buckets).all()
             start, end = dirv[t], dirv[t + 1]
@@ -141,7 +154,7 @@ def check(text: str, slots: np.ndarray, n: int):
         ew = fi.entry_dwords
         for d in range(4):
             di = fi.dims[d]
-            dirv = blob[di.off_dir:di.off_dir + di.n_buckets + 1].astype(np.int64)
+            dirv = dir_values(blob, di)
             assert dirv[0] == 0 and dirv[-1] == di.n_entries and (np.diff(dirv) >= 0).all()
             c = blob[di.off_entries + 4 + ew * np.arange(int(di.n_entries))].astype(np.int64) >> 9
             first = np.zeros(len(c), bool)
@@ -315,6 +328,16 @@ def test_hybrid_matches_oracle_synthetic(cfg):
     n = 1 << 15
     info = check_hybrid(g.text, synth.gen_slots(g, n, synth.PACKET_SEEDS[cfg]), n)
     assert 0 < info.lds_dwords * 4 <= 128 * 1024  # LDS directories, per-lane walks
+    assert info.fam[0].dims[0].off_dir16 != 0  # two-level (u16) directories
+
+
+def test_hybrid_lane_form_u32_directories(monkeypatch):
+    """NFFACL_TUNE_DIR16=0: the lane form with plain u32 directories."""
+    monkeypatch.setenv("NFFACL_TUNE_DIR16", "0")
+    g = synth.gen_rules(synth.SPECS["c3"], synth.RULE_SEEDS["c3"])
+    n = 1 << 14
+    info = check_hybrid(g.text, synth.gen_slots(g, n, 41), n)
+    assert info.lds_dwords > 0 and info.fam[0].dims[0].off_dir16 == 0
 
 
 def test_hybrid_small_directory_budget(monkeypatch):

@@ -2,7 +2,7 @@
 """Interleaved A/B timing of classify launch variants in one process
 (cdna_hip_programming.md §5.4 rule 24), with a bit-exactness check between
 variants.  Variants are NFFACL_TUNE_* environment settings read per launch.
-usage: python tools/ab.py [config] [rounds]"""
+usage: python tools/ab.py [config] [rounds] [variant set: load]"""
 import json
 import os
 import sys
@@ -19,14 +19,17 @@ from nffacl import synth  # noqa: E402
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "c2"
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 10
-VARIANTS = {
-    "rows": {"NFFACL_TUNE_COAL": "0"},
-    "coal_nt": {"NFFACL_TUNE_COAL": "2"},
-    "rowswap_nt": {"NFFACL_TUNE_COAL": "4"},
-    # speed-of-light kernels of tools/sol.hip on the same buffer (no classify):
-    "sol_coalesced_nt": {"SOL": "3"},
-    "sol_rows": {"SOL": "1"},
+VARIANT_SETS = {
+    "load": {
+        "rows": {"NFFACL_TUNE_COAL": "0"},
+        "coal_nt": {"NFFACL_TUNE_COAL": "2"},
+        "rowswap_nt": {"NFFACL_TUNE_COAL": "4"},
+        # speed-of-light kernels of tools/sol.hip on the same buffer (no classify):
+        "sol_coalesced_nt": {"SOL": "3"},
+        "sol_rows": {"SOL": "1"},
+    },
 }
+VARIANTS = VARIANT_SETS[sys.argv[3] if len(sys.argv) > 3 else "load"]
 n = 1 << 24
 if cfg == "c1":
     text = (ROOT / "tests/golden/rules/firewall.conf").read_text()

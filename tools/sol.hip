@@ -8,6 +8,9 @@
 //   coal     : lane-contiguous 16 B loads (1 KiB per wave instruction), then
 //              each packet's dword 3 gathered with ds_bpermute
 //   copy     : plain float4 copy n*64 bytes -> n*64 bytes (HBM reference)
+//   frames   : packed IMIX frames: per lane its u64 descriptor, then the
+//              frame's first 64 bytes (classify_frames' pattern); frames_pf
+//              loads the next batch's descriptors + frame lines ahead
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -94,6 +97,38 @@ __global__ void __launch_bounds__(1024) k_coal(const uint8_t *s, uint64_t n, uin
     }
 }
 
+template <bool PF>
+__global__ void __launch_bounds__(1024) k_frames(const uint8_t *fr, const uint64_t *desc, uint64_t n, uint32_t *port,
+                                                 uint64_t *bits) {
+    const uint32_t lane = lane_id();
+    const uint64_t wave0 = uint64_t(blockIdx.x) * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t step = uint64_t(gridDim.x) * (blockDim.x >> 6) * 64;
+    uint32_t nd[16];
+    uint64_t nds = 0;
+    bool first = true;
+    for (uint64_t base = wave0 * 64; base < n; base += step) {
+        const uint64_t i = base + lane;
+        uint32_t d[16];
+        if (!PF || first) {
+            const uint64_t ds = i < n ? desc[i] : 0;
+            ld16<false>(fr + (ds >> 16), d);
+            if (PF) nds = i + step < n ? desc[i + step] : 0;
+        } else {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) d[k] = nd[k];
+        }
+        if (PF) {
+            if (base + step < n) ld16<false>(fr + (nds >> 16), nd);
+            nds = i + 2 * step < n ? desc[i + 2 * step] : 0;
+        }
+        first = false;
+        const uint32_t r = fold(d);
+        if (i < n) port[i] = r;
+        const uint64_t b = __builtin_amdgcn_ballot_w64(i < n && (r & 1));
+        if (lane == 0) bits[base >> 6] = b;
+    }
+}
+
 __global__ void __launch_bounds__(256) k_copy(const u32x4 *a, u32x4 *b, uint64_t n16) {
     for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n16; i += uint64_t(gridDim.x) * blockDim.x)
         b[i] = __builtin_nontemporal_load(a + i);
@@ -115,6 +150,8 @@ extern "C" int sol_run(int which, const void *slots, uint64_t n, void *port, voi
     case 3: hipLaunchKernelGGL(k_coal, g, b, 0, st, s, n, p, bb); break;
     case 4: hipLaunchKernelGGL(k_copy, g, b, 0, st, reinterpret_cast<const u32x4 *>(slots),
                                static_cast<u32x4 *>(scratch), n * 4); break;
+    case 5: hipLaunchKernelGGL(k_frames<false>, g, b, 0, st, s, static_cast<const uint64_t *>(scratch), n, p, bb); break;
+    case 6: hipLaunchKernelGGL(k_frames<true>, g, b, 0, st, s, static_cast<const uint64_t *>(scratch), n, p, bb); break;
     default: return -1;
     }
     return hipGetLastError() == hipSuccess ? 0 : -2;
