@@ -151,11 +151,19 @@ namespace dev {
 
 extern __shared__ __attribute__((aligned(16))) uint32_t l2_lds[];
 
+// Packed shape descriptor: kind = EtherType mask | kL2PkDst | kL2PkSrc (MAC
+// masks are whole addresses or nothing, acl.go:478-491); key records follow
+// the (cap_mask + 1) buckets.
+struct L2Packed {
+    uint32_t kind, off, cap_mask, first;
+};
+constexpr uint32_t kL2PkDst = 1u << 16, kL2PkSrc = 1u << 17;
+
 struct L2Args {
     const uint32_t *tab;
     uint32_t tab_dwords;
     uint32_t n;  // LINEAR: records; HASH: shapes
-    L2Shape shapes[kL2MaxShapes];
+    L2Packed pk[kL2MaxShapes];
 };
 
 __device__ __forceinline__ uint32_t classify_l2_linear(const uint32_t (&p)[4], bool live,
@@ -227,12 +235,37 @@ __device__ __forceinline__ void l2_lookup(const L2Shape &S, const uint32_t (&p)[
     }
 }
 
+// Shape s rebuilt from its packed descriptor (L2Args::pk).  The empty
+// volatile asm keeps the rebuild inside the batch loop: hoisted for all
+// eight shapes the masks would not fit the SGPR budget of eight waves per
+// SIMD, while the packed words (4 SGPRs per shape) do.
+__device__ __forceinline__ L2Shape unpack_shape(const L2Args &a, int s) {
+    uint32_t k = a.pk[s].kind, off = a.pk[s].off, cap = a.pk[s].cap_mask, first = a.pk[s].first;
+    asm volatile("" : "+s"(k), "+s"(off), "+s"(cap), "+s"(first));
+    L2Shape S;
+    S.m[0] = (k & kL2PkDst) ? 0xFFFFFFFFu : 0u;
+    S.m[1] = ((k & kL2PkDst) ? 0x0000FFFFu : 0u) | ((k & kL2PkSrc) ? 0xFFFF0000u : 0u);
+    S.m[2] = (k & kL2PkSrc) ? 0xFFFFFFFFu : 0u;
+    S.m[3] = k & 0xFFFFu;
+    S.off = off;
+    S.cap_mask = cap;
+    S.first = first;
+    S.off_key = off + (cap + 1u) * kL2BucketSlots;
+    return S;
+}
+
+// Shapes in ascending order of their first rule; a shape is skipped once
+// every lane's match precedes it.  Unrolled with constant shape indices, so
+// the descriptors are loaded into SGPRs once per kernel instead of by two
+// scalar loads per shape and batch (each of which stalled the following LDS
+// wait: lgkmcnt counts both).
 template <bool LDS>
 __device__ __forceinline__ uint32_t classify_l2_hash(const uint32_t (&p)[4], bool live, const L2Args &a) {
     uint32_t best = 0xFFFFFFFFu, res = 0;
-#pragma unroll 1
-    for (uint32_t s = 0; s < a.n; ++s) {  // shape fields: scalar loads from the kernel arguments
-        const L2Shape S = a.shapes[s];
+#pragma unroll
+    for (int s = 0; s < int(kL2MaxShapes); ++s) {
+        if (s >= a.n) break;
+        const L2Shape S = unpack_shape(a, s);
         const bool go = live && S.first < best;  // shapes ascend by first rule index
         if (!ballot(go)) break;
         l2_lookup<LDS>(S, p, go, a.tab, best, res);
@@ -263,10 +296,21 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8)
 k_l2_slots(const uint8_t *__restrict__ slots, uint32_t stride, uint64_t n, L2Args a,
            uint32_t *__restrict__ port_out, uint64_t *__restrict__ permit_out) {
     l2_stage<LDS>(a);
-    NFFACL_WAVE_LOOP(n) {
-        const uint64_t idx = base + lane;
-        const bool live = idx < n;
-        const u32x4 v = *reinterpret_cast<const u32x4 *>(slots + (live ? idx : 0) * stride);
+    // grid-stride over 64-packet batches; the next batch's header line is
+    // loaded while this one is classified (+10 % at 256 rules,
+    // profiles/r1_l2_v3)
+    const uint32_t lane = lane_id();
+    const uint32_t wpb = blockDim.x >> 6;
+    const uint64_t step = uint64_t(gridDim.x) * wpb * 64;
+    uint64_t base = (uint64_t(blockIdx.x) * wpb + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) * 64;
+    auto header = [&](uint64_t b) {
+        return *reinterpret_cast<const u32x4 *>(slots + (b + lane < n ? b + lane : 0) * stride);
+    };
+    u32x4 nv = base < n ? header(base) : u32x4{0, 0, 0, 0};
+    for (; base < n; base += step) {
+        const u32x4 v = nv;
+        if (base + step < n) nv = header(base + step);
+        const bool live = base + lane < n;
         const uint32_t p[4] = {v.x, v.y, v.z, v.w};
         store_verdicts(base, lane, live, classify_l2<ALGO, LDS>(p, live, a), port_out, permit_out);
     }
@@ -308,7 +352,11 @@ L2Launch l2_plan(const nffacl_l2engine *eng, const L2Table *t, uint64_t n) {
     L.a.tab_dwords = static_cast<uint32_t>(t->meta.blob.size());
     const bool hash = t->meta.algo == NFFACL_ALGO_INDEXED;
     L.a.n = hash ? t->meta.n_shapes : t->meta.n_rules;
-    std::copy(t->meta.shapes, t->meta.shapes + kL2MaxShapes, L.a.shapes);
+    for (uint32_t s = 0; s < kL2MaxShapes; ++s) {
+        const L2Shape &S = t->meta.shapes[s];
+        L.a.pk[s] = dev::L2Packed{(S.m[3] & 0xFFFFu) | (S.m[0] ? dev::kL2PkDst : 0u) | (S.m[2] ? dev::kL2PkSrc : 0u),
+                                  S.off, S.cap_mask, S.first};
+    }
     L.lds_bytes = t->meta.blob.size() * sizeof(uint32_t);
     L.lds = hash && L.lds_bytes <= kL2LdsMax;
     L.block = L.lds ? 1024 : 256;
