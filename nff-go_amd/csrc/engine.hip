@@ -389,7 +389,6 @@ __device__ __forceinline__ void bounds32(const T &tab, uint32_t dir, uint32_t t,
 }
 
 struct LdsTab {
-    static constexpr bool kMaskedLoads = false;
     __device__ __forceinline__ uint32_t ld(uint32_t i) const { return lds_tab[i]; }
     __device__ __forceinline__ void bounds(uint32_t dir, uint32_t, uint32_t t, uint32_t &lo, uint32_t &hi) const {
         bounds32(*this, dir, t, lo, hi);
@@ -399,7 +398,6 @@ struct LdsTab {
     }
 };
 struct GlobalTab {
-    static constexpr bool kMaskedLoads = true;
     const uint32_t *__restrict__ p;
     __device__ __forceinline__ uint32_t ld(uint32_t i) const { return p[i]; }
     __device__ __forceinline__ void bounds(uint32_t dir, uint32_t, uint32_t t, uint32_t &lo, uint32_t &hi) const {
@@ -411,7 +409,6 @@ struct GlobalTab {
 };
 // HYBRID lane form: directories (ld) staged in LDS, entries (ld4) global.
 struct SplitTab {
-    static constexpr bool kMaskedLoads = true;
     const uint32_t *__restrict__ p;
     __device__ __forceinline__ uint32_t ld(uint32_t i) const { return lds_tab[i]; }
     // two-level directory (table.hpp): dir[t] = base[t >> 6] + dir16[t]
@@ -489,17 +486,12 @@ __device__ __forceinline__ uint32_t classify_indexed(const T &tab, const Indexed
         for (int s = 0; s < NS; ++s)
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                if constexpr (T::kMaskedLoads) {
-                    // global entries: only lanes still walking this list load
-                    // (a 16-byte load costs the TA 16 cycles per 64 active lanes)
-                    A[s][u] = B[s][u] = u32x4{0, 0, 0, 0};
-                    if (c[s] + u < e[s]) {
-                        const uint32_t off = base[s] + (c[s] + u) * ew;
-                        A[s][u] = tab.ld4(off);
-                        B[s][u] = tab.ld4(off + 4);
-                    }
-                } else {
-                    const uint32_t off = base[s] + (c[s] + u < e[s] ? c[s] + u : 0u) * ew;
+                // only lanes still walking this list load (a 16-byte load
+                // costs the TA 16 cycles per 64 active lanes; LDS: -1.3 % on
+                // C2, global: -4 % on C3, profiles/r1_masked)
+                A[s][u] = B[s][u] = u32x4{0, 0, 0, 0};
+                if (c[s] + u < e[s]) {
+                    const uint32_t off = base[s] + (c[s] + u) * ew;
                     A[s][u] = tab.ld4(off);
                     B[s][u] = tab.ld4(off + 4);
                 }
