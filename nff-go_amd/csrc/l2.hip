@@ -6,14 +6,16 @@
 //  * LINEAR: records are wave-uniform and stream through the scalar data
 //    cache; a ballot of still-undecided lanes ends the scan at the wave's
 //    last first-match (the reference's `return rule.OutputNumber`).
-//  * HASH: per rule shape one hashed probe (see l2.hpp); tables staged in LDS
-//    per workgroup when they fit, read through L1/L2 otherwise.
+//  * HASH: per rule shape both slots of a two-choice cuckoo table (see
+//    l2.hpp); tables staged in LDS per workgroup when they fit, read through
+//    L1/L2 otherwise.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <array>
 #include <cstring>
 #include <map>
+#include <set>
 #include <string>
 
 #include "devutil.hpp"
@@ -49,6 +51,79 @@ Masked masked_rule(const nffacl_l2_rule &r) {
     return x;
 }
 
+// Per shape a two-choice cuckoo table at load <= 1/4 (one 16-byte slot per
+// key: k0, k1, k2, k3 | rule index << 16).  Keys enter in ascending rule
+// index, so the first owner of a key keeps it and later duplicates (shadowed
+// rules) are dropped.  False if some key set cannot be placed within
+// 8x its size (never seen; AUTO then compiles LINEAR).
+bool build_cuckoo(const std::vector<Masked> &rules, const std::vector<nffacl_l2_rule> &eth,
+                  const std::vector<std::array<uint32_t, 4>> &shapes,
+                  const std::vector<std::vector<uint32_t>> &members, L2Compiled &c) {
+    c.algo = NFFACL_ALGO_INDEXED;
+    c.n_shapes = static_cast<uint32_t>(shapes.size());
+    c.n_rules = static_cast<uint32_t>(rules.size());
+    struct Slot {
+        std::array<uint32_t, 4> k;
+        uint32_t idx = kL2NoRule;
+    };
+    for (uint32_t s = 0; s < shapes.size(); ++s) {
+        std::vector<uint32_t> keys;  // first owner of every distinct key, ascending
+        {
+            std::set<std::array<uint32_t, 4>> seen;
+            for (uint32_t i : members[s])
+                if (seen.insert(rules[i].v).second) keys.push_back(i);
+        }
+        uint32_t cap = 4;
+        while (cap < 4 * keys.size()) cap <<= 1;
+        std::vector<Slot> tab;
+        bool placed_all = false;
+        for (; !placed_all && cap <= 32 * std::max<size_t>(keys.size(), 4); cap <<= 1) {
+            tab.assign(cap, Slot{});
+            placed_all = true;
+            for (uint32_t i : keys) {
+                Slot cur{rules[i].v, i};
+                uint32_t last = 0xFFFFFFFFu;  // the slot `cur` was just evicted from
+                bool done = false;
+                for (int kick = 0; kick < 500 && !done; ++kick) {
+                    const uint32_t h = l2_hash(cur.k[0], cur.k[1], cur.k[2], cur.k[3]);
+                    const uint32_t a0 = h & (cap - 1), a1 = l2_hash_alt(h) & (cap - 1);
+                    if (tab[a0].idx == kL2NoRule) {
+                        tab[a0] = cur;
+                        done = true;
+                    } else if (tab[a1].idx == kL2NoRule) {
+                        tab[a1] = cur;
+                        done = true;
+                    } else {  // evict an occupant; it moves on to its other slot
+                        const uint32_t victim = a0 == last ? a1 : a0;
+                        std::swap(cur, tab[victim]);
+                        last = victim;
+                    }
+                }
+                if (!done) {
+                    placed_all = false;
+                    break;
+                }
+            }
+        }
+        if (!placed_all) return false;
+        cap = static_cast<uint32_t>(tab.size());
+        L2Shape &S = c.shapes[s];
+        std::copy(shapes[s].begin(), shapes[s].end(), S.m);
+        S.off = static_cast<uint32_t>(c.blob.size());
+        S.cap_mask = cap - 1;
+        for (const Slot &x : tab) {
+            const uint32_t w[4] = {x.idx == kL2NoRule ? 0u : x.k[0], x.idx == kL2NoRule ? 0u : x.k[1],
+                                   x.idx == kL2NoRule ? 0u : x.k[2],
+                                   (x.idx == kL2NoRule ? 0u : x.k[3]) | (x.idx << 16)};
+            c.blob.insert(c.blob.end(), w, w + 4);
+        }
+    }
+    c.off_out = static_cast<uint32_t>(c.blob.size());
+    for (uint32_t i = 0; i < rules.size(); ++i) c.blob.push_back(eth[i].output_number);
+    while (c.blob.size() % 4) c.blob.push_back(0);
+    return true;
+}
+
 }  // namespace
 
 L2Compiled compile_l2(const std::vector<nffacl_l2_rule> &eth, int algo) {
@@ -71,8 +146,10 @@ L2Compiled compile_l2(const std::vector<nffacl_l2_rule> &eth, int algo) {
         }
         members[it - shapes.begin()].push_back(i);
     }
-    const bool hash = algo != NFFACL_ALGO_LINEAR && shapes.size() <= kL2MaxShapes;
+    const bool hash = algo != NFFACL_ALGO_LINEAR && shapes.size() <= kL2MaxShapes && rules.size() < kL2NoRule &&
+                      build_cuckoo(rules, eth, shapes, members, c);
     if (!hash) {
+        c = L2Compiled{};
         c.algo = NFFACL_ALGO_LINEAR;
         for (uint32_t i = 0; i < rules.size(); ++i) {
             const Masked &x = rules[i];
@@ -80,47 +157,6 @@ L2Compiled compile_l2(const std::vector<nffacl_l2_rule> &eth, int algo) {
                                               x.m[0], x.m[1], x.m[2], eth[i].output_number};
             c.blob.insert(c.blob.end(), w, w + kL2RecDwords);
         }
-        c.n_rules = static_cast<uint32_t>(rules.size());
-    } else {
-        c.algo = NFFACL_ALGO_INDEXED;
-        c.n_shapes = static_cast<uint32_t>(shapes.size());
-        for (uint32_t s = 0; s < shapes.size(); ++s) {
-            uint32_t buckets = 1;  // four slots each, at most half full
-            while (buckets * kL2BucketSlots < 2 * members[s].size()) buckets <<= 1;
-            const uint32_t slots = buckets * kL2BucketSlots;
-            L2Shape &S = c.shapes[s];
-            std::copy(shapes[s].begin(), shapes[s].end(), S.m);
-            S.off = static_cast<uint32_t>(c.blob.size());
-            S.off_key = S.off + slots;
-            S.cap_mask = buckets - 1;
-            S.first = members[s].front();
-            c.blob.resize(c.blob.size() + size_t(slots) * (1 + kL2KeyDwords), 0);
-            for (uint32_t i : members[s]) {  // ascending rule index: the first key owner wins
-                const auto &v = rules[i].v;
-                const uint32_t hv = l2_hash(v[0], v[1], v[2], v[3]);
-                uint32_t bkt = hv & S.cap_mask;
-                bool placed = false;
-                while (!placed) {
-                    for (uint32_t j = 0; j < kL2BucketSlots && !placed; ++j) {
-                        const uint32_t slot = bkt * kL2BucketSlots + j;
-                        uint32_t *fp = &c.blob[S.off + slot];
-                        uint32_t *kr = &c.blob[S.off_key + size_t(slot) * kL2KeyDwords];
-                        if (*fp == 0) {
-                            *fp = hv | 1u;
-                            kr[0] = v[0]; kr[1] = v[1]; kr[2] = v[2]; kr[3] = v[3];
-                            kr[4] = i;
-                            kr[5] = eth[i].output_number;
-                            placed = true;
-                        } else if (kr[0] == v[0] && kr[1] == v[1] && kr[2] == v[2] && kr[3] == v[3]) {
-                            placed = true;  // shadowed by an earlier rule with the same key
-                        }
-                    }
-                    bkt = (bkt + 1) & S.cap_mask;
-                }
-            }
-        }
-        std::sort(c.shapes, c.shapes + c.n_shapes,
-                  [](const L2Shape &a, const L2Shape &b) { return a.first < b.first; });
         c.n_rules = static_cast<uint32_t>(rules.size());
     }
     if (c.blob.empty()) c.blob.assign(kL2RecDwords, 0);  // keep a valid allocation
@@ -152,17 +188,17 @@ namespace dev {
 extern __shared__ __attribute__((aligned(16))) uint32_t l2_lds[];
 
 // Packed shape descriptor: kind = EtherType mask | kL2PkDst | kL2PkSrc (MAC
-// masks are whole addresses or nothing, acl.go:478-491); key records follow
-// the (cap_mask + 1) buckets.
+// masks are whole addresses or nothing, acl.go:478-491).
 struct L2Packed {
-    uint32_t kind, off, cap_mask, first;
+    uint32_t kind, off, cap_mask;
 };
 constexpr uint32_t kL2PkDst = 1u << 16, kL2PkSrc = 1u << 17;
 
 struct L2Args {
     const uint32_t *tab;
     uint32_t tab_dwords;
-    uint32_t n;  // LINEAR: records; HASH: shapes
+    uint32_t n;        // LINEAR: records; HASH: shapes
+    uint32_t off_out;  // HASH: OutputNumber per rule
     L2Packed pk[kL2MaxShapes];
 };
 
@@ -183,94 +219,57 @@ __device__ __forceinline__ uint32_t classify_l2_linear(const uint32_t (&p)[4], b
     return res;
 }
 
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-
-// i: dword index, a multiple of 4 (ld4) / 2 (ld2) — indexed in vector units
-// so the compiler emits one ds_read_b128 / ds_read_b64
+// i: dword index, a multiple of 4 (ld4) — indexed in vector units so the
+// compiler emits one ds_read_b128
 template <bool LDS>
 __device__ __forceinline__ u32x4 l2_ld4(const uint32_t *__restrict__ g, uint32_t i) {
     return LDS ? reinterpret_cast<const u32x4 *>(l2_lds)[i >> 2] : reinterpret_cast<const u32x4 *>(g)[i >> 2];
-}
-template <bool LDS>
-__device__ __forceinline__ u32x2 l2_ld2(const uint32_t *__restrict__ g, uint32_t i) {
-    return LDS ? reinterpret_cast<const u32x2 *>(l2_lds)[i >> 1] : reinterpret_cast<const u32x2 *>(g)[i >> 1];
 }
 template <bool LDS>
 __device__ __forceinline__ uint32_t l2_ld1(const uint32_t *__restrict__ g, uint32_t i) {
     return LDS ? l2_lds[i] : g[i];
 }
 
-// Shape lookups: one 16-byte fingerprint-bucket read per shape; a key record
-// only on a fingerprint match; the next bucket only when this one is full and
-// missed (rare at load <= 1/2).  Inactive lanes read bucket 0 (a broadcast).
-template <bool LDS>
-__device__ __forceinline__ void l2_lookup(const L2Shape &S, const uint32_t (&p)[4], bool go, const uint32_t *tab,
-                                          uint32_t &best, uint32_t &res) {
-    const uint32_t k0 = p[0] & S.m[0], k1 = p[1] & S.m[1], k2 = p[2] & S.m[2], k3 = p[3] & S.m[3];
-    const uint32_t hv = l2_hash(k0, k1, k2, k3);
-    const uint32_t f = hv | 1u;
-    uint32_t bkt = go ? hv & S.cap_mask : 0u;
-    while (true) {
-        const u32x4 fp = l2_ld4<LDS>(tab, S.off + bkt * kL2BucketSlots);
-        uint32_t mm = go ? (uint32_t(fp.x == f) | uint32_t(fp.y == f) << 1 | uint32_t(fp.z == f) << 2 |
-                            uint32_t(fp.w == f) << 3)
-                         : 0u;
-        const bool has_free = (fp.x == 0u) | (fp.y == 0u) | (fp.z == 0u) | (fp.w == 0u);
-        bool hit = false;
-        while (ballot(mm != 0u)) {  // fingerprint matches (almost always one at most)
-            const uint32_t j = mm ? static_cast<uint32_t>(__builtin_ctz(mm)) : 0u;
-            const uint32_t at = S.off_key + (mm ? bkt * kL2BucketSlots + j : 0u) * kL2KeyDwords;
-            const u32x4 e = l2_ld4<LDS>(tab, at);
-            const bool eq = mm != 0u && ((e.x ^ k0) | (e.y ^ k1) | (e.z ^ k2) | (e.w ^ k3)) == 0u;
-            if (eq) {
-                const u32x2 io = l2_ld2<LDS>(tab, at + 4);  // rule index, OutputNumber
-                if (io.x < best) { best = io.x; res = io.y; }
-                hit = true;
-            }
-            mm = eq ? 0u : (mm & (mm - 1u));
-        }
-        go = go && !hit && !has_free;
-        if (!ballot(go)) break;
-        bkt = go ? (bkt + 1u) & S.cap_mask : 0u;
-    }
-}
-
 // Shape s rebuilt from its packed descriptor (L2Args::pk).  The empty
 // volatile asm keeps the rebuild inside the batch loop: hoisted for all
 // eight shapes the masks would not fit the SGPR budget of eight waves per
-// SIMD, while the packed words (4 SGPRs per shape) do.
-__device__ __forceinline__ L2Shape unpack_shape(const L2Args &a, int s) {
-    uint32_t k = a.pk[s].kind, off = a.pk[s].off, cap = a.pk[s].cap_mask, first = a.pk[s].first;
-    asm volatile("" : "+s"(k), "+s"(off), "+s"(cap), "+s"(first));
-    L2Shape S;
-    S.m[0] = (k & kL2PkDst) ? 0xFFFFFFFFu : 0u;
-    S.m[1] = ((k & kL2PkDst) ? 0x0000FFFFu : 0u) | ((k & kL2PkSrc) ? 0xFFFF0000u : 0u);
-    S.m[2] = (k & kL2PkSrc) ? 0xFFFFFFFFu : 0u;
-    S.m[3] = k & 0xFFFFu;
-    S.off = off;
-    S.cap_mask = cap;
-    S.first = first;
-    S.off_key = off + (cap + 1u) * kL2BucketSlots;
-    return S;
+// SIMD, while the packed words (3 SGPRs per shape) do.
+__device__ __forceinline__ void unpack_shape(const L2Args &a, int s, uint32_t (&m)[4], uint32_t &off,
+                                             uint32_t &cap) {
+    uint32_t k = a.pk[s].kind;
+    off = a.pk[s].off;
+    cap = a.pk[s].cap_mask;
+    asm volatile("" : "+s"(k), "+s"(off), "+s"(cap));
+    m[0] = (k & kL2PkDst) ? 0xFFFFFFFFu : 0u;
+    m[1] = ((k & kL2PkDst) ? 0x0000FFFFu : 0u) | ((k & kL2PkSrc) ? 0xFFFF0000u : 0u);
+    m[2] = (k & kL2PkSrc) ? 0xFFFFFFFFu : 0u;
+    m[3] = k & 0xFFFFu;
 }
 
-// Shapes in ascending order of their first rule; a shape is skipped once
-// every lane's match precedes it.  Unrolled with constant shape indices, so
-// the descriptors are loaded into SGPRs once per kernel instead of by two
-// scalar loads per shape and batch (each of which stalled the following LDS
-// wait: lgkmcnt counts both).
+// Both cuckoo slots of every shape, no probe loop and no branch: a key is
+// in one of its two slots or absent, and the lowest matching rule index over
+// all shapes is the first match (empty slots carry kL2NoRule, which never
+// wins).  Unrolled with constant shape indices, so the descriptors are
+// loaded into SGPRs once per kernel.
 template <bool LDS>
 __device__ __forceinline__ uint32_t classify_l2_hash(const uint32_t (&p)[4], bool live, const L2Args &a) {
-    uint32_t best = 0xFFFFFFFFu, res = 0;
+    uint32_t best = kL2NoRule;
 #pragma unroll
     for (int s = 0; s < int(kL2MaxShapes); ++s) {
-        if (s >= a.n) break;
-        const L2Shape S = unpack_shape(a, s);
-        const bool go = live && S.first < best;  // shapes ascend by first rule index
-        if (!ballot(go)) break;
-        l2_lookup<LDS>(S, p, go, a.tab, best, res);
+        if (uint32_t(s) >= a.n) break;
+        uint32_t m[4], off, cap;
+        unpack_shape(a, s, m, off, cap);
+        const uint32_t k0 = p[0] & m[0], k1 = p[1] & m[1], k2 = p[2] & m[2], k3 = p[3] & m[3];
+        const uint32_t h = l2_hash(k0, k1, k2, k3);
+        const u32x4 r0 = l2_ld4<LDS>(a.tab, off + (h & cap) * 4u);
+        const u32x4 r1 = l2_ld4<LDS>(a.tab, off + (l2_hash_alt(h) & cap) * 4u);
+        const bool e0 = ((r0.x ^ k0) | (r0.y ^ k1) | (r0.z ^ k2) | ((r0.w & 0xFFFFu) ^ k3)) == 0u;
+        const bool e1 = ((r1.x ^ k0) | (r1.y ^ k1) | (r1.z ^ k2) | ((r1.w & 0xFFFFu) ^ k3)) == 0u;
+        best = min(best, e0 ? r0.w >> 16 : kL2NoRule);
+        best = min(best, e1 ? r1.w >> 16 : kL2NoRule);
     }
-    return res;
+    const bool hit = live && best != kL2NoRule;
+    return hit ? l2_ld1<LDS>(a.tab, a.off_out + best) : 0u;
 }
 
 template <int ALGO, bool LDS>
@@ -352,10 +351,11 @@ L2Launch l2_plan(const nffacl_l2engine *eng, const L2Table *t, uint64_t n) {
     L.a.tab_dwords = static_cast<uint32_t>(t->meta.blob.size());
     const bool hash = t->meta.algo == NFFACL_ALGO_INDEXED;
     L.a.n = hash ? t->meta.n_shapes : t->meta.n_rules;
+    L.a.off_out = t->meta.off_out;
     for (uint32_t s = 0; s < kL2MaxShapes; ++s) {
         const L2Shape &S = t->meta.shapes[s];
         L.a.pk[s] = dev::L2Packed{(S.m[3] & 0xFFFFu) | (S.m[0] ? dev::kL2PkDst : 0u) | (S.m[2] ? dev::kL2PkSrc : 0u),
-                                  S.off, S.cap_mask, S.first};
+                                  S.off, S.cap_mask};
     }
     L.lds_bytes = t->meta.blob.size() * sizeof(uint32_t);
     L.lds = hash && L.lds_bytes <= kL2LdsMax;

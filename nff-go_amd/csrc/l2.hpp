@@ -10,17 +10,18 @@
 // Two compiled forms, both first-match exact:
 //  LINEAR  8-dword records in file order, scanned wave-uniformly:
 //            [0..2] v0..v2, [3] v3 | m3 << 16, [4..6] m0..m2, [7] OutputNumber
-//  HASH    rules grouped by *shape* (their mask m0..m3); per shape an
-//          open-addressing table keyed by the masked header, holding the
-//          first (lowest-index) rule with that key.  A packet probes every
-//          shape whose first rule precedes its best match so far; the answer
-//          is the lowest rule index found — the reference's first match.
-//          Buckets of four slots (load <= 1/2): a bucket is four 32-bit
-//          fingerprints (key hash | 1; 0 = empty) read with one 16-byte load,
-//          and in a parallel array one 8-dword key record per slot
-//          {k0..k3, rule index, OutputNumber, 0, 0} read only on a
-//          fingerprint match.  A lookup almost always ends in its first
-//          bucket (a match, or a free slot proving absence).
+//  HASH    rules grouped by *shape* (their mask m0..m3); per shape a
+//          two-choice cuckoo table keyed by the masked header, holding the
+//          first (lowest-index) rule with that key.  A slot is one 16-byte
+//          record {k0, k1, k2, k3 | rule index << 16} (k3 = the masked
+//          EtherType, 16 bits); an empty slot has rule index 0xFFFF, which
+//          never beats a match.  A packet reads both candidate slots of every
+//          shape (no probe loop: a key is in one of its two slots or absent)
+//          and takes the lowest matching rule index over all shapes — the
+//          reference's first match; the OutputNumber comes from a per-rule
+//          array after the last shape.  Tables are sized to load <= 1/4; a
+//          key set the insertion cannot place (or 0xFFFF+ rules, or more
+//          than kL2MaxShapes shapes) compiles LINEAR.
 // Rules after the first unconstrained rule (matches everything) are dropped.
 #pragma once
 
@@ -36,32 +37,31 @@
 namespace nffacl {
 
 constexpr uint32_t kL2RecDwords = 8;
-constexpr uint32_t kL2BucketSlots = 4;
-constexpr uint32_t kL2KeyDwords = 8;
 constexpr uint32_t kL2MaxShapes = 8;
+constexpr uint32_t kL2NoRule = 0xFFFFu;  // empty cuckoo slot / no match
 
 struct L2Shape {
     uint32_t m[4];     // header masks of this shape
-    uint32_t off;      // dword offset of its fingerprint buckets (4 dwords each)
-    uint32_t cap_mask; // buckets - 1 (power of two)
-    uint32_t first;    // lowest rule index of the shape
-    uint32_t off_key;  // dword offset of its key records (8 dwords per slot)
+    uint32_t off;      // dword offset of its cuckoo slots (4 dwords each)
+    uint32_t cap_mask; // slots - 1 (power of two)
 };
 
 struct L2Compiled {
     int algo = NFFACL_ALGO_LINEAR;
-    std::vector<uint32_t> blob;  // LINEAR records or HASH tables
-    uint32_t n_rules = 0;        // live rules (LINEAR records)
+    std::vector<uint32_t> blob;  // LINEAR records, or HASH tables + OutputNumber per rule
+    uint32_t n_rules = 0;        // live rules (LINEAR records / output array length)
     uint32_t n_shapes = 0;
+    uint32_t off_out = 0;        // HASH: dword offset of the OutputNumber array
     L2Shape shapes[kL2MaxShapes] = {};
 };
 
 // Host compilation (AUTO -> HASH when the rules have <= kL2MaxShapes shapes).
 L2Compiled compile_l2(const std::vector<nffacl_l2_rule> &eth, int algo);
 
-// Header hash shared by the host compiler and the kernel.
-// (one multiply: rotations fold the four header dwords, the multiply and
-// shifts mix; collisions cost probes, never correctness)
+// Header hashes shared by the host compiler and the kernel: the two cuckoo
+// slots of a key are l2_hash & cap_mask and l2_hash_alt(l2_hash) & cap_mask.
+// (one multiply each: rotations fold the four header dwords, multiplies and
+// shifts mix)
 __host__ __device__ inline uint32_t l2_rotl(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
 __host__ __device__ inline uint32_t l2_hash(uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
     uint32_t h = k0 ^ l2_rotl(k1, 11) ^ l2_rotl(k2, 19) ^ l2_rotl(k3, 27);
@@ -69,6 +69,10 @@ __host__ __device__ inline uint32_t l2_hash(uint32_t k0, uint32_t k1, uint32_t k
     h *= 0x7FEB352Du;
     h ^= h >> 15;
     return h;
+}
+__host__ __device__ inline uint32_t l2_hash_alt(uint32_t h) {
+    h = (h ^ (h >> 16)) * 0x45D9F3Bu;
+    return h ^ (h >> 13);
 }
 
 struct L2Table {
