@@ -22,6 +22,49 @@ __device__ __forceinline__ uint32_t lane_id() {
     return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
 }
 
+// ---- lane-contiguous batch load for 64-byte slots (a wave's 64 packets =
+// 4 KiB contiguous) ---------------------------------------------------------
+// Row-swap variant (MODE 4): lane l = 16r + c loads, for instruction j, the
+// 16 bytes at 1024j + 64c + 16r — chunk r of packet 16j + c; every
+// instruction still covers one contiguous KiB.  Register j of row r then holds
+// M[r][j] = chunk r of packet 16j + c, and a 4x4 transpose across the four
+// 16-lane rows (v_permlane16_swap on register pairs (0,1), (2,3), then
+// v_permlane32_swap on (0,2), (1,3): 4 instructions per dword plane) leaves
+// register m of row r = chunk m of packet 16r + c = packet `lane` — no
+// per-lane packet remap, no permit re-order.
+template <bool NT>
+__device__ __forceinline__ void load_rowswap(const uint8_t *__restrict__ wave_base, uint32_t lane, u32x4 (&v)[4]) {
+    const u32x4 *q = reinterpret_cast<const u32x4 *>(wave_base) + 4u * (lane & 15u) + (lane >> 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = NT ? __builtin_nontemporal_load(q + 64 * j) : q[64 * j];
+}
+
+__device__ __forceinline__ void rowswap_batch(const u32x4 (&v)[4], uint32_t (&d)[16]) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {  // dword plane k of every chunk
+        uint32_t a0 = v[0][k], a1 = v[1][k], a2 = v[2][k], a3 = v[3][k];
+        const auto p01 = __builtin_amdgcn_permlane16_swap(a0, a1, false, false);
+        const auto p23 = __builtin_amdgcn_permlane16_swap(a2, a3, false, false);
+        const auto q02 = __builtin_amdgcn_permlane32_swap(p01[0], p23[0], false, false);
+        const auto q13 = __builtin_amdgcn_permlane32_swap(p01[1], p23[1], false, false);
+        d[0 + k] = q02[0];
+        d[4 + k] = q13[0];
+        d[8 + k] = q02[1];
+        d[12 + k] = q13[1];
+    }
+}
+
+// Chunk 0 (bytes 0..15) of packet `lane` only: 3 of rowswap_batch's 4 swaps
+// per dword plane (the L2 kernel's Ethernet header).
+__device__ __forceinline__ void rowswap_chunk0(const u32x4 (&v)[4], uint32_t (&d)[4]) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const auto p01 = __builtin_amdgcn_permlane16_swap(v[0][k], v[1][k], false, false);
+        const auto p23 = __builtin_amdgcn_permlane16_swap(v[2][k], v[3][k], false, false);
+        d[k] = __builtin_amdgcn_permlane32_swap(p01[0], p23[0], false, false)[0];
+    }
+}
+
 // Zero the bytes of d[] at or past `len`.
 template <int N>
 __device__ __forceinline__ void clip_dwords(uint32_t (&d)[N], uint32_t len) {

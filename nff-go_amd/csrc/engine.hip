@@ -257,35 +257,7 @@ __device__ __forceinline__ void transpose_batch(const u32x4 (&v)[4], uint32_t la
     }
 }
 
-// Row-swap variant (MODE 4): lane l = 16r + c loads, for instruction j, the
-// 16 bytes at 1024j + 64c + 16r — chunk r of packet 16j + c; every
-// instruction still covers one contiguous KiB.  Register j of row r then holds
-// M[r][j] = chunk r of packet 16j + c, and a 4x4 transpose across the four
-// 16-lane rows (v_permlane16_swap on register pairs (0,1), (2,3), then
-// v_permlane32_swap on (0,2), (1,3): 4 instructions per dword plane) leaves
-// register m of row r = chunk m of packet 16r + c = packet `lane` — no
-// per-lane packet remap, no permit re-order.
-template <bool NT>
-__device__ __forceinline__ void load_rowswap(const uint8_t *__restrict__ wave_base, uint32_t lane, u32x4 (&v)[4]) {
-    const u32x4 *q = reinterpret_cast<const u32x4 *>(wave_base) + 4u * (lane & 15u) + (lane >> 4);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = NT ? __builtin_nontemporal_load(q + 64 * j) : q[64 * j];
-}
-
-__device__ __forceinline__ void rowswap_batch(const u32x4 (&v)[4], uint32_t (&d)[16]) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {  // dword plane k of every chunk
-        uint32_t a0 = v[0][k], a1 = v[1][k], a2 = v[2][k], a3 = v[3][k];
-        const auto p01 = __builtin_amdgcn_permlane16_swap(a0, a1, false, false);
-        const auto p23 = __builtin_amdgcn_permlane16_swap(a2, a3, false, false);
-        const auto q02 = __builtin_amdgcn_permlane32_swap(p01[0], p23[0], false, false);
-        const auto q13 = __builtin_amdgcn_permlane32_swap(p01[1], p23[1], false, false);
-        d[0 + k] = q02[0];
-        d[4 + k] = q13[0];
-        d[8 + k] = q02[1];
-        d[12 + k] = q13[1];
-    }
-}
+// Row-swap variant (MODE 4): load_rowswap / rowswap_batch, devutil.hpp.
 
 // Packet index (within the wave's 64) held by lane l after transpose_batch.
 __device__ __forceinline__ uint32_t coal_packet(uint32_t lane) { return 16u * (lane & 3u) + (lane >> 2); }

@@ -13,10 +13,12 @@
 
 #include <algorithm>
 #include <array>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <set>
 #include <string>
+#include <type_traits>
 
 #include "devutil.hpp"
 #include "l2.hpp"
@@ -290,27 +292,38 @@ __device__ __forceinline__ void l2_stage(const L2Args &a) {
 // Two 1024-thread workgroups per CU (LDS mode) need 8 waves per SIMD: at most
 // 64 VGPRs and 80 SGPRs (MI355X_MICROARCH.md: blocks per CU <=
 // 800 / (ceil(sgpr/16)*16 + 16)).
-template <int ALGO, bool LDS>
+// COAL (stride 64): a full batch's 4 KiB are loaded lane-contiguously
+// (load_rowswap: one contiguous KiB per instruction, non-temporal) and each
+// lane's header assembled with permlane swaps; otherwise one 16-byte row
+// piece per lane.  Either way the next batch is loaded while this one is
+// classified.
+template <int ALGO, bool LDS, bool COAL>
 __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8)))
 k_l2_slots(const uint8_t *__restrict__ slots, uint32_t stride, uint64_t n, L2Args a,
            uint32_t *__restrict__ port_out, uint64_t *__restrict__ permit_out) {
     l2_stage<LDS>(a);
-    // grid-stride over 64-packet batches; the next batch's header line is
-    // loaded while this one is classified (+10 % at 256 rules,
-    // profiles/r1_l2_v3)
     const uint32_t lane = lane_id();
     const uint32_t wpb = blockDim.x >> 6;
     const uint64_t step = uint64_t(gridDim.x) * wpb * 64;
     uint64_t base = (uint64_t(blockIdx.x) * wpb + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) * 64;
-    auto header = [&](uint64_t b) {
-        return *reinterpret_cast<const u32x4 *>(slots + (b + lane < n ? b + lane : 0) * stride);
+    // next batch in flight: COAL full batches in nv[0..3], else the row piece in nv[0]
+    u32x4 nv[4] = {};
+    auto fetch = [&](uint64_t b) {
+        if (COAL && b + 64 <= n)
+            load_rowswap<true>(slots + b * 64, lane, nv);
+        else
+            nv[0] = *reinterpret_cast<const u32x4 *>(slots + (b + lane < n ? b + lane : 0) * stride);
     };
-    u32x4 nv = base < n ? header(base) : u32x4{0, 0, 0, 0};
+    if (base < n) fetch(base);
     for (; base < n; base += step) {
-        const u32x4 v = nv;
-        if (base + step < n) nv = header(base + step);
+        uint32_t p[4];
+        if (COAL && base + 64 <= n) {
+            rowswap_chunk0(nv, p);
+        } else {
+            p[0] = nv[0].x; p[1] = nv[0].y; p[2] = nv[0].z; p[3] = nv[0].w;
+        }
+        if (base + step < n) fetch(base + step);
         const bool live = base + lane < n;
-        const uint32_t p[4] = {v.x, v.y, v.z, v.w};
         store_verdicts(base, lane, live, classify_l2<ALGO, LDS>(p, live, a), port_out, permit_out);
     }
 }
@@ -372,7 +385,8 @@ int l2_prepare_kernels() {
     static std::once_flag once;
     static hipError_t err = hipSuccess;
     std::call_once(once, [] {
-        const void *k[2] = {reinterpret_cast<const void *>(dev::k_l2_slots<NFFACL_ALGO_INDEXED, true>),
+        const void *k[3] = {reinterpret_cast<const void *>(dev::k_l2_slots<NFFACL_ALGO_INDEXED, true, false>),
+                            reinterpret_cast<const void *>(dev::k_l2_slots<NFFACL_ALGO_INDEXED, true, true>),
                             reinterpret_cast<const void *>(dev::k_l2_frames<NFFACL_ALGO_INDEXED, true>)};
         for (const void *f : k) {
             hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kL2LdsMax));
@@ -391,12 +405,24 @@ int l2_launch_slots(nffacl_l2engine *eng, const L2Table *t, const uint8_t *d_slo
     if (n == 0) return NFFACL_OK;
     const L2Launch L = l2_plan(eng, t, n);
     const dim3 g(L.grid), b(L.block);
-    if (t->meta.algo == NFFACL_ALGO_LINEAR)
-        hipLaunchKernelGGL((dev::k_l2_slots<NFFACL_ALGO_LINEAR, false>), g, b, 0, stream, d_slots, stride, n, L.a, d_port, d_permit);
-    else if (L.lds)
-        hipLaunchKernelGGL((dev::k_l2_slots<NFFACL_ALGO_INDEXED, true>), g, b, L.lds_bytes, stream, d_slots, stride, n, L.a, d_port, d_permit);
-    else
-        hipLaunchKernelGGL((dev::k_l2_slots<NFFACL_ALGO_INDEXED, false>), g, b, 0, stream, d_slots, stride, n, L.a, d_port, d_permit);
+    const char *cv = std::getenv("NFFACL_TUNE_L2_COAL");  // A/B override
+    const bool coal = stride == 64 && !(cv && *cv == '0');
+    auto go = [&](auto algo_c, auto lds_c, auto coal_c) {
+        hipLaunchKernelGGL((dev::k_l2_slots<decltype(algo_c)::value, decltype(lds_c)::value, decltype(coal_c)::value>),
+                           g, b, decltype(lds_c)::value ? L.lds_bytes : 0, stream, d_slots, stride, n, L.a, d_port,
+                           d_permit);
+    };
+    using lin = std::integral_constant<int, NFFACL_ALGO_LINEAR>;
+    using hsh = std::integral_constant<int, NFFACL_ALGO_INDEXED>;
+    using yes = std::true_type;
+    using no = std::false_type;
+    if (t->meta.algo == NFFACL_ALGO_LINEAR) {
+        if (coal) go(lin{}, no{}, yes{}); else go(lin{}, no{}, no{});
+    } else if (L.lds) {
+        if (coal) go(hsh{}, yes{}, yes{}); else go(hsh{}, yes{}, no{});
+    } else {
+        if (coal) go(hsh{}, no{}, yes{}); else go(hsh{}, no{}, no{});
+    }
     HIP_TRY(hipGetLastError());
     return NFFACL_OK;
 }
