@@ -259,6 +259,26 @@ __device__ __forceinline__ void transpose_batch(const u32x4 (&v)[4], uint32_t la
 
 // Row-swap variant (MODE 4): load_rowswap / rowswap_batch, devutil.hpp.
 
+// Packed frames, the same layout: for instruction j lane 16r + c loads chunk
+// r of frame 16j + c (that frame's offset fetched from lane 16j + c with
+// ds_bpermute), so every instruction consumes whole 64-byte frame lines and
+// non-temporal loads pay off; rowswap_batch then gives lane l the first 64
+// bytes of its own frame.  (sol `frames_rs_nt` 0.293 ms vs 0.340 ms for one
+// frame per lane, C3 IMIX, profiles/r1_frames_rs/.)  Every lane of the wave
+// must be active; `off` is this lane's frame offset (any valid offset for
+// lanes past the batch end).
+__device__ __forceinline__ void load_frames_rs(const uint8_t *__restrict__ frames, uint64_t off, uint32_t lane,
+                                               u32x4 (&v)[4]) {
+    const uint32_t lo = static_cast<uint32_t>(off), hi = static_cast<uint32_t>(off >> 32);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int src = static_cast<int>((16u * j + (lane & 15u)) << 2);
+        const uint64_t o = uint64_t(static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(lo)))) |
+                           uint64_t(static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(hi)))) << 32;
+        v[j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(frames + o) + (lane >> 4));
+    }
+}
+
 // Packet index (within the wave's 64) held by lane l after transpose_batch.
 __device__ __forceinline__ uint32_t coal_packet(uint32_t lane) { return 16u * (lane & 3u) + (lane >> 2); }
 
@@ -852,27 +872,34 @@ k_indexed_frames(const uint8_t *__restrict__ frames, const uint64_t *__restrict_
     // other of two register buffers (ping-pong, no copies), and the
     // descriptors of the batch after.
     constexpr bool PF = TM == kTabSplit;
+    // Frame lines load cooperatively (load_frames_rs) and are assembled per
+    // lane just before their batch is classified.
+    auto run_batch = [&](uint64_t b, uint64_t ds, const u32x4(&v)[4]) {
+        uint32_t d[16];
+        rowswap_batch(v, d);
+        classify_batch(b, ds, d);
+    };
     if (PF) {
-        uint32_t A[16], B[16];
+        u32x4 A[4], B[4];
         uint64_t dsA = desc_at(base), dsB = 0;
-        load16(frames + (dsA >> 16), A);
+        load_frames_rs(frames, dsA >> 16, lane, A);
         uint64_t dsN = desc_at(base + S);  // descriptor of the batch after the one in flight
         while (true) {
             const uint64_t b1 = base + S;
             if (b1 < n) {
                 dsB = dsN;
-                load16(frames + (dsB >> 16), B);
+                load_frames_rs(frames, dsB >> 16, lane, B);
                 dsN = desc_at(b1 + S);
             }
-            classify_batch(base, dsA, A);
+            run_batch(base, dsA, A);
             if (b1 >= n) break;
             const uint64_t b2 = b1 + S;
             if (b2 < n) {
                 dsA = dsN;
-                load16(frames + (dsA >> 16), A);
+                load_frames_rs(frames, dsA >> 16, lane, A);
                 dsN = desc_at(b2 + S);
             }
-            classify_batch(b1, dsB, B);
+            run_batch(b1, dsB, B);
             if (b2 >= n) break;
             base = b2;
         }
@@ -881,9 +908,9 @@ k_indexed_frames(const uint8_t *__restrict__ frames, const uint64_t *__restrict_
         for (; base < n; base += S) {
             const uint64_t ds = ds_next;
             ds_next = desc_at(base + S);
-            uint32_t d[16];
-            load16(frames + (ds >> 16), d);
-            classify_batch(base, ds, d);
+            u32x4 v[4];
+            load_frames_rs(frames, ds >> 16, lane, v);
+            run_batch(base, ds, v);
         }
     }
 }

@@ -411,3 +411,35 @@ def test_hybrid_directory_budgets(torch_cuda, monkeypatch, dir_kb, flat):
         torch.cuda.synchronize()
         np.testing.assert_array_equal(port.cpu().numpy().view(np.uint32),
                                       oracle.classify_frames(frames, desc, a4, a6, threads=THREADS))
+
+
+@pytest.mark.parametrize("algo", ALGOS)
+@pytest.mark.parametrize("n", [1, 63, 65, 4097, (1 << 20) + 3])
+def test_frames_ragged_and_short(torch_cuda, algo, n):
+    """Packed frames (the cooperative 64-lane frame-line loads): ragged batch
+    counts, and frames of 0..80 bytes whose bytes past the length hold
+    garbage that must read as 0 — against the oracle on the same buffer."""
+    torch = torch_cuda
+    g = synth.gen_rules(synth.SPECS["c3"], synth.RULE_SEEDS["c3"])
+    rules, (a4, a6) = _rules_and_arrays(g.text)
+    rng = np.random.default_rng(n)
+    m = min(n, 4096)
+    short = synth.gen_slots(g, m, 41, stride=96).reshape(m, 96)
+    lens = rng.integers(0, 81, m)
+    frames = np.full(m * 96 + 64, 0xEE, np.uint8)
+    for i in range(m):
+        frames[i * 96:i * 96 + lens[i]] = short[i, :lens[i]]
+    desc = (np.arange(m, dtype=np.uint64) * np.uint64(96) << np.uint64(16)) | lens.astype(np.uint64)
+    if n > m:  # the bulk: IMIX frames after the short ones
+        big, bdesc = synth.gen_imix(g, n - m, 42)
+        bdesc = bdesc + (np.uint64(len(frames)) << np.uint64(16))
+        frames = np.concatenate([frames, big])
+        desc = np.concatenate([desc, bdesc])
+    with nffacl.Engine(rules, algo=algo) as eng:
+        port = torch.zeros(n, dtype=torch.int32, device="cuda")
+        permit = torch.zeros((n + 63) // 64, dtype=torch.int64, device="cuda")
+        eng.classify_frames_device(to_dev(torch, frames), to_dev(torch, desc.view(np.int64)), n, port, permit)
+        torch.cuda.synchronize()
+    want = oracle.classify_frames(frames, desc, a4, a6, threads=THREADS)
+    np.testing.assert_array_equal(port.cpu().numpy().view(np.uint32), want)
+    np.testing.assert_array_equal(permit.cpu().numpy().view(np.uint64), permit_bits(want))

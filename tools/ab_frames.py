@@ -40,6 +40,10 @@ V = {
                                       8, 256, stream.cuda_stream),
     "sol_frames_pf": lambda: sol.sol_run(6, d_frames.data_ptr(), n, port.data_ptr(), bits.data_ptr(),
                                          d_desc.data_ptr(), 8, 256, stream.cuda_stream),
+    "sol_frames_rs": lambda: sol.sol_run(7, d_frames.data_ptr(), n, port.data_ptr(), bits.data_ptr(),
+                                         d_desc.data_ptr(), 8, 256, stream.cuda_stream),
+    "sol_frames_rs_nt": lambda: sol.sol_run(8, d_frames.data_ptr(), n, port.data_ptr(), bits.data_ptr(),
+                                            d_desc.data_ptr(), 8, 256, stream.cuda_stream),
     "sol_frames_16w": lambda: sol.sol_run(5, d_frames.data_ptr(), n, port.data_ptr(), bits.data_ptr(),
                                           d_desc.data_ptr(), 1, 1024, stream.cuda_stream),
 }

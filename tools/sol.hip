@@ -11,14 +11,17 @@
 //   frames   : packed IMIX frames: per lane its u64 descriptor, then the
 //              frame's first 64 bytes (classify_frames' pattern); frames_pf
 //              loads the next batch's descriptors + frame lines ahead
+//   frames_rs: frames, each wave instruction loading one 16-byte chunk of 64
+//              frames' first lines (lane 16r + c: chunk r of frame 16j + c,
+//              offsets fetched with ds_bpermute), lanes' frames assembled
+//              with permlane row swaps (libnffacl's load_rowswap layout)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+#include "../nff-go_amd/csrc/devutil.hpp"
 
-__device__ __forceinline__ uint32_t lane_id() {
-    return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-}
+using nffacl::dev::u32x4;
+using nffacl::dev::lane_id;
 
 template <bool NT>
 __device__ __forceinline__ void ld16(const uint8_t *p, uint32_t (&d)[16]) {
@@ -129,6 +132,36 @@ __global__ void __launch_bounds__(1024) k_frames(const uint8_t *fr, const uint64
     }
 }
 
+__device__ __forceinline__ uint32_t bperm32(uint32_t v, uint32_t src) {
+    return static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(static_cast<int>(src << 2), static_cast<int>(v)));
+}
+
+template <bool NT>
+__global__ void __launch_bounds__(1024) k_frames_rs(const uint8_t *fr, const uint64_t *desc, uint64_t n,
+                                                    uint32_t *port, uint64_t *bits) {
+    const uint32_t lane = lane_id();
+    const uint64_t wave0 = uint64_t(blockIdx.x) * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t step = uint64_t(gridDim.x) * (blockDim.x >> 6) * 64;
+    for (uint64_t base = wave0 * 64; base < n; base += step) {
+        const uint64_t i = base + lane;
+        const uint64_t off = (i < n ? desc[i] : 0) >> 16;
+        u32x4 v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t src = 16u * j + (lane & 15u);
+            const uint64_t o = uint64_t(bperm32(uint32_t(off), src)) | uint64_t(bperm32(uint32_t(off >> 32), src)) << 32;
+            const u32x4 *q = reinterpret_cast<const u32x4 *>(fr + o) + (lane >> 4);
+            v[j] = NT ? __builtin_nontemporal_load(q) : *q;
+        }
+        uint32_t d[16];
+        nffacl::dev::rowswap_batch(v, d);
+        const uint32_t r = fold(d);
+        if (i < n) port[i] = r;
+        const uint64_t b = __builtin_amdgcn_ballot_w64(i < n && (r & 1));
+        if (lane == 0) bits[base >> 6] = b;
+    }
+}
+
 __global__ void __launch_bounds__(256) k_copy(const u32x4 *a, u32x4 *b, uint64_t n16) {
     for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n16; i += uint64_t(gridDim.x) * blockDim.x)
         b[i] = __builtin_nontemporal_load(a + i);
@@ -152,6 +185,8 @@ extern "C" int sol_run(int which, const void *slots, uint64_t n, void *port, voi
                                static_cast<u32x4 *>(scratch), n * 4); break;
     case 5: hipLaunchKernelGGL(k_frames<false>, g, b, 0, st, s, static_cast<const uint64_t *>(scratch), n, p, bb); break;
     case 6: hipLaunchKernelGGL(k_frames<true>, g, b, 0, st, s, static_cast<const uint64_t *>(scratch), n, p, bb); break;
+    case 7: hipLaunchKernelGGL(k_frames_rs<false>, g, b, 0, st, s, static_cast<const uint64_t *>(scratch), n, p, bb); break;
+    case 8: hipLaunchKernelGGL(k_frames_rs<true>, g, b, 0, st, s, static_cast<const uint64_t *>(scratch), n, p, bb); break;
     default: return -1;
     }
     return hipGetLastError() == hipSuccess ? 0 : -2;
