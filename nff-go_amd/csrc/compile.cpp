@@ -523,42 +523,41 @@ void build_hybrid(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vec
         for (int k = 0; k < 4; ++k) all[4 * f + k] = &plan[f].dims[k];
     double weight[8];
     for (int i = 0; i < 8; ++i) weight[i] = double(i < 4 ? n4 : n6) / double(std::max<uint32_t>(1, n4 + n6));
-    // Policy (profiles/r1_hybrid/): directories in LDS with per-lane walks
-    // while that keeps the expected candidates per packet short; past that,
-    // wide directories in global memory and the wave-flattened candidates.
+    // Policy: the flat walk over directories staged in LDS (flat-LDS) — it
+    // beat the per-lane walks on C3 (0.519 vs 0.531 ms) and the flat walk
+    // over 1 MiB global directories on C5 (0.918 vs 1.027 ms): lists sized
+    // for LDS directories replicate short prefixes across far fewer buckets
+    // and stay nearly L2-resident (C5: 3.8 MB of entries instead of ~10 MB),
+    // profiles/r1_flat_lds/.
     // Tuning overrides (experiments, tests; unset in production):
-    // NFFACL_TUNE_DIR_KB sets the directory budget, NFFACL_TUNE_FLAT=0/1
-    // forces the form (directories past LDS size always give the flat form).
+    // NFFACL_TUNE_DIR_KB sets the directory budget, NFFACL_TUNE_FLAT forces
+    // the form (0 lane: INDEXED's inline entries walked per lane; 1 flat
+    // with global directories; 2 flat-LDS); directory budgets past LDS size
+    // always give the global flat form.
     const size_t tuned = tuned_dir_budget();
     const char *fv = std::getenv("NFFACL_TUNE_FLAT");
-    const int force = fv && *fv ? std::atoi(fv) : -1;
+    const int force = fv && *fv ? std::atoi(fv) : 2;
     const char *dv = std::getenv("NFFACL_TUNE_DIR16");
     const bool want16 = !(dv && *dv && std::atoi(dv) == 0);
-    bool flat;
-    if (tuned) {
-        flat = force == 1 || tuned > kLdsTableBytes;
-        size_and_fill(all, weight, tuned, !flat && want16);
-    } else if (force >= 0) {
-        flat = force == 1;
-        size_and_fill(all, weight, flat ? kHybFlatDirBytes : kHybLaneDirBytes, !flat && want16);
-    } else {
-        flat = size_and_fill(all, weight, kHybLaneDirBytes, want16) > kHybFlatCandidates;
-        if (flat) size_and_fill(all, weight, kHybFlatDirBytes);
-    }
-    // lane form: two-level directories unless some 64-bucket group holds
-    // 65536+ entries (then plain u32, re-sized for the same budget)
-    bool dir16 = !flat && want16;
+    const size_t budget = tuned ? tuned : (force == 1 ? kHybFlatDirBytes : kHybLaneDirBytes);
+    const bool lds_dirs = force != 1 && budget <= kHybLdsDirMaxBytes;
+    const bool flat = force != 0 || !lds_dirs;
+    size_and_fill(all, weight, budget, lds_dirs && want16);
+    // LDS directories: two-level unless some 64-bucket group holds 65536+
+    // entries (then plain u32, re-sized for the same budget)
+    bool dir16 = lds_dirs && want16;
     for (int i = 0; i < 8 && dir16; ++i) {
         const std::vector<uint32_t> &dir = all[i]->dir;
         for (size_t t = 0; t < dir.size(); ++t)
             if (dir[t] - dir[(t >> kDir16GroupShift) << kDir16GroupShift] > 0xFFFFu) { dir16 = false; break; }
     }
-    if (!flat && want16 && !dir16) size_and_fill(all, weight, tuned ? tuned : kHybLaneDirBytes, false);
+    if (lds_dirs && want16 && !dir16) size_and_fill(all, weight, tuned ? tuned : kHybLaneDirBytes, false);
     std::vector<uint32_t> &blob = out.blob;
     FamilyIndex *fi[2] = {&out.idx4, &out.idx6};
     const std::vector<uint32_t> *recs[2] = {&rec4, &rec6};
     const uint32_t rw[2] = {kRec4Dwords, kRec6Dwords};
-    // the eight directories first: the LDS image of the lane form
+    // the eight directories first: the LDS image of the lane and flat-LDS forms
+    uint32_t dir_words[8];  // directory words holding entry numbers (base words when two-level)
     for (int f = 0; f < 2; ++f)
         for (int k = 0; k < 4; ++k) {
             const std::vector<uint32_t> &dir = all[4 * f + k]->dir;
@@ -566,11 +565,13 @@ void build_hybrid(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vec
             di.off_dir = static_cast<uint32_t>(blob.size());
             if (!dir16) {
                 blob.insert(blob.end(), dir.begin(), dir.end());
+                dir_words[4 * f + k] = static_cast<uint32_t>(dir.size());
                 continue;
             }
             const size_t nb = dir.size() - 1;
             const size_t groups = (nb >> kDir16GroupShift) + 2;  // base[g + 1] stays readable
             for (size_t g = 0; g < groups; ++g) blob.push_back(dir[std::min(g << kDir16GroupShift, nb)]);
+            dir_words[4 * f + k] = static_cast<uint32_t>(groups);
             di.off_dir16 = static_cast<uint32_t>(blob.size());
             auto rel = [&](size_t t) -> uint32_t {
                 return t <= nb ? dir[t] - dir[(t >> kDir16GroupShift) << kDir16GroupShift] : 0u;
@@ -579,7 +580,7 @@ void build_hybrid(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vec
             for (size_t w = 0; w < words; ++w) blob.push_back(rel(2 * w) | rel(2 * w + 1) << 16);
         }
     while (blob.size() % 4) blob.push_back(0);
-    out.lds_dwords = flat ? 0u : static_cast<uint32_t>(blob.size());
+    out.lds_dwords = lds_dirs ? static_cast<uint32_t>(blob.size()) : 0u;
     for (int f = 0; f < 2; ++f) {
         const bool v6 = f == 1;
         // lane form: INDEXED's inline entries (exact, output inline — a hit
@@ -598,7 +599,7 @@ void build_hybrid(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vec
             di.off_ent = static_cast<uint32_t>(blob.size());
             if (flat) {  // directory values: absolute entry numbers (16-byte units)
                 const uint32_t first = di.off_ent / kHybEntDwords;
-                for (size_t t = 0; t <= di.n_buckets; ++t) blob[di.off_dir + t] += first;
+                for (uint32_t t = 0; t < dir_words[4 * f + k]; ++t) blob[di.off_dir + t] += first;
                 for (uint32_t r : d.ents) emit_hyb_entry(recs[f]->data() + size_t(r) * rw[f], v6, r, blob);
             } else {     // relative to off_ent, as INDEXED
                 for (uint32_t r : d.ents) emit_entry(recs[f]->data() + size_t(r) * rw[f], v6, r, blob);

@@ -364,6 +364,9 @@ enum TableMode : int {
                      // candidates of a wave's 64 packets tested 64 at a time,
                      // 2 rounds of loads in flight
     kTabFlat4 = 5,   // the same, 4 rounds in flight
+    kTabFlatLds = 6, // HYBRID flat-LDS: the flat walk (2 rounds in flight)
+                     // over directories staged in LDS, one 1024-thread
+                     // workgroup per CU, candidate scratch after the image
 };
 
 extern __shared__ __attribute__((aligned(16))) uint32_t lds_tab[];
@@ -584,11 +587,11 @@ __device__ __forceinline__ bool hyb_cold_ok(const IndexedArgs &a, bool v6, uint3
 // carries the mark forward.  Each passing candidate posts its rule index to
 // the packet's LDS minimum (ds_min_u32): the minimum over every candidate is
 // the first match of the ordered lists, no early exit needed.
-constexpr int kFlatMaxRounds = 4;
+template <int R>
 struct FlatScratch {
-    uint32_t mark[64 * kFlatMaxRounds];   // window position -> (list id << 8 | position) + 1, 0 = none
-    uint32_t delta[64 * kFlatMaxRounds];  // window position -> entry number - candidate number
-    uint32_t best[64];                    // per packet (lane): lowest passing rule index
+    uint32_t mark[64 * R];   // window position -> (list id << 8 | position) + 1, 0 = none
+    uint32_t delta[64 * R];  // window position -> entry number - candidate number
+    uint32_t best[64];       // per packet (lane): lowest passing rule index
 };
 
 // Order this wave's LDS writes before its following LDS reads of other lanes'
@@ -632,8 +635,8 @@ __device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
     return x;
 }
 
-template <int NS, int R>
-__device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fields &f, FlatScratch &W,
+template <int NS, int R, bool LDS_DIRS>
+__device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fields &f, FlatScratch<R> &W,
                                                   uint32_t lane) {
     const bool v6 = f.is6;
     const bool mine = f.is4 || f.is6;
@@ -649,8 +652,14 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
         const uint32_t shift = v6 ? s6.shift : s4.shift;
         const uint32_t dir = v6 ? s6.off_dir : s4.off_dir;
         const uint32_t t = key[s] >> shift;
-        st[s] = a.tab[dir + t];
-        ln[s] = mine ? a.tab[dir + t + 1] - st[s] : 0u;
+        if (LDS_DIRS) {
+            uint32_t hi;
+            SplitTab{a.tab}.bounds(dir, v6 ? s6.off_dir16 : s4.off_dir16, t, st[s], hi);
+            ln[s] = mine ? hi - st[s] : 0u;
+        } else {
+            st[s] = a.tab[dir + t];
+            ln[s] = mine ? a.tab[dir + t + 1] - st[s] : 0u;
+        }
     }
     uint32_t total = 0;
 #pragma unroll
@@ -752,9 +761,15 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
 template <int NS, int TM>
 __device__ __forceinline__ uint32_t classify_any(const IndexedArgs &a, const Fields &f) {
     if (TM == kTabFlat || TM == kTabFlat4) {
-        FlatScratch *W = reinterpret_cast<FlatScratch *>(lds_tab);
+        constexpr int R = TM == kTabFlat4 ? 4 : 2;
+        FlatScratch<R> *W = reinterpret_cast<FlatScratch<R> *>(lds_tab);
         const uint32_t lane = lane_id();
-        return classify_flat<NS, TM == kTabFlat4 ? 4 : 2>(a, f, W[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)], lane);
+        return classify_flat<NS, R, false>(a, f, W[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)], lane);
+    }
+    if (TM == kTabFlatLds) {  // scratch after the staged directories (stage_dwords: multiple of 4)
+        FlatScratch<2> *W = reinterpret_cast<FlatScratch<2> *>(lds_tab + a.stage_dwords);
+        const uint32_t lane = lane_id();
+        return classify_flat<NS, 2, true>(a, f, W[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)], lane);
     }
     if (TM == kTabLds) return classify_indexed<NS, 1>(LdsTab{}, a, f);
     if (TM == kTabSplit) return classify_indexed<NS, 1>(SplitTab{a.tab}, a, f);
@@ -772,7 +787,7 @@ template <int NS, int TM, int MODE>
 __global__ void __launch_bounds__(1024)
 k_indexed_slots(const uint8_t *__restrict__ slots, uint32_t stride, uint64_t n, IndexedArgs a,
                 uint32_t *__restrict__ port_out, uint64_t *__restrict__ permit_out) {
-    if (TM == kTabLds || TM == kTabSplit) stage_table(a);
+    if (TM == kTabLds || TM == kTabSplit || TM == kTabFlatLds) stage_table(a);
     const uint32_t lane = lane_id();
     const uint32_t wpb = blockDim.x >> 6;
     const uint64_t wave0 = uint64_t(blockIdx.x) * wpb + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -843,7 +858,7 @@ template <int NS, int TM>
 __global__ void __launch_bounds__(1024)
 k_indexed_frames(const uint8_t *__restrict__ frames, const uint64_t *__restrict__ desc, uint64_t n,
                  IndexedArgs a, uint32_t *__restrict__ port_out, uint64_t *__restrict__ permit_out) {
-    if (TM == kTabLds || TM == kTabSplit) stage_table(a);
+    if (TM == kTabLds || TM == kTabSplit || TM == kTabFlatLds) stage_table(a);
     const uint32_t lane = lane_id();
     const uint32_t wpb = blockDim.x >> 6;
     const uint64_t S = uint64_t(gridDim.x) * wpb * 64;  // grid stride in packets
@@ -1000,9 +1015,10 @@ static int tune_env(const char *name, int dflt) {
 static bool table_consistent(const DevTable *t) {
     const CompiledTable &m = t->meta;
     const size_t dw = m.blob.size();
-    if (m.algo == NFFACL_ALGO_HYBRID && m.lds_dwords == 0)
+    if (m.algo == NFFACL_ALGO_HYBRID && (m.lds_dwords == 0 || m.idx4.entry_dwords == kHybEntDwords))
         return m.idx4.entry_dwords == kHybEntDwords && m.idx6.entry_dwords == kHybEntDwords &&
-               m.off_rec4 <= dw && m.off_rec6 <= dw;
+               m.off_rec4 <= dw && m.off_rec6 <= dw &&
+               size_t(m.lds_dwords) * sizeof(uint32_t) <= kHybLdsDirMaxBytes && m.lds_dwords <= dw;
     if (m.algo == NFFACL_ALGO_HYBRID)
         return size_t(m.lds_dwords) * sizeof(uint32_t) <= kLdsTableBytes && m.lds_dwords <= dw &&
                m.idx4.entry_dwords == kEnt4Dwords && m.idx6.entry_dwords == kEnt6Dwords;
@@ -1018,10 +1034,18 @@ static IndexedLaunch indexed_launch(const DevTable *t) {
     // staged in LDS, inline entries walked per lane; flat form (lds_dwords 0):
     // directories and compact entries in global memory, candidates flat.
     if (t->meta.algo == NFFACL_ALGO_HYBRID && t->meta.lds_dwords == 0) {
-        L.tm = tune_env("NFFACL_TUNE_ROUNDS", 4) == 2 ? dev::kTabFlat : dev::kTabFlat4;
+        const bool r2 = tune_env("NFFACL_TUNE_ROUNDS", 4) == 2;
+        L.tm = r2 ? dev::kTabFlat : dev::kTabFlat4;
         L.block = static_cast<uint32_t>(tune_env("NFFACL_TUNE_BLOCK", 256));
         L.per_cu = static_cast<uint32_t>(tune_env("NFFACL_TUNE_PER_CU", 8));
-        L.lds_bytes = sizeof(dev::FlatScratch) * (L.block / 64);
+        L.lds_bytes = (r2 ? sizeof(dev::FlatScratch<2>) : sizeof(dev::FlatScratch<4>)) * (L.block / 64);
+        return L;
+    }
+    if (t->meta.algo == NFFACL_ALGO_HYBRID && t->meta.idx4.entry_dwords == kHybEntDwords) {  // flat-LDS
+        L.tm = dev::kTabFlatLds;
+        L.block = 1024u;
+        L.per_cu = 1u;
+        L.lds_bytes = size_t(t->meta.lds_dwords) * sizeof(uint32_t) + sizeof(dev::FlatScratch<2>) * (L.block / 64);
         return L;
     }
     if (t->meta.algo == NFFACL_ALGO_HYBRID) {
@@ -1081,6 +1105,7 @@ static void dispatch_indexed(int ns, int tm, F &&f) {
         case dev::kTabSplit: f(nsc, std::integral_constant<int, dev::kTabSplit>{}); break;
         case dev::kTabFlat: f(nsc, std::integral_constant<int, dev::kTabFlat>{}); break;
         case dev::kTabFlat4: f(nsc, std::integral_constant<int, dev::kTabFlat4>{}); break;
+        case dev::kTabFlatLds: f(nsc, std::integral_constant<int, dev::kTabFlatLds>{}); break;
         default: f(nsc, std::integral_constant<int, dev::kTabGlobal>{}); break;
         }
     };
@@ -1094,7 +1119,7 @@ int prepare_kernels() {
     static hipError_t err = hipSuccess;
     std::call_once(once, [] {
         for (int ns = 2; ns <= 4; ++ns)
-            for (int tm : {int(dev::kTabLds), int(dev::kTabSplit)})
+            for (int tm : {int(dev::kTabLds), int(dev::kTabSplit), int(dev::kTabFlatLds)})
                 dispatch_indexed(ns, tm, [&](auto nsc, auto tmc) {
                     const hipError_t e = allow_lds_modes<decltype(nsc)::value, decltype(tmc)::value>();
                     if (e != hipSuccess) err = e;
@@ -1113,7 +1138,7 @@ static void launch_slots_tm(int mode, const IndexedLaunch &L, uint32_t grid, hip
                             uint32_t *d_port, uint64_t *d_permit) {
     const dim3 g(grid), b(L.block);
     const size_t lds = TM == dev::kTabGlobal ? 0 : L.lds_bytes;
-    if (TM == dev::kTabFlat || TM == dev::kTabFlat4) {  // built with load modes 0 and 4 only
+    if (TM == dev::kTabFlat || TM == dev::kTabFlat4 || TM == dev::kTabFlatLds) {  // built with load modes 0 and 4 only
         if (mode == 0)
             hipLaunchKernelGGL((dev::k_indexed_slots<NS, TM, 0>), g, b, lds, stream, d_slots, stride, n, a, d_port, d_permit);
         else

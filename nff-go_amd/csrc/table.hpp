@@ -65,17 +65,22 @@ constexpr uint32_t kMaxIndexedRules = 1u << 23;
 // ---- hybrid table (tables whose inline index outgrows LDS) ---------------
 //
 // Same slot assignment and ascending bucket lists as the indexed table, with
-// the eight directories (both families) first in the blob, in one of two forms:
-//  * lane form (lds_dwords > 0): the directories, radix widths chosen to fit
-//    kHybLaneDirBytes, are the LDS image — two-level (kDir16GroupShift) when
-//    every group fits u16 offsets; the lists hold INDEXED's inline entries
-//    (directory values relative to the slot's entries, as above) read from
-//    global memory, each lane walking its own lists;
-//  * flat form (lds_dwords == 0) — when LDS-sized directories leave more than
-//    kHybFlatCandidates expected candidates per packet: plain u32 directories
-//    sized to kHybFlatDirBytes, read from global memory, values = absolute
-//    entry numbers (16-byte units of the blob); a wave tests its packets'
-//    candidates 64 at a time, and a list entry is 16 compact bytes:
+// the eight directories (both families) first in the blob, in one of three
+// forms:
+//  * flat-LDS (default; lds_dwords > 0, entry_dwords == kHybEntDwords): the
+//    directories, radix widths chosen to fit kHybLaneDirBytes, are the LDS
+//    image — two-level (kDir16GroupShift) when every group fits u16
+//    offsets — holding absolute entry numbers (16-byte units of the blob;
+//    two-level: in the base words); a wave tests its packets' candidates 64
+//    at a time, list entries compact (below);
+//  * lane form (forced; lds_dwords > 0, INDEXED entry sizes): the same LDS
+//    directories, values relative to the slot's entries; the lists hold
+//    INDEXED's inline entries read from global memory, each lane walking its
+//    own lists;
+//  * flat form (forced, or directory budgets past LDS; lds_dwords == 0):
+//    plain u32 directories sized to kHybFlatDirBytes read from global
+//    memory, values and entries as flat-LDS.
+// A compact list entry is 16 bytes:
 //      [0] src word, big-endian value (IPv6: top 32 bits)
 //      [1] dst word, big-endian value
 //      [2] meta = id | exact << 8 | rule_index << 9          (as inline)
@@ -89,8 +94,8 @@ constexpr uint32_t kMaxIndexedRules = 1u << 23;
 //      of the inline entry (src[1..3], src_mask[1..3], dst[1..3], dst_mask[1..3]).
 //    An entry with the cold bit (port ranges not made of whole blocks, IPv6
 //    prefixes longer than 32) is confirmed against its cold record.
-// The flat form encodes only CIDR masks and id_mask in {0, 0xff} (what the
-// parsers produce); other rule sets compile INDEXED.
+// The hybrid forms encode only CIDR masks and id_mask in {0, 0xff} (what
+// the parsers produce); other rule sets compile INDEXED.
 constexpr uint32_t kHybEntDwords = 4;
 constexpr uint32_t kHybCold = 1u << 12;
 constexpr uint32_t kHybOutShift = 13;
@@ -104,7 +109,9 @@ constexpr uint32_t kHybCold6Dwords = 16;
 // two (C3: 0.64 vs 0.69 ms, profiles/r1_hybrid/).
 constexpr size_t kHybLaneDirBytes = 128 * 1024;
 constexpr size_t kHybFlatDirBytes = 1024 * 1024;
-constexpr double kHybFlatCandidates = 6.0;
+// Largest LDS directory image of the flat-LDS form: 160 KiB minus the 16
+// waves' candidate scratch (engine.hip FlatScratch<2>, 1280 B each) and 1 KiB.
+constexpr size_t kHybLdsDirMaxBytes = 139 * 1024;
 // Lane-form directories are two-level: a u32 base per group of 64 buckets +
 // a u16 offset per bucket (2.06 B per bucket instead of 4), so the LDS budget
 // holds twice the buckets.  A group whose lists exceed 65535 entries keeps

@@ -357,7 +357,7 @@ def test_full_size_c2_properties(torch_cuda):
     np.testing.assert_array_equal(got, want)
 
 
-@pytest.mark.parametrize("flat", [0, 1])
+@pytest.mark.parametrize("flat", [0, 1, 2])
 def test_full_size_c5_hybrid(torch_cuda, monkeypatch, flat):
     """C5 (100k rules with port ranges) at 2^22 packets: HYBRID (AUTO's choice)
     == INDEXED read from global memory on every packet, and a 2^14 random
@@ -386,7 +386,7 @@ def test_full_size_c5_hybrid(torch_cuda, monkeypatch, flat):
     np.testing.assert_array_equal(outs[nffacl.ALGO_AUTO].cpu().numpy().view(np.uint32)[idx], want)
 
 
-@pytest.mark.parametrize("flat", [0, 1])
+@pytest.mark.parametrize("flat", [0, 1, 2])
 @pytest.mark.parametrize("dir_kb", [1, 16, 1024])
 def test_hybrid_directory_budgets(torch_cuda, monkeypatch, dir_kb, flat):
     """Narrow directories (long candidate lists) and wide ones stay exact,

@@ -278,8 +278,7 @@ def emulate_hybrid(blob, info, F, n):
             if di.n_rules == 0:
                 continue
             key = KEYS[di.kind](F).astype(np.uint64)
-            dirv = blob[di.off_dir:di.off_dir + di.n_buckets + 1].astype(np.int64)
-            assert info.lds_dwords == 0 or di.off_dir + di.n_buckets + 1 <= info.lds_dwords
+            dirv = dir_values(blob, di)  # global (flat) or LDS image (flat-LDS)
             t = (key >> np.uint64(di.shift)).astype(np.int64)
             start, end = dirv[t], dirv[t + 1]
             for k in range(di.max_list):
@@ -315,7 +314,8 @@ def check_hybrid(text: str, slots: np.ndarray, n: int, dir_kb=None, monkeypatch=
     want, _ = oracle.classify_slots_which(slots, 64, n, a4, a6)
     F = fields(slots, n)
     # lane form (directories in LDS): INDEXED's inline entries; flat form: compact + cold
-    best, out = emulate(blob, info, F, n) if info.lds_dwords else emulate_hybrid(blob, info, F, n)
+    lane = info.fam[0].entry_dwords != 4  # compact 16-byte entries: a flat form
+    best, out = emulate(blob, info, F, n) if lane else emulate_hybrid(blob, info, F, n)
     sel = ~F["skip"]
     got = np.where(best != 0xFFFFFFFF, out, 0)
     np.testing.assert_array_equal(got[sel], want[sel])
@@ -327,17 +327,32 @@ def test_hybrid_matches_oracle_synthetic(cfg):
     g = synth.gen_rules(synth.SPECS[cfg], synth.RULE_SEEDS[cfg])
     n = 1 << 15
     info = check_hybrid(g.text, synth.gen_slots(g, n, synth.PACKET_SEEDS[cfg]), n)
-    assert 0 < info.lds_dwords * 4 <= 128 * 1024  # LDS directories, per-lane walks
+    assert 0 < info.lds_dwords * 4 <= 128 * 1024  # LDS directories (flat-LDS form)
     assert info.fam[0].dims[0].off_dir16 != 0  # two-level (u16) directories
 
 
-def test_hybrid_lane_form_u32_directories(monkeypatch):
-    """NFFACL_TUNE_DIR16=0: the lane form with plain u32 directories."""
+@pytest.mark.parametrize("flat", [0, 2])
+def test_hybrid_lds_forms_u32_directories(monkeypatch, flat):
+    """NFFACL_TUNE_DIR16=0: the lane form (0) and the flat-LDS form (2) with
+    plain u32 LDS directories."""
     monkeypatch.setenv("NFFACL_TUNE_DIR16", "0")
+    monkeypatch.setenv("NFFACL_TUNE_FLAT", str(flat))
     g = synth.gen_rules(synth.SPECS["c3"], synth.RULE_SEEDS["c3"])
     n = 1 << 14
     info = check_hybrid(g.text, synth.gen_slots(g, n, 41), n)
     assert info.lds_dwords > 0 and info.fam[0].dims[0].off_dir16 == 0
+    assert (info.fam[0].entry_dwords == 4) == (flat == 2)
+
+
+@pytest.mark.parametrize("cfg", ["c2", "c3", "c5"])
+def test_hybrid_lane_form(cfg, monkeypatch):
+    """NFFACL_TUNE_FLAT=0: INDEXED's inline entries walked per lane over the
+    LDS directories."""
+    monkeypatch.setenv("NFFACL_TUNE_FLAT", "0")
+    g = synth.gen_rules(synth.SPECS[cfg], synth.RULE_SEEDS[cfg])
+    n = 1 << 13
+    info = check_hybrid(g.text, synth.gen_slots(g, n, 43), n)
+    assert info.lds_dwords > 0 and info.fam[0].entry_dwords == 8
 
 
 def test_hybrid_small_directory_budget(monkeypatch):
@@ -389,12 +404,29 @@ def test_hybrid_falls_back_on_non_cidr_masks():
     assert info.algo == nffacl.ALGO_INDEXED
 
 
-def test_hybrid_policy_c5_flat():
-    """C5 (100k rules): LDS-sized directories would leave long lists, so the
-    compiler picks wide global directories (the wave-flattened form,
-    lds_dwords == 0); the structure still gives the oracle's first match."""
+def test_hybrid_policy_c5_flat(monkeypatch):
+    """C5 (100k rules): the default is the flat-LDS form (compact entries,
+    LDS directories); NFFACL_TUNE_FLAT=1 gives wide global directories
+    (lds_dwords == 0).  Both give the oracle's first match."""
     g = synth.gen_rules(synth.SPECS["c5"], synth.RULE_SEEDS["c5"])
     n = 1 << 12
-    info = check_hybrid(g.text, synth.gen_slots(g, n, synth.PACKET_SEEDS["c5"]), n)
-    assert info.lds_dwords == 0
+    slots = synth.gen_slots(g, n, synth.PACKET_SEEDS["c5"])
+    info = check_hybrid(g.text, slots, n)
+    assert 0 < info.lds_dwords * 4 <= 139 * 1024 and info.fam[0].entry_dwords == 4
     assert info.fam[0].dims[3].n_rules == 0  # sparse source-port slot folded away
+    monkeypatch.setenv("NFFACL_TUNE_FLAT", "1")
+    info = check_hybrid(g.text, slots, n)
+    assert info.lds_dwords == 0 and info.fam[0].entry_dwords == 4
+
+
+@pytest.mark.parametrize("cfg", ["c3", "c5"])
+def test_hybrid_flat_lds_form(cfg, monkeypatch):
+    """NFFACL_TUNE_FLAT=2: compact entries + cold records walked flat, with
+    the directories (two-level, absolute entry numbers in the base words)
+    as the LDS image."""
+    monkeypatch.setenv("NFFACL_TUNE_FLAT", "2")
+    g = synth.gen_rules(synth.SPECS[cfg], synth.RULE_SEEDS[cfg])
+    n = 1 << 13
+    info = check_hybrid(g.text, synth.gen_slots(g, n, 51), n)
+    assert 0 < info.lds_dwords * 4 <= 139 * 1024
+    assert info.fam[0].entry_dwords == 4 and info.fam[0].dims[0].off_dir16 != 0
