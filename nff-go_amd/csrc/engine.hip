@@ -1043,8 +1043,8 @@ static IndexedLaunch indexed_launch(const DevTable *t) {
     }
     if (t->meta.algo == NFFACL_ALGO_HYBRID && t->meta.idx4.entry_dwords == kHybEntDwords) {  // flat-LDS
         L.tm = dev::kTabFlatLds;
-        L.block = 1024u;
-        L.per_cu = 1u;
+        L.block = static_cast<uint32_t>(tune_env("NFFACL_TUNE_BLOCK", 1024));
+        L.per_cu = static_cast<uint32_t>(tune_env("NFFACL_TUNE_PER_CU", 1));
         L.lds_bytes = size_t(t->meta.lds_dwords) * sizeof(uint32_t) + sizeof(dev::FlatScratch<2>) * (L.block / 64);
         return L;
     }
