@@ -367,6 +367,7 @@ enum TableMode : int {
     kTabFlatLds = 6, // HYBRID flat-LDS: the flat walk (2 rounds in flight)
                      // over directories staged in LDS, one 1024-thread
                      // workgroup per CU, candidate scratch after the image
+    kTabFlatLds4 = 7,  // the same, 4 rounds in flight (larger scratch)
 };
 
 extern __shared__ __attribute__((aligned(16))) uint32_t lds_tab[];
@@ -766,10 +767,11 @@ __device__ __forceinline__ uint32_t classify_any(const IndexedArgs &a, const Fie
         const uint32_t lane = lane_id();
         return classify_flat<NS, R, false>(a, f, W[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)], lane);
     }
-    if (TM == kTabFlatLds) {  // scratch after the staged directories (stage_dwords: multiple of 4)
-        FlatScratch<2> *W = reinterpret_cast<FlatScratch<2> *>(lds_tab + a.stage_dwords);
+    if (TM == kTabFlatLds || TM == kTabFlatLds4) {  // scratch after the staged directories (stage_dwords: multiple of 4)
+        constexpr int R = TM == kTabFlatLds4 ? 4 : 2;
+        FlatScratch<R> *W = reinterpret_cast<FlatScratch<R> *>(lds_tab + a.stage_dwords);
         const uint32_t lane = lane_id();
-        return classify_flat<NS, 2, true>(a, f, W[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)], lane);
+        return classify_flat<NS, R, true>(a, f, W[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)], lane);
     }
     if (TM == kTabLds) return classify_indexed<NS, 1>(LdsTab{}, a, f);
     if (TM == kTabSplit) return classify_indexed<NS, 1>(SplitTab{a.tab}, a, f);
@@ -787,7 +789,7 @@ template <int NS, int TM, int MODE>
 __global__ void __launch_bounds__(1024)
 k_indexed_slots(const uint8_t *__restrict__ slots, uint32_t stride, uint64_t n, IndexedArgs a,
                 uint32_t *__restrict__ port_out, uint64_t *__restrict__ permit_out) {
-    if (TM == kTabLds || TM == kTabSplit || TM == kTabFlatLds) stage_table(a);
+    if (TM == kTabLds || TM == kTabSplit || TM == kTabFlatLds || TM == kTabFlatLds4) stage_table(a);
     const uint32_t lane = lane_id();
     const uint32_t wpb = blockDim.x >> 6;
     const uint64_t wave0 = uint64_t(blockIdx.x) * wpb + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -858,7 +860,7 @@ template <int NS, int TM>
 __global__ void __launch_bounds__(1024)
 k_indexed_frames(const uint8_t *__restrict__ frames, const uint64_t *__restrict__ desc, uint64_t n,
                  IndexedArgs a, uint32_t *__restrict__ port_out, uint64_t *__restrict__ permit_out) {
-    if (TM == kTabLds || TM == kTabSplit || TM == kTabFlatLds) stage_table(a);
+    if (TM == kTabLds || TM == kTabSplit || TM == kTabFlatLds || TM == kTabFlatLds4) stage_table(a);
     const uint32_t lane = lane_id();
     const uint32_t wpb = blockDim.x >> 6;
     const uint64_t S = uint64_t(gridDim.x) * wpb * 64;  // grid stride in packets
@@ -1042,10 +1044,13 @@ static IndexedLaunch indexed_launch(const DevTable *t) {
         return L;
     }
     if (t->meta.algo == NFFACL_ALGO_HYBRID && t->meta.idx4.entry_dwords == kHybEntDwords) {  // flat-LDS
-        L.tm = dev::kTabFlatLds;
         L.block = static_cast<uint32_t>(tune_env("NFFACL_TUNE_BLOCK", 1024));
         L.per_cu = static_cast<uint32_t>(tune_env("NFFACL_TUNE_PER_CU", 1));
-        L.lds_bytes = size_t(t->meta.lds_dwords) * sizeof(uint32_t) + sizeof(dev::FlatScratch<2>) * (L.block / 64);
+        const size_t image = size_t(t->meta.lds_dwords) * sizeof(uint32_t);
+        const size_t lds4 = image + sizeof(dev::FlatScratch<4>) * (L.block / 64);
+        const bool r4 = tune_env("NFFACL_TUNE_ROUNDS", kHybFlatLdsRounds) == 4 && lds4 <= kLdsBytes;
+        L.tm = r4 ? dev::kTabFlatLds4 : dev::kTabFlatLds;
+        L.lds_bytes = r4 ? lds4 : image + sizeof(dev::FlatScratch<2>) * (L.block / 64);
         return L;
     }
     if (t->meta.algo == NFFACL_ALGO_HYBRID) {
@@ -1106,6 +1111,7 @@ static void dispatch_indexed(int ns, int tm, F &&f) {
         case dev::kTabFlat: f(nsc, std::integral_constant<int, dev::kTabFlat>{}); break;
         case dev::kTabFlat4: f(nsc, std::integral_constant<int, dev::kTabFlat4>{}); break;
         case dev::kTabFlatLds: f(nsc, std::integral_constant<int, dev::kTabFlatLds>{}); break;
+        case dev::kTabFlatLds4: f(nsc, std::integral_constant<int, dev::kTabFlatLds4>{}); break;
         default: f(nsc, std::integral_constant<int, dev::kTabGlobal>{}); break;
         }
     };
@@ -1119,7 +1125,7 @@ int prepare_kernels() {
     static hipError_t err = hipSuccess;
     std::call_once(once, [] {
         for (int ns = 2; ns <= 4; ++ns)
-            for (int tm : {int(dev::kTabLds), int(dev::kTabSplit), int(dev::kTabFlatLds)})
+            for (int tm : {int(dev::kTabLds), int(dev::kTabSplit), int(dev::kTabFlatLds), int(dev::kTabFlatLds4)})
                 dispatch_indexed(ns, tm, [&](auto nsc, auto tmc) {
                     const hipError_t e = allow_lds_modes<decltype(nsc)::value, decltype(tmc)::value>();
                     if (e != hipSuccess) err = e;
@@ -1138,7 +1144,7 @@ static void launch_slots_tm(int mode, const IndexedLaunch &L, uint32_t grid, hip
                             uint32_t *d_port, uint64_t *d_permit) {
     const dim3 g(grid), b(L.block);
     const size_t lds = TM == dev::kTabGlobal ? 0 : L.lds_bytes;
-    if (TM == dev::kTabFlat || TM == dev::kTabFlat4 || TM == dev::kTabFlatLds) {  // built with load modes 0 and 4 only
+    if (TM == dev::kTabFlat || TM == dev::kTabFlat4 || TM == dev::kTabFlatLds || TM == dev::kTabFlatLds4) {  // built with load modes 0 and 4 only
         if (mode == 0)
             hipLaunchKernelGGL((dev::k_indexed_slots<NS, TM, 0>), g, b, lds, stream, d_slots, stride, n, a, d_port, d_permit);
         else

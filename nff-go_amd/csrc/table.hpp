@@ -112,6 +112,9 @@ constexpr size_t kHybFlatDirBytes = 1024 * 1024;
 // Largest LDS directory image of the flat-LDS form: 160 KiB minus the 16
 // waves' candidate scratch (engine.hip FlatScratch<2>, 1280 B each) and 1 KiB.
 constexpr size_t kHybLdsDirMaxBytes = 139 * 1024;
+// Rounds of candidate loads in flight in the flat-LDS walk (2 or 4; 4 needs
+// 2304 B of scratch per wave, i.e. directories <= 122 KiB at 16 waves).
+constexpr int kHybFlatLdsRounds = 2;
 // Lane-form directories are two-level: a u32 base per group of 64 buckets +
 // a u16 offset per bucket (2.06 B per bucket instead of 4), so the LDS budget
 // holds twice the buckets.  A group whose lists exceed 65535 entries keeps
