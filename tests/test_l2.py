@@ -317,3 +317,24 @@ def test_gpu_empty_and_swap(torch_cuda):
         with pytest.raises(nffacl.NFError):
             eng.classify_device(torch_cuda.zeros(64, dtype=torch_cuda.uint8, device="cuda"), 48, 1,
                                 torch_cuda.zeros(1, dtype=torch_cuda.int32, device="cuda"))
+
+
+@pytest.mark.gpu
+def test_gpu_rule_count_limit_falls_back_to_linear(torch_cuda):
+    """The cuckoo slots carry 16-bit rule indices: 65 535+ live rules compile
+    LINEAR under AUTO (and stay exact); just below the limit they hash."""
+    rng = np.random.default_rng(17)
+    n = 4096
+    slots = rng.integers(0, 256, (n, 64), dtype=np.uint8)
+    for nrules, want_algo in ((65534, nffacl.ALGO_INDEXED), (70000, nffacl.ALGO_LINEAR)):
+        eth = np.zeros(nrules, nffacl.L2RULE)
+        eth["daddr_not_any"] = True
+        eth["daddr"] = rng.integers(0, 256, (nrules, 6))
+        eth["output_number"] = rng.integers(1, 9, nrules)
+        eth["daddr"][-100:] = slots[:100, 0:6]  # late rules that packets hit
+        with nffacl.L2Engine(nffacl.L2Rules.from_array(eth)) as eng:
+            assert eng.algo == want_algo
+            p, _ = _gpu_ports(torch_cuda, eng, slots.reshape(-1), 64, n)
+        want = oracle.l2_classify_slots(slots.reshape(-1), 64, n, eth)
+        np.testing.assert_array_equal(p, want)
+        assert (want[:100] != 0).all()
