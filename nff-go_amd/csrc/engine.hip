@@ -700,31 +700,61 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
             const uint32_t ent = k + W.delta[(m - 1u) & 0xFFu];
             E[j] = G[valid[j] ? ent : 0u];
         }
+        // coarse test of every round, then the cold confirmations of all
+        // rounds together (one dependent round trip per window, not per round)
+        bool pass[R], cold[R];
+        uint32_t opt[R], opf[R];
 #pragma unroll
         for (int j = 0; j < R; ++j) {
             // the owner packet's fields
             const uint32_t o = owner[j];
             const uint32_t oks = bperm(ks, o), okd = bperm(kd, o);
-            const uint32_t opf = bperm(proto_fam, o), opt = bperm(f.ports, o);
-            const uint32_t osp = opt & 0xFFFFu, odp = opt >> 16;
+            opf[j] = bperm(proto_fam, o);
+            opt[j] = bperm(f.ports, o);
+            const uint32_t osp = opt[j] & 0xFFFFu, odp = opt[j] >> 16;
             const uint32_t pb = (1u << (16 + (osp >> kHybPortBlockShift))) | (1u << (24 + (odp >> kHybPortBlockShift)));
-            const uint32_t idx = E[j].z >> kEntIndexShift;
-            bool pass = valid[j] && hyb_pass(E[j], oks, okd, opf & 0xFFu, pb);
-            const bool cold = pass && (E[j].w & kHybCold);
-            if (ballot(cold)) {
-                // owner's IPv6 address words 1..3 (whole wave: bpermute reads every lane)
-                Fields of;
-                of.ports = opt;
-                of.is6 = (opf & 0x100u) != 0u;
+            pass[j] = valid[j] && hyb_pass(E[j], oks, okd, opf[j] & 0xFFu, pb);
+            cold[j] = pass[j] && (E[j].w & kHybCold);
+        }
+        bool any_cold = false;
 #pragma unroll
-                for (int q = 1; q < 4; ++q) {
-                    of.s[q] = bperm(f.s[q], o);
-                    of.t[q] = bperm(f.t[q], o);
-                }
-                if (cold) pass = hyb_cold_ok(a, of.is6, idx, of);
+        for (int j = 0; j < R; ++j) any_cold |= cold[j];
+        if (ballot(any_cold)) {
+            const GlobalTab g{a.tab};
+            u32x4 C[R];
+#pragma unroll
+            for (int j = 0; j < R; ++j) {  // first 16 bytes of every needed cold record
+                const uint32_t idx = E[j].z >> kEntIndexShift;
+                const bool six = (opf[j] & 0x100u) != 0u;
+                const uint32_t off = six ? a.f6.off_cold + idx * kHybCold6Dwords : a.f4.off_cold + idx * kHybCold4Dwords;
+                C[j] = u32x4{0, 0xFFFFFFFFu, 0xFFFFFFFFu, 0};
+                if (cold[j]) C[j] = g.ld4(off);
             }
+#pragma unroll
+            for (int j = 0; j < R; ++j) {
+                const bool six = (opf[j] & 0x100u) != 0u;
+                if (cold[j]) pass[j] = port_miss(opt[j], C[j].x, C[j].y) == 0u;
+                if (ballot(cold[j] && six && pass[j])) {
+                    // owner's IPv6 address words 1..3 (whole wave: bpermute reads every lane)
+                    Fields of;
+                    const uint32_t o = owner[j];
+#pragma unroll
+                    for (int q = 1; q < 4; ++q) {
+                        of.s[q] = bperm(f.s[q], o);
+                        of.t[q] = bperm(f.t[q], o);
+                    }
+                    if (cold[j] && six && pass[j]) {
+                        const uint32_t idx = E[j].z >> kEntIndexShift;
+                        pass[j] = entry_miss_ext(g, a.f6.off_cold + idx * kHybCold6Dwords + 4, of) == 0u;
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
             // rule index << 3 | output code: the minimum carries the winner's output
-            if (pass) atomicMin(&W.best[o], (idx << 3) | ((E[j].w >> kHybOutShift) & 7u));
+            const uint32_t idx = E[j].z >> kEntIndexShift;
+            if (pass[j]) atomicMin(&W.best[owner[j]], (idx << 3) | ((E[j].w >> kHybOutShift) & 7u));
         }
         wave_lds_sync();
     }
@@ -888,7 +918,7 @@ k_indexed_frames(const uint8_t *__restrict__ frames, const uint64_t *__restrict_
     // VGPRs to spare): also the next batch's 64-byte frame lines, into the
     // other of two register buffers (ping-pong, no copies), and the
     // descriptors of the batch after.
-    constexpr bool PF = TM == kTabSplit;
+    constexpr bool PF = TM == kTabSplit;  // (flat-LDS: +0.6 % on C3, profiles/r1_flat_lds/cold/)
     // Frame lines load cooperatively (load_frames_rs) and are assembled per
     // lane just before their batch is classified.
     auto run_batch = [&](uint64_t b, uint64_t ds, const u32x4(&v)[4]) {
