@@ -539,10 +539,17 @@ void build_hybrid(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vec
     const int force = fv && *fv ? std::atoi(fv) : 2;
     const char *dv = std::getenv("NFFACL_TUNE_DIR16");
     const bool want16 = !(dv && *dv && std::atoi(dv) == 0);
-    const size_t budget = tuned ? tuned : (force == 1 ? kHybFlatDirBytes : kHybLaneDirBytes);
+    size_t budget = tuned ? tuned : (force == 1 ? kHybFlatDirBytes : kHybLaneDirBytes);
     const bool lds_dirs = force != 1 && budget <= kHybLdsDirMaxBytes;
     const bool flat = force != 0 || !lds_dirs;
-    size_and_fill(all, weight, budget, lds_dirs && want16);
+    const double expect = size_and_fill(all, weight, budget, lds_dirs && want16);
+    // flat-LDS with many candidates per packet: 4 rounds in flight, whose
+    // larger scratch takes some of the directory budget
+    if (flat && lds_dirs && !tuned && expect > kHybFlat4Candidates) {
+        budget = kHybFlat4DirBytes;
+        size_and_fill(all, weight, budget, want16);
+        out.flat_rounds = 4;
+    }
     // LDS directories: two-level unless some 64-bucket group holds 65536+
     // entries (then plain u32, re-sized for the same budget)
     bool dir16 = lds_dirs && want16;
@@ -551,7 +558,7 @@ void build_hybrid(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vec
         for (size_t t = 0; t < dir.size(); ++t)
             if (dir[t] - dir[(t >> kDir16GroupShift) << kDir16GroupShift] > 0xFFFFu) { dir16 = false; break; }
     }
-    if (lds_dirs && want16 && !dir16) size_and_fill(all, weight, tuned ? tuned : kHybLaneDirBytes, false);
+    if (lds_dirs && want16 && !dir16) size_and_fill(all, weight, budget, false);
     std::vector<uint32_t> &blob = out.blob;
     FamilyIndex *fi[2] = {&out.idx4, &out.idx6};
     const std::vector<uint32_t> *recs[2] = {&rec4, &rec6};

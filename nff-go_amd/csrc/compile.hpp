@@ -47,6 +47,8 @@ struct CompiledTable {
     // directories staged in LDS.
     FamilyIndex idx4, idx6;
     uint32_t lds_dwords = 0;
+    // HYBRID flat-LDS: rounds of candidate loads in flight (2 or 4)
+    uint32_t flat_rounds = 2;
 };
 
 // Compile `rules`.  algo: NFFACL_ALGO_LINEAR, _INDEXED, _HYBRID or AUTO.

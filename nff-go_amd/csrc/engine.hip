@@ -1078,7 +1078,7 @@ static IndexedLaunch indexed_launch(const DevTable *t) {
         L.per_cu = static_cast<uint32_t>(tune_env("NFFACL_TUNE_PER_CU", 1));
         const size_t image = size_t(t->meta.lds_dwords) * sizeof(uint32_t);
         const size_t lds4 = image + sizeof(dev::FlatScratch<4>) * (L.block / 64);
-        const bool r4 = tune_env("NFFACL_TUNE_ROUNDS", kHybFlatLdsRounds) == 4 && lds4 <= kLdsBytes;
+        const bool r4 = tune_env("NFFACL_TUNE_ROUNDS", static_cast<int>(t->meta.flat_rounds)) == 4 && lds4 <= kLdsBytes;
         L.tm = r4 ? dev::kTabFlatLds4 : dev::kTabFlatLds;
         L.lds_bytes = r4 ? lds4 : image + sizeof(dev::FlatScratch<2>) * (L.block / 64);
         return L;

@@ -112,9 +112,13 @@ constexpr size_t kHybFlatDirBytes = 1024 * 1024;
 // Largest LDS directory image of the flat-LDS form: 160 KiB minus the 16
 // waves' candidate scratch (engine.hip FlatScratch<2>, 1280 B each) and 1 KiB.
 constexpr size_t kHybLdsDirMaxBytes = 139 * 1024;
-// Rounds of candidate loads in flight in the flat-LDS walk (2 or 4; 4 needs
-// 2304 B of scratch per wave, i.e. directories <= 122 KiB at 16 waves).
-constexpr int kHybFlatLdsRounds = 2;
+// Rounds of candidate loads in flight in the flat-LDS walk: 4 when the
+// expected candidates per packet exceed kHybFlat4Candidates (C5: E ≈ 10,
+// 0.855 vs 0.895 ms), else 2 (C3: E ≈ 1.3, 0.526 vs 0.541 ms;
+// profiles/r1_flat_lds/tune/).  4 rounds need 2304 B of scratch per wave,
+// so their directories get kHybFlat4DirBytes.
+constexpr double kHybFlat4Candidates = 6.0;
+constexpr size_t kHybFlat4DirBytes = 120 * 1024;
 // Lane-form directories are two-level: a u32 base per group of 64 buckets +
 // a u16 offset per bucket (2.06 B per bucket instead of 4), so the LDS budget
 // holds twice the buckets.  A group whose lists exceed 65535 entries keeps
