@@ -210,12 +210,15 @@ def cpu_baseline_l2(slots: np.ndarray, n: int, eth, budget_s: float):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "l2"])
     ap.add_argument("--algo", default="auto", choices=["auto", "linear", "indexed", "hybrid"])
     ap.add_argument("--packets", type=int, default=1 << 24, help="packets per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--timing", default="region", choices=["launch", "region"],
+                    help="HIP events around every launch, or one pair around the K launches "
+                         "(kernel_ms = region / K, inter-launch gaps included)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host", action="store_true", help="skip the PCIe-inclusive measurement")
     ap.add_argument("--no-scatter", action="store_true",
@@ -295,15 +298,24 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t_start = time.perf_counter()
-    for s in range(args.steps):
-        evs[s][0].record(stream)
-        launch()
-        evs[s][1].record(stream)
+    if args.timing == "region":
+        evs[0][0].record(stream)
+        for s in range(args.steps):
+            launch()
+        evs[0][1].record(stream)
+    else:
+        for s in range(args.steps):
+            evs[s][0].record(stream)
+            launch()
+            evs[s][1].record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
-    kms = np.array([a.elapsed_time(b) for a, b in evs])  # per-launch kernel time (ms)
+    if args.timing == "region":  # mean launch duration over the region, gaps included
+        kms = np.full(args.steps, evs[0][0].elapsed_time(evs[0][1]) / args.steps)
+    else:
+        kms = np.array([a.elapsed_time(b) for a, b in evs])  # per-launch kernel time (ms)
     elapsed = nd.max_over_ranks(elapsed, dev)
 
     # ---- spot parity check (outside timing): GPU verdicts vs oracle sample ----
