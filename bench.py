@@ -7,24 +7,33 @@ roofline.  One step = one classify launch (nffacl_classify_device, the HIP
 path) over the whole per-GPU batch of synthetic 64-byte slots already
 resident in HBM.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c1|c3|c4|c5|l2] [--algo auto|linear|indexed]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c1|c3|c4|c5|l2]
+                  [--extra c3,c5|none] [--algo auto|linear|indexed|hybrid]
 
-(`--config l2` measures the L2 ACL kernel, SURVEY.md §8f row 4 — not a
-BASELINE.json config: 256 GetL2ACLFromTextTable rules over 64 B slots.)
+At N = 1 the same process then measures the other single-GPU BASELINE.json
+configs named by --extra (default C3: 10 k rules on IMIX frames, C5: 100 k
+rules with port ranges — the "LDS rule-table tiling stress") and reports them
+under "configs", each with its own metric, roofline and CPU baseline; `value`
+stays the C2 headline.  (`--config l2` measures the L2 ACL kernel, SURVEY.md
+§8f row 4 — not a BASELINE.json config.)
 
 N > 1 runs under torch.distributed.run (one rank per GPU, RCCL): rank 0
 generates the rule file and broadcasts its bytes over RCCL (the path's one real
 exchange step, outside the timed region); every rank classifies its own
-resident shard — no data-path collective ("scaling": "weak").
+resident shard — no data-path collective ("scaling": "weak").  The
+root-scattered deployment (dist.scatter of slots / dist.gather of verdicts)
+is reported beside it as "scatter_inclusive".
 
-The JSON line carries:
-  roofline     achieved = 68 algorithmic bytes/packet (64 B read + 4 B port
-               write) x packets per launch / mean kernel time
+Every JSON record carries:
+  roofline     achieved = algorithmic bytes/packet (C2/C5: 64 B slot read +
+               4 B port write; C3: 64 B first frame line + 8 B descriptor +
+               4 B) x packets per launch / mean kernel time
                (HIP events on the launch stream); peak = 8 TB/s HBM3E;
                traffic = PMC bytes per launch from profiles/ (if collected)
-  cpu_baseline the oracle (oracle/acl_oracle.c, reference algorithm restated
-               in C) on a bounded sample of the same packets, on this host's
-               cores, rank 0 at N = 1 only
+  cpu_baseline the oracle (oracle/acl_oracle.c, the reference algorithm
+               restated in C) on a bounded sample of the same packets, on
+               this host's cores: the GPU box's CPU share (<= 16 threads,
+               `value`), all visible cores, and 1 core; rank 0 at N = 1 only
 """
 from __future__ import annotations
 
@@ -42,8 +51,14 @@ sys.path.insert(0, str(ROOT))
 import numpy as np  # noqa: E402
 
 METRIC = "Mpackets/s device-resident L3 ACL classify, 64B pkts @1k rules; % HBM roofline"
-METRIC_L2 = "Mpackets/s device-resident L2 ACL classify, 64B pkts @256 rules (SURVEY.md §8f, not a BASELINE metric)"
-BYTES_PER_PACKET = 68  # 64 B slot read + 4 B verdict write
+METRICS = {
+    "c1": "Mpackets/s device-resident L3 ACL classify, 64B pkts @firewall.conf (4 ip4 + 1 ip6 rules); % HBM roofline",
+    "c2": METRIC,
+    "c3": "Mpackets/s device-resident L3+L4 ACL classify, IMIX 64/570/1518B (7:4:1) frames @10k rules; % HBM roofline",
+    "c4": METRIC,
+    "c5": "Mpackets/s device-resident L3+L4 ACL classify, 64B pkts @100k rules with port ranges; % HBM roofline",
+    "l2": "Mpackets/s device-resident L2 ACL classify, 64B pkts @256 rules (SURVEY.md §8f, not a BASELINE metric)",
+}
 HBM_PEAK_GBPS = 8000.0
 WORKLOADS = {
     "c1": "C1 firewall.conf (4 text rules -> 4 ip4 + 1 ip6), 64B packets, device-resident",
@@ -55,10 +70,9 @@ WORKLOADS = {
 }
 ALGO_NAMES = {1: "linear", 2: "indexed", 3: "hybrid"}  # nffacl.ALGO_*
 L2_RULES = 256
-# L2 reads the 16-byte line holding the Ethernet header and writes 4 B
-BYTES_PER_PACKET_L2 = 20
-# C3 reads each frame's first 64-byte line + its 8-byte descriptor and writes 4 B
-BYTES_PER_PACKET_FRAMES = 76
+# bytes per packet: 64 B slot + 4 B verdict; L2 reads the 16-byte Ethernet
+# line + 4 B; C3 reads each frame's first 64-byte line + its 8-byte descriptor + 4 B
+BYTES_PER_PACKET = {"l2": 20, "c3": 76}
 
 
 def log(*a):
@@ -100,184 +114,115 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def cpu_baseline_frames(frames: np.ndarray, desc: np.ndarray, a4, a6, budget_s: float):
-    """C3: the oracle over the same packed IMIX frames (descriptor order)."""
-    from oracle import oracle
+def cpu_topology():
+    """(visible cores, sockets, cgroup CPU quota in cores or None)."""
     try:
-        cores = len(os.sched_getaffinity(0))
+        visible = len(os.sched_getaffinity(0))
     except AttributeError:
-        cores = os.cpu_count() or 1
-    cores = max(1, min(cores, 16))
-    n = len(desc)
-    cal = min(n, 1 << 15)
-    t = time.perf_counter()
-    oracle.classify_frames(frames, desc[:cal], a4, a6, threads=cores)
-    rate = cal / max(time.perf_counter() - t, 1e-6)
-    sample = int(min(n, max(cal, rate * budget_s)))
-    passes, done, dt = 0, 0, 0.0
-    while True:
-        t = time.perf_counter()
-        ports = oracle.classify_frames(frames, desc[:sample], a4, a6, threads=cores)
-        dt += time.perf_counter() - t
-        passes += 1
-        done += sample
-        if dt >= budget_s or passes >= 50:
-            break
-    one = min(sample, 1 << 15)
-    t1 = time.perf_counter()
-    oracle.classify_frames(frames, desc[:one], a4, a6, threads=1)
-    dt1 = time.perf_counter() - t1
-    return {
-        "value": round(done / dt / 1e6, 3), "unit": "Mpps", "cores": cores, "kind": "port",
-        "sample": f"first {sample} IMIX frames x {passes} pass(es) (oracle/acl_oracle.c = acl.go l3ACL "
-                  f"restated in C, {cores} threads, {dt:.1f}s)",
-        "single_core_mpps": round(one / dt1 / 1e6, 3),
-    }, ports[:sample]
-
-
-def cpu_baseline(slots: np.ndarray, n: int, a4, a6, budget_s: float, eth=None):
-    from oracle import oracle
-    if eth is not None:
-        return cpu_baseline_l2(slots, n, eth, budget_s)
+        visible = os.cpu_count() or 1
+    sockets = set()
     try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
-    cores = max(1, min(cores, 16))  # the GPU box's CPU share for one GPU
-    # calibrate on a small prefix, then size the sample for ~budget_s
-    cal = min(n, 1 << 15)
-    t = time.perf_counter()
-    oracle.classify_slots(slots, 64, cal, a4, a6, threads=cores)
-    rate = cal / max(time.perf_counter() - t, 1e-6)
-    sample = int(min(n, max(cal, rate * budget_s)))
-    passes, done, dt = 0, 0, 0.0
-    while True:  # whole passes over the sample until ~budget_s of CPU work
-        t = time.perf_counter()
-        ports, which = oracle.classify_slots_which(slots, 64, sample, a4, a6, threads=cores)
-        dt += time.perf_counter() - t
-        passes += 1
-        done += sample
-        if dt >= budget_s or passes >= 50:
-            break
-    t1 = time.perf_counter()
-    one = min(sample, 1 << 16)
-    oracle.classify_slots(slots, 64, one, a4, a6, threads=1)
-    dt1 = time.perf_counter() - t1
-    hit = which >= 0
-    return {
-        "value": round(done / dt / 1e6, 3), "unit": "Mpps", "cores": cores, "kind": "port",
-        "sample": f"first {sample} packets of rank 0's batch x {passes} pass(es) "
-                  f"(oracle/acl_oracle.c = acl.go l3ACL restated in C, {cores} threads, {dt:.1f}s)",
-        "single_core_mpps": round(one / dt1 / 1e6, 3),
-        "mean_first_match_index": round(float(which[hit].mean()), 1) if hit.any() else None,
-        "match_fraction": round(float(hit.mean()), 4),
-    }, ports[:sample]
-
-
-def cpu_baseline_l2(slots: np.ndarray, n: int, eth, budget_s: float):
-    from oracle import oracle
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("physical id"):
+                sockets.add(line.split(":", 1)[1].strip())
+    except OSError:
+        pass
+    quota = None
     try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
-    cores = max(1, min(cores, 16))
-    cal = min(n, 1 << 16)
-    t = time.perf_counter()
-    oracle.l2_classify_slots(slots, 64, cal, eth, threads=cores)
-    rate = cal / max(time.perf_counter() - t, 1e-6)
-    sample = int(min(n, max(cal, rate * budget_s)))
-    passes, done, dt = 0, 0, 0.0
-    while True:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = round(int(q) / int(period), 2)
+    except (OSError, ValueError):
+        pass
+    return visible, max(1, len(sockets)), quota
+
+
+def cpu_leg(run, n: int, budget_s: float, what: str, all_budget_s: float = 2.0):
+    """CPU baseline of the oracle: `run(count, threads)` classifies the first
+    `count` packets of the workload and returns their ports.  Timed at the GPU
+    box's CPU share (<= 16 threads, the reported `value`), on all visible
+    cores, and on 1 core, each over a sample sized for its time budget."""
+    visible, sockets, quota = cpu_topology()
+    box = max(1, min(visible, 16))
+
+    def timed(threads, budget):
+        cal = min(n, 1 << 14)
         t = time.perf_counter()
-        ports = oracle.l2_classify_slots(slots, 64, sample, eth, threads=cores)
-        dt += time.perf_counter() - t
-        passes += 1
-        done += sample
-        if dt >= budget_s or passes >= 50:
-            break
-    one = min(sample, 1 << 16)
-    t1 = time.perf_counter()
-    oracle.l2_classify_slots(slots, 64, one, eth, threads=1)
-    dt1 = time.perf_counter() - t1
-    return {
-        "value": round(done / dt / 1e6, 3), "unit": "Mpps", "cores": cores, "kind": "port",
-        "sample": f"first {sample} packets x {passes} pass(es) (oracle/acl_oracle.c = acl.go l2ACL "
-                  f"restated in C, {cores} threads, {dt:.1f}s)",
-        "single_core_mpps": round(one / dt1 / 1e6, 3),
-    }, ports[:sample]
+        run(cal, threads)
+        rate = cal / max(time.perf_counter() - t, 1e-6)
+        sample = int(min(n, max(cal, rate * budget)))
+        passes, done, dt, ports = 0, 0, 0.0, None
+        while True:  # whole passes over the sample until ~budget of CPU work
+            t = time.perf_counter()
+            ports = run(sample, threads)
+            dt += time.perf_counter() - t
+            passes += 1
+            done += sample
+            if dt >= budget or passes >= 50:
+                break
+        return done / dt / 1e6, sample, passes, dt, ports
+
+    v, sample, passes, dt, ports = timed(box, budget_s)
+    out = {
+        "value": round(v, 3), "unit": "Mpps", "cores": box, "kind": "port",
+        "sample": f"first {sample} {what} x {passes} pass(es) (oracle/acl_oracle.c = acl.go l3ACL "
+                  f"restated in C, {box} threads, {dt:.1f}s)",
+    }
+    v1, s1, _, _, _ = timed(1, min(budget_s, 3.0))
+    out["single_core_mpps"] = round(v1, 3)
+    if visible > box:
+        va, sa, pa, da, _ = timed(visible, all_budget_s)
+        out.update(value_all_cores=round(va, 3), cores_all=visible,
+                   sample_all_cores=f"first {sa} {what} x {pa} pass(es), {visible} threads, {da:.1f}s")
+    else:
+        out.update(value_all_cores=round(v, 3), cores_all=visible)
+    out.update(cpu_model=cpu_model(), sockets=sockets, cgroup_cpu_quota=quota)
+    return out, ports[:sample]
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=100)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "l2"])
-    ap.add_argument("--algo", default="auto", choices=["auto", "linear", "indexed", "hybrid"])
-    ap.add_argument("--packets", type=int, default=1 << 24, help="packets per GPU")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--timing", default="region", choices=["launch", "region"],
-                    help="HIP events around every launch, or one pair around the K launches "
-                         "(kernel_ms = region / K, inter-launch gaps included)")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-host", action="store_true", help="skip the PCIe-inclusive measurement")
-    ap.add_argument("--no-scatter", action="store_true",
-                    help="N>1: skip the root-scattered (scatter+classify+gather) measurement")
-    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
-                    help="process-group backend for N>1 (nccl = RCCL on ROCm)")
-    args = ap.parse_args()
-
+def run_config(cfg: str, args, rank: int, world: int, local: int, dev, nd, headline: bool):
+    """Measure one config on this rank: returns (record dict, state for the
+    headline's extra legs)."""
     import torch
     import torch.distributed as dist
     import nffacl
-    from nffacl import dist as nd
+    from nffacl import synth
+    from oracle import oracle, rules_oracle as ro
 
-    rank, world, local = nd.world()
-    if os.environ.get("NFFACL_BENCH_ONE_GPU") == "1":  # rehearse N ranks on one GPU (gloo)
-        local = 0
-    if world != args.gpus:
-        log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        nd.init(args.backend, dev)
-
-    cfg = args.config
     n = args.packets
     algo_id = {"auto": nffacl.ALGO_AUTO, "linear": nffacl.ALGO_LINEAR, "indexed": nffacl.ALGO_INDEXED,
-               "hybrid": nffacl.ALGO_HYBRID}[args.algo]
-
+               "hybrid": nffacl.ALGO_HYBRID}[args.algo if headline else "auto"]
     # ---- rules: rank 0 generates, RCCL broadcast of the rule file bytes ----
     text, gen = build_rules(cfg)
     text = nd.broadcast_rules(text if rank == 0 else None, dev)
     l2_mode = cfg == "l2"
+    frames_mode = cfg == "c3"
     if l2_mode:
         rules = nffacl.L2Rules.parse_text(text)
         n4, n6 = rules.count(), 0
         eng = nffacl.L2Engine(rules, device=local, algo=algo_id)
-        algo_name = ALGO_NAMES[eng.algo]
     else:
         rules = nffacl.L3Rules.parse_text(text)
         n4, n6 = rules.counts()
         eng = nffacl.Engine(rules, device=local, algo=algo_id)
-        algo_name = ALGO_NAMES[eng.algo]
+    algo_name = ALGO_NAMES[eng.algo]
 
     # ---- packets: per-rank shard, resident in HBM before timing ----
-    from nffacl import synth
     t0 = time.perf_counter()
-    frames_mode = cfg == "c3"
+    seed = synth.PACKET_SEEDS.get(cfg, 0) + 7919 * rank
+    slots = frames = desc = None
     if frames_mode:
-        frames, desc = synth.gen_imix(gen, n, synth.PACKET_SEEDS[cfg] + 7919 * rank)
+        frames, desc = synth.gen_imix(gen, n, seed)
         d_frames = torch.from_numpy(frames).to(dev)
         d_desc = torch.from_numpy(desc.view(np.int64)).to(dev)
-        slots = None
     elif l2_mode:
         slots = synth.gen_l2_slots(gen, n, synth.L2_PACKET_SEED + 7919 * rank)
         d_slots = torch.from_numpy(slots).to(dev)
     else:
-        slots = synth.gen_slots(gen, n, synth.PACKET_SEEDS[cfg] + 7919 * rank)
+        slots = synth.gen_slots(gen, n, seed)
         d_slots = torch.from_numpy(slots).to(dev)
-    log(f"[rank {rank}] generated {n} packets in {time.perf_counter() - t0:.1f}s; rules ip4={n4} ip6={n6}; algo={algo_name}")
+    log(f"[rank {rank}] {cfg}: generated {n} packets in {time.perf_counter() - t0:.1f}s; "
+        f"rules ip4={n4} ip6={n6}; algo={algo_name}")
     port = torch.empty(n, dtype=torch.int32, device=dev)
     permit = torch.empty((n + 63) // 64, dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream(dev)
@@ -300,7 +245,7 @@ def main():
     t_start = time.perf_counter()
     if args.timing == "region":
         evs[0][0].record(stream)
-        for s in range(args.steps):
+        for _ in range(args.steps):
             launch()
         evs[0][1].record(stream)
     else:
@@ -329,7 +274,6 @@ def main():
     elapsed = nd.max_over_ranks(elapsed, dev)
 
     # ---- spot parity check (outside timing): GPU verdicts vs oracle sample ----
-    from oracle import oracle, rules_oracle as ro
     got = port.cpu().numpy().view(np.uint32)
     rng = np.random.default_rng(rank)
     idx = np.sort(rng.choice(n, min(n, 4096), replace=False))
@@ -339,32 +283,23 @@ def main():
         want = oracle.l2_classify_slots(slots.reshape(n, 64)[idx].reshape(-1), 64, len(idx), eth, threads=4)
     else:
         a4, a6 = ro.parse_text_table(text.encode()).arrays()
-    if l2_mode:
-        pass
-    elif frames_mode:
-        want = oracle.classify_frames(frames, desc[idx], a4, a6, threads=4)
-    else:
-        want = oracle.classify_slots(slots.reshape(n, 64)[idx].reshape(-1), 64, len(idx), a4, a6, threads=4)
+        if frames_mode:
+            want = oracle.classify_frames(frames, desc[idx], a4, a6, threads=4)
+        else:
+            want = oracle.classify_slots(slots.reshape(n, 64)[idx].reshape(-1), 64, len(idx), a4, a6, threads=4)
     bit_exact = bool((got[idx] == want).all())
 
     total = n * world * args.steps
     value = total / elapsed / 1e6
     mean_k = float(kms.mean()) / 1e3
-    bpp = BYTES_PER_PACKET_FRAMES if frames_mode else BYTES_PER_PACKET_L2 if l2_mode else BYTES_PER_PACKET
+    bpp = BYTES_PER_PACKET.get(cfg, 68)
     achieved = bpp * n / mean_k / 1e9
-    out = {
-        "metric": METRIC_L2 if l2_mode else METRIC,
+    rec = {
+        "metric": METRICS[cfg],
         "value": round(value, 1),
         "unit": "Mpps",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "u32",
-        "data": "synthetic (deterministic seeds; SURVEY.md §8d mix)",
+        "steps": args.steps,
         "config": {
             "workload": WORKLOADS.get(cfg, cfg), "rules_ip4": n4, "rules_ip6": n6,
             "packets_per_gpu": n, "slot_bytes": None if frames_mode else 64,
@@ -382,17 +317,99 @@ def main():
         },
         "bit_exact_sample": bit_exact,
     }
+    state = dict(eng=eng, n=n, port=port, got=got, idx=idx, slots=slots, frames=frames, desc=desc,
+                 d_slots=None if frames_mode else d_slots, a4=a4, a6=a6, eth=eth, stream=stream,
+                 frames_mode=frames_mode, l2_mode=l2_mode)
+    return rec, state
+
+
+def cpu_baseline_for(cfg: str, st: dict, budget_s: float):
+    from oracle import oracle
+    a4, a6, n = st["a4"], st["a6"], st["n"]
+    if st["l2_mode"]:
+        slots, eth = st["slots"], st["eth"]
+        return cpu_leg(lambda c, t: oracle.l2_classify_slots(slots, 64, c, eth, threads=t), n, budget_s,
+                       "packets")
+    if st["frames_mode"]:
+        frames, desc = st["frames"], st["desc"]
+        return cpu_leg(lambda c, t: oracle.classify_frames(frames, desc[:c], a4, a6, threads=t), n, budget_s,
+                       "IMIX frames")
+    slots = st["slots"]
+    cb, ports = cpu_leg(lambda c, t: oracle.classify_slots(slots, 64, c, a4, a6, threads=t), n, budget_s,
+                        "packets of rank 0's batch")
+    m = min(n, 1 << 20)  # match statistics of the workload
+    _, which = oracle.classify_slots_which(slots, 64, m, a4, a6, threads=16)
+    hit = which >= 0
+    cb["mean_first_match_index"] = round(float(which[hit].mean()), 1) if hit.any() else None
+    cb["match_fraction"] = round(float(hit.mean()), 4)
+    return cb, ports
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "l2"])
+    ap.add_argument("--extra", default="c3,c5",
+                    help="N=1: further configs measured in the same process (comma list, or 'none')")
+    ap.add_argument("--algo", default="auto", choices=["auto", "linear", "indexed", "hybrid"])
+    ap.add_argument("--packets", type=int, default=1 << 24, help="packets per GPU")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--timing", default="region", choices=["launch", "region"],
+                    help="HIP events around every launch, or one pair around the K launches "
+                         "(kernel_ms = region / K, inter-launch gaps included)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host", action="store_true", help="skip the PCIe-inclusive measurement")
+    ap.add_argument("--no-scatter", action="store_true",
+                    help="N>1: skip the root-scattered (scatter+classify+gather) measurement")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend for N>1 (nccl = RCCL on ROCm)")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    from nffacl import dist as nd
+
+    rank, world, local = nd.world()
+    if os.environ.get("NFFACL_BENCH_ONE_GPU") == "1":  # rehearse N ranks on one GPU (gloo)
+        local = 0
+    if world != args.gpus:
+        log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        nd.init(args.backend, dev)
+
+    cfg = args.config
+    rec, st = run_config(cfg, args, rank, world, local, dev, nd, headline=True)
+    out = {
+        "metric": rec["metric"], "value": rec["value"], "unit": "Mpps", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": rec["ms_per_step"],
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+        "data": "synthetic (deterministic seeds; SURVEY.md §8d mix)",
+        "config": rec["config"], "roofline": rec["roofline"], "bit_exact_sample": rec["bit_exact_sample"],
+    }
+    ok = rec["bit_exact_sample"]
+    eng, n, got, idx = st["eng"], st["n"], st["got"], st["idx"]
 
     # ---- N>1: root-scattered curve (SURVEY.md §8e curve 2; not `value`) ----
-    # rank 0's resident batch is scattered over RCCL/xGMI, classified on every
-    # rank, verdicts gathered back; bit-exact vs rank 0's own classify above.
-    if world > 1 and not args.no_scatter and not frames_mode and not l2_mode:
+    # rank 0's resident batch goes out with one dist.scatter (RCCL: the
+    # root's sends to all peers concurrently over xGMI), every rank classifies
+    # its shard, verdicts come back with one dist.gather; bit-exact vs rank
+    # 0's own classify of the whole batch above.
+    if world > 1:
+        out["rccl_ranks"] = dist.get_world_size()
+        out["backend"] = dist.get_backend()
+    if world > 1 and not args.no_scatter and not st["frames_mode"] and not st["l2_mode"]:
+        stream = st["stream"]
+
         def classify_shard(sl, cnt):
             sl = sl.to(dev)  # gloo rehearsal: shards arrive in host memory
             p = torch.empty(cnt, dtype=torch.int32, device=dev)
             eng.classify_device(sl, 64, cnt, p, None, stream)
             return p
-        root = d_slots if rank == 0 else None
+        root = st["d_slots"] if rank == 0 else None
         nd.scatter_classify_gather(root, n, 64, classify_shard, dev)  # warm-up
         times = []
         for _ in range(3):
@@ -402,13 +419,14 @@ def main():
             best = min(times)
             out["scatter_inclusive"] = {
                 "mpps": round(n / best / 1e6, 1), "ms": round(best * 1e3, 3), "packets": n,
-                "bytes_scattered": n * 64, "bit_exact_vs_local": bool(torch.equal(full.cpu(), port.cpu())),
+                "bytes_scattered": n * 64, "collectives": "dist.scatter + dist.gather",
+                "bit_exact_vs_local": bool(torch.equal(full.cpu(), st["port"].cpu())),
             }
 
     # ---- PCIe-inclusive rate (not `value`) ----
-    if rank == 0 and not args.no_host and not frames_mode:
+    if rank == 0 and not args.no_host and not st["frames_mode"]:
         m = min(n, 1 << 22)
-        pinned = torch.from_numpy(slots[: m * 64]).pin_memory().numpy()
+        pinned = torch.from_numpy(st["slots"][: m * 64]).pin_memory().numpy()
         eng.classify_host(pinned, 64, m)
         t = time.perf_counter()
         hp, _ = eng.classify_host(pinned, 64, m)
@@ -417,22 +435,37 @@ def main():
         out["host_inclusive_bit_exact_sample"] = bool((hp[idx[idx < m]] == got[idx[idx < m]]).all())
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        if frames_mode:
-            cb, cports = cpu_baseline_frames(frames, desc, a4, a6, args.cpu_seconds)
-        else:
-            cb, cports = cpu_baseline(slots, n, a4, a6, args.cpu_seconds, eth)
+        cb, cports = cpu_baseline_for(cfg, st, args.cpu_seconds)
         cb["bit_exact_vs_gpu"] = bool((cports == got[: len(cports)]).all())
-        cb["cpu_model"] = cpu_model()
         out["cpu_baseline"] = cb
+        ok = ok and cb["bit_exact_vs_gpu"]
     elif rank == 0:
         out["cpu_baseline"] = None
+    eng.close()
+    del st
+
+    # ---- further single-GPU configs in the same process (N = 1) ----
+    extras = [] if args.extra in ("", "none") or world > 1 else [c for c in args.extra.split(",") if c != cfg]
+    if extras:
+        out["configs"] = {}
+    for c in extras:
+        rec, st = run_config(c, args, rank, world, local, dev, nd, headline=False)
+        if not args.no_cpu_baseline:
+            cb, cports = cpu_baseline_for(c, st, max(3.0, args.cpu_seconds * 0.6))
+            cb["bit_exact_vs_gpu"] = bool((cports == st["got"][: len(cports)]).all())
+            rec["cpu_baseline"] = cb
+            ok = ok and cb["bit_exact_vs_gpu"]
+        ok = ok and rec["bit_exact_sample"]
+        out["configs"][c] = rec
+        st["eng"].close()
+        del st
+        torch.cuda.empty_cache()
 
     if rank == 0:
         print(json.dumps(out), flush=True)
-    eng.close()
     if world > 1:
         dist.destroy_process_group()
-    return 0 if bit_exact else 1
+    return 0 if ok else 1
 
 
 if __name__ == "__main__":

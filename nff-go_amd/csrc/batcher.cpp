@@ -52,7 +52,8 @@ void launch_one(nffacl_batcher *b, std::unique_lock<std::mutex> &lk) {
     while (x.written.load(std::memory_order_acquire) < n) std::this_thread::yield();  // copies in progress
     // zero-copy: the kernel reads the mapped slots and writes the mapped ports
     hipError_t e = hipSuccess;
-    int st = launch_slots(b->eng, acquire_table(b->eng), x.d_slots, b->stride, n, x.d_port, nullptr, x.stream);
+    const TablePtr t = acquire_table(b->eng);  // held while enqueued; the launch records its use
+    int st = launch_slots(b->eng, t.get(), x.d_slots, b->stride, n, x.d_port, nullptr, x.stream);
     if (st == NFFACL_OK) e = hipEventRecord(x.done, x.stream);
     lk.lock();
     if (e != hipSuccess || st != NFFACL_OK) {

@@ -91,13 +91,29 @@ int parse_with(const char *text, size_t len, R **out, char *err, size_t errlen, 
     return finish_parse(ok, r, pe, out, err, errlen);
 }
 
-bool pointer_is_pinned(const void *p) {
-    hipPointerAttribute_t attr;
-    if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+// True iff all of [p, p + bytes) is page-locked host memory of ONE
+// allocation (DMA-able as a single copy); otherwise the caller stages it.
+bool range_is_pinned(const void *p, size_t bytes) {
+    if (bytes == 0) return false;
+    hipPointerAttribute_t a, b;
+    const void *last = static_cast<const uint8_t *>(p) + bytes - 1;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess || hipPointerGetAttributes(&b, last) != hipSuccess) {
         (void)hipGetLastError();
         return false;
     }
-    return attr.type == hipMemoryTypeHost;
+    if (a.type != hipMemoryTypeHost || b.type != hipMemoryTypeHost || !a.devicePointer || !b.devicePointer)
+        return false;
+    // one allocation: its device alias is contiguous over the range
+    const uintptr_t da = reinterpret_cast<uintptr_t>(a.devicePointer), db = reinterpret_cast<uintptr_t>(b.devicePointer);
+    if (db - da != bytes - 1) return false;
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    if (hipMemGetAddressRange(&base, &size, a.devicePointer) != hipSuccess) {
+        (void)hipGetLastError();
+        return true;  // the runtime does not track host ranges: the endpoint checks above stand
+    }
+    const uintptr_t lo = reinterpret_cast<uintptr_t>(base);
+    return da >= lo && db < lo + size;
 }
 
 }  // namespace
@@ -186,7 +202,12 @@ int nffacl_table_compile(const nffacl_rules *rules, int algo, uint32_t *blob, ui
     if (!rules || !info) return NFFACL_ERR_INVALID_ARG;
     CompiledTable ct;
     std::string err;
-    if (!compile_table(*rules, algo, ct, err)) {
+    CompileOptions opt;  // tooling: the layout knobs are read per call
+    if (!CompileOptions::from_env(opt, err)) {
+        set_last_error("tuning knob: " + err);
+        return NFFACL_ERR_INVALID_ARG;
+    }
+    if (!compile_table(*rules, algo, opt, ct, err)) {
         set_last_error("compile: " + err);
         return NFFACL_ERR_INVALID_ARG;
     }
@@ -235,16 +256,26 @@ int nffacl_engine_create_ex(int hip_device, const nffacl_rules *rules, int algo,
     if (!eng) return NFFACL_ERR_NOMEM;
     eng->device = hip_device;
     eng->algo_req = algo;
+    std::string terr;
+    if (!Tune::from_env(eng->tune, terr)) {  // read once; never on the launch path
+        set_last_error("tuning knob: " + terr);
+        delete eng;
+        return NFFACL_ERR_INVALID_ARG;
+    }
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, hip_device) == hipSuccess && cus > 0)
         eng->num_cus = cus;
-    DevTable *t = nullptr;
-    int st = upload_table(hip_device, *rules, algo, t);
+    hipError_t e = eng->home.init(hip_device);
+    if (e != hipSuccess) {
+        set_last_error(std::string("engine stream: ") + hipGetErrorString(e));
+        delete eng;
+        return NFFACL_ERR_HIP;
+    }
+    int st = upload_table(eng, *rules, eng->active);
     if (st != NFFACL_OK) {
         delete eng;
         return st;
     }
-    eng->active = t;
     *out = eng;
     return NFFACL_OK;
 }
@@ -255,31 +286,32 @@ int nffacl_engine_create(int hip_device, const nffacl_rules *rules, nffacl_engin
 
 int nffacl_engine_swap_rules(nffacl_engine *eng, const nffacl_rules *rules) {
     if (!eng || !rules) return NFFACL_ERR_INVALID_ARG;
-    DevTable *t = nullptr;
-    int st = upload_table(eng->device, *rules, eng->algo_req, t);
+    TablePtr t;
+    int st = upload_table(eng, *rules, t);
     if (st != NFFACL_OK) return st;
-    DevTable *old_retired = nullptr;
     {
         std::lock_guard<std::mutex> g(eng->table_mu);
-        old_retired = eng->retired;
-        eng->retired = eng->active;
-        eng->active = t;
+        eng->active.swap(t);
     }
-    if (old_retired) {
-        // Launches that used it were issued before the previous swap returned.
-        HIP_CHECK(hipSetDevice(eng->device));
-        HIP_CHECK(hipDeviceSynchronize());
-        delete old_retired;
-    }
+    // `t` is now the previous table: dropping this reference retires it once
+    // no launch / host pipeline / batcher holds it any more — its blob is
+    // freed stream-ordered behind the completion events of the work enqueued
+    // with it (tables.hpp), without blocking any stream.
+    t.reset();
+    eng->home.reap(false);  // release earlier retirees whose work has completed
     return NFFACL_OK;
 }
 
 void nffacl_engine_destroy(nffacl_engine *eng) {
     if (!eng) return;
     (void)hipSetDevice(eng->device);
-    (void)hipDeviceSynchronize();
-    delete eng->active;
-    delete eng->retired;
+    // no classification may be running (header contract): the engine's own
+    // streams are synchronised, the table retires behind the user streams'
+    // recorded work, and home.shutdown() waits for exactly that
+    for (int b = 0; b < 2; ++b)
+        if (eng->streams[b]) (void)hipStreamSynchronize(eng->streams[b]);
+    eng->active.reset();
+    eng->home.shutdown();
     for (int b = 0; b < 2; ++b) {
         if (eng->h_stage[b]) (void)hipHostFree(eng->h_stage[b]);
         if (eng->h_port[b]) (void)hipHostFree(eng->h_port[b]);
@@ -292,13 +324,16 @@ void nffacl_engine_destroy(nffacl_engine *eng) {
 }
 
 int nffacl_engine_algo(const nffacl_engine *eng) {
-    if (!eng || !eng->active) return NFFACL_ERR_INVALID_ARG;
-    return eng->active->meta.algo;
+    if (!eng) return NFFACL_ERR_INVALID_ARG;
+    const TablePtr t = acquire_table(const_cast<nffacl_engine *>(eng));
+    return t ? t->meta.algo : NFFACL_ERR_INVALID_ARG;
 }
 
 int nffacl_engine_table_bytes(const nffacl_engine *eng, uint64_t *bytes) {
-    if (!eng || !eng->active || !bytes) return NFFACL_ERR_INVALID_ARG;
-    *bytes = eng->active->bytes;
+    if (!eng || !bytes) return NFFACL_ERR_INVALID_ARG;
+    const TablePtr t = acquire_table(const_cast<nffacl_engine *>(eng));
+    if (!t) return NFFACL_ERR_INVALID_ARG;
+    *bytes = t->bytes;
     return NFFACL_OK;
 }
 
@@ -320,7 +355,8 @@ int nffacl_classify_device_ex(nffacl_engine *eng, const uint8_t *d_slots, uint32
         return NFFACL_ERR_INVALID_ARG;
     if (!d_port && !d_permit_bits) return NFFACL_OK;
     HIP_CHECK(hipSetDevice(eng->device));
-    return launch_slots(eng, acquire_table(eng), d_slots, stride, n, d_port, d_permit_bits,
+    const TablePtr t = acquire_table(eng);  // held while the launch is enqueued
+    return launch_slots(eng, t.get(), d_slots, stride, n, d_port, d_permit_bits,
                         static_cast<hipStream_t>(stream), flags);
 }
 
@@ -338,7 +374,8 @@ int nffacl_classify_frames_device_ex(nffacl_engine *eng, const uint8_t *d_frames
         return NFFACL_ERR_INVALID_ARG;
     if (!d_port && !d_permit_bits) return NFFACL_OK;
     HIP_CHECK(hipSetDevice(eng->device));
-    return launch_frames(eng, acquire_table(eng), d_frames, d_desc, n, d_port, d_permit_bits,
+    const TablePtr t = acquire_table(eng);
+    return launch_frames(eng, t.get(), d_frames, d_desc, n, d_port, d_permit_bits,
                          static_cast<hipStream_t>(stream), flags);
 }
 
@@ -384,8 +421,8 @@ int nffacl_classify_host_ex(nffacl_engine *eng, const uint8_t *h_slots, uint32_t
     HIP_CHECK(hipSetDevice(eng->device));
     int st = ensure_host_pipeline(eng, stride, n);
     if (st != NFFACL_OK) return st;
-    DevTable *t = acquire_table(eng);
-    const bool direct = pointer_is_pinned(h_slots);
+    const TablePtr t = acquire_table(eng);  // one table for every chunk of this call
+    const bool direct = range_is_pinned(h_slots, n * stride);
     const uint64_t chunk = eng->chunk;
     const uint64_t nchunks = (n + chunk - 1) / chunk;
     uint64_t pending_chunk[2] = {~0ull, ~0ull};
@@ -412,7 +449,7 @@ int nffacl_classify_host_ex(nffacl_engine *eng, const uint8_t *h_slots, uint32_t
             src = eng->h_stage[b];
         }
         HIP_CHECK(hipMemcpyAsync(eng->d_slots[b], src, cnt * stride, hipMemcpyHostToDevice, eng->streams[b]));
-        st = launch_slots(eng, t, eng->d_slots[b], stride, cnt, eng->d_port[b], nullptr, eng->streams[b], flags);
+        st = launch_slots(eng, t.get(), eng->d_slots[b], stride, cnt, eng->d_port[b], nullptr, eng->streams[b], flags);
         if (st != NFFACL_OK) return st;
         HIP_CHECK(hipMemcpyAsync(eng->h_port[b], eng->d_port[b], cnt * 4, hipMemcpyDeviceToHost, eng->streams[b]));
         HIP_CHECK(hipEventRecord(eng->done[b], eng->streams[b]));
@@ -468,9 +505,15 @@ int nffacl_l2_engine_create(int hip_device, const nffacl_l2rules *rules, nffacl_
     return nffacl_l2_engine_create_ex(hip_device, rules, NFFACL_ALGO_AUTO, out);
 }
 
+static L2TablePtr acquire_l2(nffacl_l2engine *eng) {
+    std::lock_guard<std::mutex> g(eng->table_mu);
+    return eng->active;
+}
+
 int nffacl_l2_engine_algo(const nffacl_l2engine *eng) {
-    if (!eng || !eng->active) return NFFACL_ERR_INVALID_ARG;
-    return eng->active->meta.algo;
+    if (!eng) return NFFACL_ERR_INVALID_ARG;
+    const L2TablePtr t = acquire_l2(const_cast<nffacl_l2engine *>(eng));
+    return t ? t->meta.algo : NFFACL_ERR_INVALID_ARG;
 }
 
 int nffacl_l2_engine_create_ex(int hip_device, const nffacl_l2rules *rules, int algo, nffacl_l2engine **out) {
@@ -492,55 +535,57 @@ int nffacl_l2_engine_create_ex(int hip_device, const nffacl_l2rules *rules, int 
     if (!eng) return NFFACL_ERR_NOMEM;
     eng->device = hip_device;
     eng->algo_req = algo;
+    long v = 0;
+    bool set = false;
+    std::string terr;
+    if (!env_knob("NFFACL_TUNE_L2_COAL", 0, 1, v, set, terr)) {  // read once; never on the launch path
+        set_last_error("tuning knob: " + terr);
+        delete eng;
+        return NFFACL_ERR_INVALID_ARG;
+    }
+    if (set) eng->coal = v != 0;
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, hip_device) == hipSuccess && cus > 0)
         eng->num_cus = cus;
-    L2Table *t = nullptr;
-    int st = upload_l2(hip_device, *rules, algo, t);
+    hipError_t e = eng->home.init(hip_device);
+    if (e != hipSuccess) {
+        set_last_error(std::string("engine stream: ") + hipGetErrorString(e));
+        delete eng;
+        return NFFACL_ERR_HIP;
+    }
+    int st = upload_l2(eng, *rules, eng->active);
     if (st != NFFACL_OK) {
         delete eng;
         return st;
     }
-    eng->active = t;
     *out = eng;
     return NFFACL_OK;
 }
 
 int nffacl_l2_engine_swap_rules(nffacl_l2engine *eng, const nffacl_l2rules *rules) {
     if (!eng || !rules) return NFFACL_ERR_INVALID_ARG;
-    L2Table *t = nullptr;
-    int st = upload_l2(eng->device, *rules, eng->algo_req, t);
+    L2TablePtr t;
+    int st = upload_l2(eng, *rules, t);
     if (st != NFFACL_OK) return st;
-    L2Table *old_retired = nullptr;
     {
         std::lock_guard<std::mutex> g(eng->table_mu);
-        old_retired = eng->retired;
-        eng->retired = eng->active;
-        eng->active = t;
+        eng->active.swap(t);
     }
-    if (old_retired) {
-        HIP_CHECK(hipSetDevice(eng->device));
-        HIP_CHECK(hipDeviceSynchronize());
-        delete old_retired;
-    }
+    t.reset();  // retires the previous table behind its recorded work (tables.hpp)
+    eng->home.reap(false);
     return NFFACL_OK;
 }
 
 void nffacl_l2_engine_destroy(nffacl_l2engine *eng) {
     if (!eng) return;
     (void)hipSetDevice(eng->device);
-    (void)hipDeviceSynchronize();
-    delete eng->active;
-    delete eng->retired;
+    if (eng->stream) (void)hipStreamSynchronize(eng->stream);
+    eng->active.reset();
+    eng->home.shutdown();
     if (eng->d_slots) (void)hipFree(eng->d_slots);
     if (eng->d_port) (void)hipFree(eng->d_port);
     if (eng->stream) (void)hipStreamDestroy(eng->stream);
     delete eng;
-}
-
-static L2Table *acquire_l2(nffacl_l2engine *eng) {
-    std::lock_guard<std::mutex> g(eng->table_mu);
-    return eng->active;
 }
 
 int nffacl_l2_classify_device(nffacl_l2engine *eng, const uint8_t *d_slots, uint32_t stride, uint64_t n,
@@ -551,7 +596,8 @@ int nffacl_l2_classify_device(nffacl_l2engine *eng, const uint8_t *d_slots, uint
         return NFFACL_ERR_INVALID_ARG;
     if (!d_port && !d_permit_bits) return NFFACL_OK;
     HIP_CHECK(hipSetDevice(eng->device));
-    return l2_launch_slots(eng, acquire_l2(eng), d_slots, stride, n, d_port, d_permit_bits,
+    const L2TablePtr t = acquire_l2(eng);
+    return l2_launch_slots(eng, t.get(), d_slots, stride, n, d_port, d_permit_bits,
                            static_cast<hipStream_t>(stream));
 }
 
@@ -562,7 +608,8 @@ int nffacl_l2_classify_frames_device(nffacl_l2engine *eng, const uint8_t *d_fram
     if (!d_frames || !d_desc || (reinterpret_cast<uintptr_t>(d_frames) % 16) != 0) return NFFACL_ERR_INVALID_ARG;
     if (!d_port && !d_permit_bits) return NFFACL_OK;
     HIP_CHECK(hipSetDevice(eng->device));
-    return l2_launch_frames(eng, acquire_l2(eng), d_frames, d_desc, n, d_port, d_permit_bits,
+    const L2TablePtr t = acquire_l2(eng);
+    return l2_launch_frames(eng, t.get(), d_frames, d_desc, n, d_port, d_permit_bits,
                             static_cast<hipStream_t>(stream));
 }
 
@@ -596,7 +643,8 @@ int nffacl_l2_classify_host(nffacl_l2engine *eng, const uint8_t *h_slots, uint32
         port = tmp.data();
     }
     HIP_CHECK(hipMemcpyAsync(eng->d_slots, h_slots, n * stride, hipMemcpyHostToDevice, eng->stream));
-    int st = l2_launch_slots(eng, acquire_l2(eng), eng->d_slots, stride, n, eng->d_port, nullptr, eng->stream);
+    const L2TablePtr t = acquire_l2(eng);
+    int st = l2_launch_slots(eng, t.get(), eng->d_slots, stride, n, eng->d_port, nullptr, eng->stream);
     if (st != NFFACL_OK) return st;
     HIP_CHECK(hipMemcpyAsync(port, eng->d_port, n * 4, hipMemcpyDeviceToHost, eng->stream));
     HIP_CHECK(hipStreamSynchronize(eng->stream));

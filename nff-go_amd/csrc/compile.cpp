@@ -484,13 +484,6 @@ void fill_lists(DimBuild &d) {
             d.ents[fill[t]++] = d.rules[i];
 }
 
-// Directory budget override (tuning experiments); 0 = the default policy.
-size_t tuned_dir_budget() {
-    const char *v = std::getenv("NFFACL_TUNE_DIR_KB");
-    const long kb = v && *v ? std::atol(v) : 0;
-    return kb > 0 ? size_t(kb) * 1024 : 0;
-}
-
 // Radix widths for `budget` bytes of directories, then the bucket lists;
 // returns the expected candidates per packet (mean list length summed over
 // the slots, families weighted by their share of the rules).
@@ -514,7 +507,7 @@ double size_and_fill(DimBuild *const *all, const double *weight, size_t budget, 
 }
 
 void build_hybrid(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vector<uint32_t> &rec6, uint32_t n6,
-                  CompiledTable &out) {
+                  const CompileOptions &opt, CompiledTable &out) {
     FamilyPlan plan[2];
     assign_family(rec4, kRec4Dwords, false, n4, plan[0]);
     assign_family(rec6, kRec6Dwords, true, n6, plan[1]);
@@ -529,16 +522,13 @@ void build_hybrid(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vec
     // for LDS directories replicate short prefixes across far fewer buckets
     // and stay nearly L2-resident (C5: 3.8 MB of entries instead of ~10 MB),
     // profiles/r1_flat_lds/.
-    // Tuning overrides (experiments, tests; unset in production):
-    // NFFACL_TUNE_DIR_KB sets the directory budget, NFFACL_TUNE_FLAT forces
-    // the form (0 lane: INDEXED's inline entries walked per lane; 1 flat
-    // with global directories; 2 flat-LDS); directory budgets past LDS size
-    // always give the global flat form.
-    const size_t tuned = tuned_dir_budget();
-    const char *fv = std::getenv("NFFACL_TUNE_FLAT");
-    const int force = fv && *fv ? std::atoi(fv) : 2;
-    const char *dv = std::getenv("NFFACL_TUNE_DIR16");
-    const bool want16 = !(dv && *dv && std::atoi(dv) == 0);
+    // Tuning overrides (CompileOptions; experiments, tests): dir_bytes sets
+    // the directory budget, flat forces the form (0 lane: INDEXED's inline
+    // entries walked per lane; 1 flat with global directories; 2 flat-LDS);
+    // directory budgets past LDS size always give the global flat form.
+    const size_t tuned = opt.dir_bytes;
+    const int force = opt.flat;
+    const bool want16 = opt.dir16;
     size_t budget = tuned ? tuned : (force == 1 ? kHybFlatDirBytes : kHybLaneDirBytes);
     const bool lds_dirs = force != 1 && budget <= kHybLdsDirMaxBytes;
     const bool flat = force != 0 || !lds_dirs;
@@ -642,7 +632,35 @@ bool indexable(const nffacl_rules &rules) {
 
 }  // namespace
 
-bool compile_table(const nffacl_rules &rules, int algo, CompiledTable &out, std::string &err) {
+bool env_knob(const char *name, long lo, long hi, long &v, bool &set, std::string &err) {
+    const char *s = std::getenv(name);
+    set = s && *s;
+    if (!set) return true;
+    char *end = nullptr;
+    v = std::strtol(s, &end, 10);
+    if (*end != '\0' || v < lo || v > hi) {
+        err = std::string(name) + "=" + s + ": expected an integer in [" + std::to_string(lo) + ", " +
+              std::to_string(hi) + "]";
+        return false;
+    }
+    return true;
+}
+
+bool CompileOptions::from_env(CompileOptions &o, std::string &err) {
+    o = CompileOptions{};
+    long v = 0;
+    bool set = false;
+    if (!env_knob("NFFACL_TUNE_FLAT", 0, 2, v, set, err)) return false;
+    if (set) o.flat = static_cast<int>(v);
+    if (!env_knob("NFFACL_TUNE_DIR_KB", 1, 1 << 20, v, set, err)) return false;
+    if (set) o.dir_bytes = size_t(v) * 1024;
+    if (!env_knob("NFFACL_TUNE_DIR16", 0, 1, v, set, err)) return false;
+    if (set) o.dir16 = v != 0;
+    return true;
+}
+
+bool compile_table(const nffacl_rules &rules, int algo, const CompileOptions &opt, CompiledTable &out,
+                   std::string &err) {
     if (algo != NFFACL_ALGO_AUTO && algo != NFFACL_ALGO_LINEAR && algo != NFFACL_ALGO_INDEXED &&
         algo != NFFACL_ALGO_HYBRID) {
         err = "unknown algorithm";
@@ -663,7 +681,7 @@ bool compile_table(const nffacl_rules &rules, int algo, CompiledTable &out, std:
     if (algo == NFFACL_ALGO_HYBRID && !hybrid_encodable(rec4, out.n4, rec6, out.n6)) algo = NFFACL_ALGO_INDEXED;
     if (algo == NFFACL_ALGO_HYBRID) {
         out.algo = NFFACL_ALGO_HYBRID;
-        build_hybrid(rec4, out.n4, rec6, out.n6, out);
+        build_hybrid(rec4, out.n4, rec6, out.n6, opt, out);
     } else if (algo != NFFACL_ALGO_LINEAR && indexable(rules)) {
         out.algo = NFFACL_ALGO_INDEXED;
         build_family(rec4, kRec4Dwords, false, out.n4, out.blob, out.idx4);
@@ -675,7 +693,7 @@ bool compile_table(const nffacl_rules &rules, int algo, CompiledTable &out, std:
             out.n4 = n4;
             out.n6 = n6;
             out.algo = NFFACL_ALGO_HYBRID;
-            build_hybrid(rec4, n4, rec6, n6, out);
+            build_hybrid(rec4, n4, rec6, n6, opt, out);
         }
     } else {
         out.algo = NFFACL_ALGO_LINEAR;

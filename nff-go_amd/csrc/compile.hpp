@@ -2,6 +2,7 @@
 // table blob (internal to libnffacl).
 #pragma once
 
+#include <cstddef>
 #include <cstdint>
 #include <string>
 #include <vector>
@@ -51,7 +52,21 @@ struct CompiledTable {
     uint32_t flat_rounds = 2;
 };
 
+// Table-layout overrides for tuning experiments (unset in production).
+struct CompileOptions {
+    int flat = 2;           // NFFACL_TUNE_FLAT: HYBRID form 0 lane, 1 flat (global dirs), 2 flat-LDS
+    size_t dir_bytes = 0;   // NFFACL_TUNE_DIR_KB: HYBRID directory budget (0 = policy)
+    bool dir16 = true;      // NFFACL_TUNE_DIR16: two-level u16 LDS directories allowed
+    // false (+ `err`) if a set variable is out of range
+    static bool from_env(CompileOptions &o, std::string &err);
+};
+
+// Integer environment variable in [lo, hi]: false (+ `err`) if set but
+// malformed or out of range; `set` says whether it was set.
+bool env_knob(const char *name, long lo, long hi, long &v, bool &set, std::string &err);
+
 // Compile `rules`.  algo: NFFACL_ALGO_LINEAR, _INDEXED, _HYBRID or AUTO.
-bool compile_table(const nffacl_rules &rules, int algo, CompiledTable &out, std::string &err);
+bool compile_table(const nffacl_rules &rules, int algo, const CompileOptions &opt, CompiledTable &out,
+                   std::string &err);
 
 }  // namespace nffacl

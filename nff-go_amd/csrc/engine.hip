@@ -260,23 +260,44 @@ __device__ __forceinline__ void transpose_batch(const u32x4 (&v)[4], uint32_t la
 // Row-swap variant (MODE 4): load_rowswap / rowswap_batch, devutil.hpp.
 
 // Packed frames, the same layout: for instruction j lane 16r + c loads chunk
-// r of frame 16j + c (that frame's offset fetched from lane 16j + c with
+// r of frame 16j + c (that frame's descriptor fetched from lane 16j + c with
 // ds_bpermute), so every instruction consumes whole 64-byte frame lines and
 // non-temporal loads pay off; rowswap_batch then gives lane l the first 64
 // bytes of its own frame.  (sol `frames_rs_nt` 0.293 ms vs 0.340 ms for one
 // frame per lane, C3 IMIX, profiles/r1_frames_rs/.)  Every lane of the wave
-// must be active; `off` is this lane's frame offset (any valid offset for
-// lanes past the batch end).
-__device__ __forceinline__ void load_frames_rs(const uint8_t *__restrict__ frames, uint64_t off, uint32_t lane,
+// must be active; `ds` is this lane's descriptor (offset << 16 | length; 0
+// for lanes past the batch end).  A chunk is read only if it starts inside
+// its frame: a 16-byte aligned load that starts at a frame byte stays in
+// that byte's page, so nothing past the last frame of the buffer is touched.
+__device__ __forceinline__ void load_frames_rs(const uint8_t *__restrict__ frames, uint64_t ds, uint32_t lane,
                                                u32x4 (&v)[4]) {
-    const uint32_t lo = static_cast<uint32_t>(off), hi = static_cast<uint32_t>(off >> 32);
+    const uint32_t lo = static_cast<uint32_t>(ds), hi = static_cast<uint32_t>(ds >> 32);
+    const uint32_t chunk = 16u * (lane >> 4);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const int src = static_cast<int>((16u * j + (lane & 15u)) << 2);
-        const uint64_t o = uint64_t(static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(lo)))) |
-                           uint64_t(static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(hi)))) << 32;
-        v[j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(frames + o) + (lane >> 4));
+        const uint32_t l = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(lo)));
+        const uint32_t h = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(hi)));
+        const uint64_t o = (uint64_t(h) << 32 | l) >> 16;
+        v[j] = u32x4{0, 0, 0, 0};
+        if (chunk < (l & 0xFFFFu)) v[j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(frames + o) + (lane >> 4));
     }
+}
+
+// One lane's frame: the first 64 bytes, chunks past `len` not read (see
+// load_frames_rs), then bytes past `len` zeroed.
+__device__ __forceinline__ void load16_frame(const uint8_t *__restrict__ p, uint32_t len, uint32_t (&d)[16]) {
+    const u32x4 *q = reinterpret_cast<const u32x4 *>(p);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        u32x4 v = u32x4{0, 0, 0, 0};
+        if (16u * j < len) v = q[j];
+        d[4 * j + 0] = v.x;
+        d[4 * j + 1] = v.y;
+        d[4 * j + 2] = v.z;
+        d[4 * j + 3] = v.w;
+    }
+    clip16(d, len);
 }
 
 // Packet index (within the wave's 64) held by lane l after transpose_batch.
@@ -320,8 +341,7 @@ k_linear_frames(const uint8_t *__restrict__ frames, const uint64_t *__restrict__
         const uint32_t len = static_cast<uint32_t>(ds & 0xFFFFu);
         const uint8_t *pkt = frames + (ds >> 16);
         uint32_t d[16];
-        load16(pkt, d);
-        clip16(d, len);
+        load16_frame(pkt, len, d);
         Fields f;
         parse_fields(d, live, f, [&](uint32_t k, uint32_t &lo, uint32_t &hi) {
             far_dwords(pkt, len, k, lo, hi);
@@ -929,13 +949,13 @@ k_indexed_frames(const uint8_t *__restrict__ frames, const uint64_t *__restrict_
     if (PF) {
         u32x4 A[4], B[4];
         uint64_t dsA = desc_at(base), dsB = 0;
-        load_frames_rs(frames, dsA >> 16, lane, A);
+        load_frames_rs(frames, dsA, lane, A);
         uint64_t dsN = desc_at(base + S);  // descriptor of the batch after the one in flight
         while (true) {
             const uint64_t b1 = base + S;
             if (b1 < n) {
                 dsB = dsN;
-                load_frames_rs(frames, dsB >> 16, lane, B);
+                load_frames_rs(frames, dsB, lane, B);
                 dsN = desc_at(b1 + S);
             }
             run_batch(base, dsA, A);
@@ -943,7 +963,7 @@ k_indexed_frames(const uint8_t *__restrict__ frames, const uint64_t *__restrict_
             const uint64_t b2 = b1 + S;
             if (b2 < n) {
                 dsA = dsN;
-                load_frames_rs(frames, dsA >> 16, lane, A);
+                load_frames_rs(frames, dsA, lane, A);
                 dsN = desc_at(b2 + S);
             }
             run_batch(b1, dsB, B);
@@ -956,7 +976,7 @@ k_indexed_frames(const uint8_t *__restrict__ frames, const uint64_t *__restrict_
             const uint64_t ds = ds_next;
             ds_next = desc_at(base + S);
             u32x4 v[4];
-            load_frames_rs(frames, ds >> 16, lane, v);
+            load_frames_rs(frames, ds, lane, v);
             run_batch(base, ds, v);
         }
     }
@@ -968,34 +988,45 @@ k_indexed_frames(const uint8_t *__restrict__ frames, const uint64_t *__restrict_
 // Host side of the engine
 // ---------------------------------------------------------------------------
 
-DevTable::~DevTable() {
-    if (d_blob) (void)hipFree(d_blob);
+bool Tune::from_env(Tune &t, std::string &err) {
+    t = Tune{};
+    long v = 0;
+    bool set = false;
+    if (!env_knob("NFFACL_TUNE_COAL", 0, 4, v, set, err)) return false;
+    if (set) t.coal = static_cast<int>(v);
+    if (!env_knob("NFFACL_TUNE_BLOCK", 64, 1024, v, set, err)) return false;
+    if (set && v % 64 != 0) {
+        err = "NFFACL_TUNE_BLOCK: expected a multiple of 64";
+        return false;
+    }
+    if (set) t.block = static_cast<int>(v);
+    if (!env_knob("NFFACL_TUNE_PER_CU", 1, 32, v, set, err)) return false;
+    if (set) t.per_cu = static_cast<int>(v);
+    if (!env_knob("NFFACL_TUNE_ROUNDS", 2, 4, v, set, err)) return false;
+    if (set && v == 3) {
+        err = "NFFACL_TUNE_ROUNDS: expected 2 or 4";
+        return false;
+    }
+    if (set) t.rounds = static_cast<int>(v);
+    if (!env_knob("NFFACL_TUNE_LDS", 0, 1, v, set, err)) return false;
+    if (set) t.lds = static_cast<int>(v);
+    return CompileOptions::from_env(t.copt, err);
 }
 
-int upload_table(int device, const nffacl_rules &rules, int algo, DevTable *&out) {
-    CompiledTable ct;
+int upload_table(nffacl_engine *eng, const nffacl_rules &rules, TablePtr &out) {
+    auto t = std::make_shared<DevTable>();
     std::string err;
-    if (!compile_table(rules, algo, ct, err)) {
+    if (!compile_table(rules, eng->algo_req, eng->tune.copt, t->meta, err)) {
         set_last_error("compile: " + err);
         return NFFACL_ERR_INVALID_ARG;
     }
-    HIP_TRY(hipSetDevice(device));
-    DevTable *t = new DevTable();
-    t->meta = std::move(ct);
-    t->bytes = t->meta.blob.size() * sizeof(uint32_t);
-    hipError_t e = hipMalloc(reinterpret_cast<void **>(&t->d_blob), t->bytes);
+    HIP_TRY(hipSetDevice(eng->device));
+    const hipError_t e = t->upload(&eng->home, t->meta.blob.data(), t->meta.blob.size());
     if (e != hipSuccess) {
-        set_last_error(std::string("hipMalloc(table): ") + hipGetErrorString(e));
-        delete t;
-        return NFFACL_ERR_NOMEM;
+        set_last_error(std::string("table upload: ") + hipGetErrorString(e));
+        return e == hipErrorOutOfMemory ? NFFACL_ERR_NOMEM : NFFACL_ERR_HIP;
     }
-    e = hipMemcpy(t->d_blob, t->meta.blob.data(), t->bytes, hipMemcpyHostToDevice);
-    if (e != hipSuccess) {
-        set_last_error(std::string("hipMemcpy(table): ") + hipGetErrorString(e));
-        delete t;
-        return NFFACL_ERR_HIP;
-    }
-    out = t;
+    out = std::move(t);
     return NFFACL_OK;
 }
 
@@ -1035,12 +1066,6 @@ struct IndexedLaunch {
     size_t lds_bytes;
 };
 
-// Launch-shape overrides for tuning experiments (tools/sol.py); unset in production.
-static int tune_env(const char *name, int dflt) {
-    const char *v = std::getenv(name);
-    return v && *v ? std::atoi(v) : dflt;
-}
-
 // The kernel a table gets must match the layout it was compiled to: checked
 // on the host before every indexed launch (a mismatch would read the blob
 // with the wrong offsets).
@@ -1057,7 +1082,9 @@ static bool table_consistent(const DevTable *t) {
     return m.idx4.entry_dwords == kEnt4Dwords && m.idx6.entry_dwords == kEnt6Dwords;
 }
 
-static IndexedLaunch indexed_launch(const DevTable *t) {
+// Launch shape of an indexed table; Tune overrides (frozen at engine creation).
+static IndexedLaunch indexed_launch(const nffacl_engine *eng, const DevTable *t) {
+    const Tune &tu = eng->tune;
     const uint32_t used = std::max(t->meta.idx4.used_slots, t->meta.idx6.used_slots);
     const int ns = used <= 2 ? 2 : static_cast<int>(used);
     IndexedLaunch L{dev::kTabGlobal, ns, 256u, 8u, 0};
@@ -1066,19 +1093,20 @@ static IndexedLaunch indexed_launch(const DevTable *t) {
     // staged in LDS, inline entries walked per lane; flat form (lds_dwords 0):
     // directories and compact entries in global memory, candidates flat.
     if (t->meta.algo == NFFACL_ALGO_HYBRID && t->meta.lds_dwords == 0) {
-        const bool r2 = tune_env("NFFACL_TUNE_ROUNDS", 4) == 2;
+        const bool r2 = tu.rounds == 2;
         L.tm = r2 ? dev::kTabFlat : dev::kTabFlat4;
-        L.block = static_cast<uint32_t>(tune_env("NFFACL_TUNE_BLOCK", 256));
-        L.per_cu = static_cast<uint32_t>(tune_env("NFFACL_TUNE_PER_CU", 8));
+        L.block = tu.block ? static_cast<uint32_t>(tu.block) : 256u;
+        L.per_cu = tu.per_cu ? static_cast<uint32_t>(tu.per_cu) : 8u;
         L.lds_bytes = (r2 ? sizeof(dev::FlatScratch<2>) : sizeof(dev::FlatScratch<4>)) * (L.block / 64);
         return L;
     }
     if (t->meta.algo == NFFACL_ALGO_HYBRID && t->meta.idx4.entry_dwords == kHybEntDwords) {  // flat-LDS
-        L.block = static_cast<uint32_t>(tune_env("NFFACL_TUNE_BLOCK", 1024));
-        L.per_cu = static_cast<uint32_t>(tune_env("NFFACL_TUNE_PER_CU", 1));
+        L.block = tu.block ? static_cast<uint32_t>(tu.block) : 1024u;
+        L.per_cu = tu.per_cu ? static_cast<uint32_t>(tu.per_cu) : 1u;
         const size_t image = size_t(t->meta.lds_dwords) * sizeof(uint32_t);
         const size_t lds4 = image + sizeof(dev::FlatScratch<4>) * (L.block / 64);
-        const bool r4 = tune_env("NFFACL_TUNE_ROUNDS", static_cast<int>(t->meta.flat_rounds)) == 4 && lds4 <= kLdsBytes;
+        const int rounds = tu.rounds ? tu.rounds : static_cast<int>(t->meta.flat_rounds);
+        const bool r4 = rounds == 4 && lds4 <= kLdsBytes;
         L.tm = r4 ? dev::kTabFlatLds4 : dev::kTabFlatLds;
         L.lds_bytes = r4 ? lds4 : image + sizeof(dev::FlatScratch<2>) * (L.block / 64);
         return L;
@@ -1088,7 +1116,7 @@ static IndexedLaunch indexed_launch(const DevTable *t) {
         L.tm = dev::kTabSplit;
     } else {
         const size_t bytes = t->meta.blob.size() * sizeof(uint32_t);
-        if (bytes <= kLdsTableBytes && tune_env("NFFACL_TUNE_LDS", 1) != 0) {
+        if (bytes <= kLdsTableBytes && tu.lds != 0) {
             L.tm = dev::kTabLds;
             staged = bytes;
         }
@@ -1101,8 +1129,8 @@ static IndexedLaunch indexed_launch(const DevTable *t) {
                        : static_cast<uint32_t>(std::max<size_t>(1, std::min<size_t>(2, kLdsBytes / std::max<size_t>(staged, 16))));
         L.lds_bytes = std::max<size_t>(staged, 16);
     }
-    L.block = static_cast<uint32_t>(tune_env("NFFACL_TUNE_BLOCK", static_cast<int>(L.block)));
-    L.per_cu = static_cast<uint32_t>(tune_env("NFFACL_TUNE_PER_CU", static_cast<int>(L.per_cu)));
+    if (tu.block) L.block = static_cast<uint32_t>(tu.block);
+    if (tu.per_cu) L.per_cu = static_cast<uint32_t>(tu.per_cu);
     return L;
 }
 
@@ -1202,7 +1230,7 @@ static void launch_frames_tm(const IndexedLaunch &L, uint32_t grid, hipStream_t 
                        a, d_port, d_permit);
 }
 
-int launch_slots(nffacl_engine *eng, const DevTable *t, const uint8_t *d_slots, uint32_t stride,
+int launch_slots(nffacl_engine *eng, DevTable *t, const uint8_t *d_slots, uint32_t stride,
                  uint64_t n, uint32_t *d_port, uint64_t *d_permit, hipStream_t stream, uint32_t flags) {
     if (n == 0) return NFFACL_OK;
     if (t->meta.algo != NFFACL_ALGO_LINEAR) {
@@ -1212,9 +1240,9 @@ int launch_slots(nffacl_engine *eng, const DevTable *t, const uint8_t *d_slots, 
         }
         dev::IndexedArgs a = indexed_args(t);
         a.flags = flags;
-        const IndexedLaunch L = indexed_launch(t);
+        const IndexedLaunch L = indexed_launch(eng, t);
         const uint32_t grid = grid_for(eng, n, L.block, L.per_cu);
-        const int mode = stride == 64 ? std::min(4, std::max(0, tune_env("NFFACL_TUNE_COAL", 4))) : 0;
+        const int mode = stride == 64 ? eng->tune.coal : 0;
         dispatch_indexed(L.ns, L.tm, [&](auto nsc, auto tmc) {
             launch_slots_tm<decltype(nsc)::value, decltype(tmc)::value>(mode, L, grid, stream, d_slots, stride, n, a,
                                                                       d_port, d_permit);
@@ -1228,10 +1256,11 @@ int launch_slots(nffacl_engine *eng, const DevTable *t, const uint8_t *d_slots, 
                            n, a, d_port, d_permit);
     }
     HIP_TRY(hipGetLastError());
+    HIP_TRY(t->note_use(stream));
     return NFFACL_OK;
 }
 
-int launch_frames(nffacl_engine *eng, const DevTable *t, const uint8_t *d_frames,
+int launch_frames(nffacl_engine *eng, DevTable *t, const uint8_t *d_frames,
                   const uint64_t *d_desc, uint64_t n, uint32_t *d_port, uint64_t *d_permit,
                   hipStream_t stream, uint32_t flags) {
     if (n == 0) return NFFACL_OK;
@@ -1242,7 +1271,7 @@ int launch_frames(nffacl_engine *eng, const DevTable *t, const uint8_t *d_frames
         }
         dev::IndexedArgs a = indexed_args(t);
         a.flags = flags;
-        const IndexedLaunch L = indexed_launch(t);
+        const IndexedLaunch L = indexed_launch(eng, t);
         const uint32_t grid = grid_for(eng, n, L.block, L.per_cu);
         dispatch_indexed(L.ns, L.tm, [&](auto nsc, auto tmc) {
             launch_frames_tm<decltype(nsc)::value, decltype(tmc)::value>(L, grid, stream, d_frames, d_desc, n, a,
@@ -1257,6 +1286,7 @@ int launch_frames(nffacl_engine *eng, const DevTable *t, const uint8_t *d_frames
                            n, a, d_port, d_permit);
     }
     HIP_TRY(hipGetLastError());
+    HIP_TRY(t->note_use(stream));
     return NFFACL_OK;
 }
 

@@ -5,25 +5,39 @@
 
 #include <atomic>
 #include <cstdint>
+#include <memory>
 #include <mutex>
 #include <string>
 
 #include "compile.hpp"
+#include "tables.hpp"
 
 namespace nffacl {
 
 void set_last_error(const std::string &s);
 const char *last_error();
 
-// One compiled table resident in HBM.
-struct DevTable {
-    uint32_t *d_blob = nullptr;
-    size_t bytes = 0;
+// One compiled table resident in HBM (lifetime: tables.hpp).
+struct DevTable : DeviceBlob {
     CompiledTable meta;
-    ~DevTable();
+};
+using TablePtr = std::shared_ptr<DevTable>;
+
+// Launch-shape knobs, read from the environment ONCE at engine creation
+// (tools/ab_env.py experiments; unset in production) and validated there —
+// never on the launch path.
+struct Tune {
+    int coal = 4;    // NFFACL_TUNE_COAL: 64-byte slot load mode 0..4 (engine.hip)
+    int block = 0;   // NFFACL_TUNE_BLOCK: threads per workgroup (0 = kernel default)
+    int per_cu = 0;  // NFFACL_TUNE_PER_CU: workgroups per CU (0 = kernel default)
+    int rounds = 0;  // NFFACL_TUNE_ROUNDS: flat walks, loads in flight (0 = compiled, 2 or 4)
+    int lds = 1;     // NFFACL_TUNE_LDS: 0 keeps INDEXED tables in global memory
+    CompileOptions copt;  // NFFACL_TUNE_FLAT / _DIR_KB / _DIR16 (table layout)
+    // false (+ `err`) if a set variable is out of range
+    static bool from_env(Tune &t, std::string &err);
 };
 
-int upload_table(int device, const nffacl_rules &rules, int algo, DevTable *&out);
+int upload_table(nffacl_engine *eng, const nffacl_rules &rules, TablePtr &out);
 
 }  // namespace nffacl
 
@@ -31,11 +45,14 @@ struct nffacl_engine {
     int device = 0;
     int algo_req = NFFACL_ALGO_AUTO;
     int num_cus = 256;
-    // Active table (read by every launch) and the table it replaced, kept
-    // alive until the next swap has drained the device.
+    nffacl::Tune tune;
+    // Table uploads + stream-ordered frees of retired tables.  Declared
+    // before `active` so that it is destroyed after it.
+    nffacl::TableHome home;
+    // The table launches issued now use (swap_rules replaces it; holders of
+    // the previous one keep it alive, tables.hpp).
     std::mutex table_mu;
-    nffacl::DevTable *active = nullptr;
-    nffacl::DevTable *retired = nullptr;
+    nffacl::TablePtr active;
     // Host-inclusive pipeline state (nffacl_classify_host), created lazily.
     std::mutex host_mu;
     size_t chunk = 0;
@@ -49,15 +66,18 @@ struct nffacl_engine {
 };
 
 namespace nffacl {
-// The table launches issued now must use (swap_rules may replace it later).
-inline DevTable *acquire_table(nffacl_engine *eng) {
+// The table launches issued now must use; the caller holds it while it
+// enqueues work (swap_rules may replace it meanwhile).
+inline TablePtr acquire_table(nffacl_engine *eng) {
     std::lock_guard<std::mutex> g(eng->table_mu);
     return eng->active;
 }
 int prepare_kernels();
-int launch_slots(nffacl_engine *eng, const DevTable *t, const uint8_t *d_slots, uint32_t stride,
+// Both record the launch on `t` (DeviceBlob::note_use) so that a retired
+// table outlives the work enqueued with it.
+int launch_slots(nffacl_engine *eng, DevTable *t, const uint8_t *d_slots, uint32_t stride,
                  uint64_t n, uint32_t *d_port, uint64_t *d_permit, hipStream_t stream, uint32_t flags = 0);
-int launch_frames(nffacl_engine *eng, const DevTable *t, const uint8_t *d_frames,
+int launch_frames(nffacl_engine *eng, DevTable *t, const uint8_t *d_frames,
                   const uint64_t *d_desc, uint64_t n, uint32_t *d_port, uint64_t *d_permit,
                   hipStream_t stream, uint32_t flags = 0);
 }  // namespace nffacl

@@ -165,23 +165,16 @@ L2Compiled compile_l2(const std::vector<nffacl_l2_rule> &eth, int algo) {
     return c;
 }
 
-L2Table::~L2Table() {
-    if (d_blob) (void)hipFree(d_blob);
-}
-
-int upload_l2(int device, const nffacl_l2rules &rules, int algo, L2Table *&out) {
-    HIP_TRY(hipSetDevice(device));
-    L2Table *t = new L2Table();
-    t->meta = compile_l2(rules.eth, algo);
-    const size_t bytes = t->meta.blob.size() * sizeof(uint32_t);
-    hipError_t e = hipMalloc(reinterpret_cast<void **>(&t->d_blob), bytes);
-    if (e == hipSuccess) e = hipMemcpy(t->d_blob, t->meta.blob.data(), bytes, hipMemcpyHostToDevice);
+int upload_l2(nffacl_l2engine *eng, const nffacl_l2rules &rules, L2TablePtr &out) {
+    HIP_TRY(hipSetDevice(eng->device));
+    auto t = std::make_shared<L2Table>();
+    t->meta = compile_l2(rules.eth, eng->algo_req);
+    const hipError_t e = t->upload(&eng->home, t->meta.blob.data(), t->meta.blob.size());
     if (e != hipSuccess) {
         set_last_error(std::string("L2 table upload: ") + hipGetErrorString(e));
-        delete t;
-        return NFFACL_ERR_HIP;
+        return e == hipErrorOutOfMemory ? NFFACL_ERR_NOMEM : NFFACL_ERR_HIP;
     }
-    out = t;
+    out = std::move(t);
     return NFFACL_OK;
 }
 
@@ -338,7 +331,11 @@ k_l2_frames(const uint8_t *__restrict__ frames, const uint64_t *__restrict__ des
         const uint64_t idx = base + lane;
         const bool live = idx < n;
         const uint64_t ds = live ? desc[idx] : 0;
-        const u32x4 v = *reinterpret_cast<const u32x4 *>(frames + (ds >> 16));
+        // only frames with bytes are read: a 16-byte aligned load that starts
+        // inside a frame stays inside that frame's page (no read past the
+        // buffer, whatever follows the last frame)
+        u32x4 v = u32x4{0, 0, 0, 0};
+        if ((ds & 0xFFFFu) != 0u) v = *reinterpret_cast<const u32x4 *>(frames + (ds >> 16));
         uint32_t p[4] = {v.x, v.y, v.z, v.w};
         clip_dwords<4>(p, static_cast<uint32_t>(ds & 0xFFFFu));
         store_verdicts(base, lane, live, classify_l2<ALGO, LDS>(p, live, a), port_out, permit_out);
@@ -400,13 +397,12 @@ int l2_prepare_kernels() {
     return NFFACL_OK;
 }
 
-int l2_launch_slots(nffacl_l2engine *eng, const L2Table *t, const uint8_t *d_slots, uint32_t stride,
+int l2_launch_slots(nffacl_l2engine *eng, L2Table *t, const uint8_t *d_slots, uint32_t stride,
                     uint64_t n, uint32_t *d_port, uint64_t *d_permit, hipStream_t stream) {
     if (n == 0) return NFFACL_OK;
     const L2Launch L = l2_plan(eng, t, n);
     const dim3 g(L.grid), b(L.block);
-    const char *cv = std::getenv("NFFACL_TUNE_L2_COAL");  // A/B override
-    const bool coal = stride == 64 && !(cv && *cv == '0');
+    const bool coal = stride == 64 && eng->coal;
     auto go = [&](auto algo_c, auto lds_c, auto coal_c) {
         hipLaunchKernelGGL((dev::k_l2_slots<decltype(algo_c)::value, decltype(lds_c)::value, decltype(coal_c)::value>),
                            g, b, decltype(lds_c)::value ? L.lds_bytes : 0, stream, d_slots, stride, n, L.a, d_port,
@@ -424,10 +420,11 @@ int l2_launch_slots(nffacl_l2engine *eng, const L2Table *t, const uint8_t *d_slo
         if (coal) go(hsh{}, no{}, yes{}); else go(hsh{}, no{}, no{});
     }
     HIP_TRY(hipGetLastError());
+    HIP_TRY(t->note_use(stream));
     return NFFACL_OK;
 }
 
-int l2_launch_frames(nffacl_l2engine *eng, const L2Table *t, const uint8_t *d_frames, const uint64_t *d_desc,
+int l2_launch_frames(nffacl_l2engine *eng, L2Table *t, const uint8_t *d_frames, const uint64_t *d_desc,
                      uint64_t n, uint32_t *d_port, uint64_t *d_permit, hipStream_t stream) {
     if (n == 0) return NFFACL_OK;
     const L2Launch L = l2_plan(eng, t, n);
@@ -439,6 +436,7 @@ int l2_launch_frames(nffacl_l2engine *eng, const L2Table *t, const uint8_t *d_fr
     else
         hipLaunchKernelGGL((dev::k_l2_frames<NFFACL_ALGO_INDEXED, false>), g, b, 0, stream, d_frames, d_desc, n, L.a, d_port, d_permit);
     HIP_TRY(hipGetLastError());
+    HIP_TRY(t->note_use(stream));
     return NFFACL_OK;
 }
 

@@ -28,11 +28,13 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <memory>
 #include <mutex>
 #include <vector>
 
 #include "nffacl.h"
 #include "rules.hpp"
+#include "tables.hpp"
 
 namespace nffacl {
 
@@ -75,13 +77,11 @@ __host__ __device__ inline uint32_t l2_hash_alt(uint32_t h) {
     return h ^ (h >> 13);
 }
 
-struct L2Table {
-    uint32_t *d_blob = nullptr;
+// One compiled L2 table resident in HBM (lifetime: tables.hpp).
+struct L2Table : DeviceBlob {
     L2Compiled meta;
-    ~L2Table();
 };
-
-int upload_l2(int device, const nffacl_l2rules &rules, int algo, L2Table *&out);
+using L2TablePtr = std::shared_ptr<L2Table>;
 
 }  // namespace nffacl
 
@@ -89,9 +89,10 @@ struct nffacl_l2engine {
     int device = 0;
     int num_cus = 256;
     int algo_req = NFFACL_ALGO_AUTO;
+    bool coal = true;  // NFFACL_TUNE_L2_COAL (read once at creation): lane-contiguous 64-byte slot loads
+    nffacl::TableHome home;  // before `active`: destroyed after it
     std::mutex table_mu;
-    nffacl::L2Table *active = nullptr;
-    nffacl::L2Table *retired = nullptr;
+    nffacl::L2TablePtr active;
     // host path staging (nffacl_l2_classify_host), grown on demand
     std::mutex host_mu;
     hipStream_t stream = nullptr;
@@ -101,10 +102,12 @@ struct nffacl_l2engine {
 };
 
 namespace nffacl {
+int upload_l2(nffacl_l2engine *eng, const nffacl_l2rules &rules, L2TablePtr &out);
 int l2_prepare_kernels();
-int l2_launch_slots(nffacl_l2engine *eng, const L2Table *t, const uint8_t *d_slots, uint32_t stride,
+// Both record the launch on `t` (DeviceBlob::note_use).
+int l2_launch_slots(nffacl_l2engine *eng, L2Table *t, const uint8_t *d_slots, uint32_t stride,
                     uint64_t n, uint32_t *d_port, uint64_t *d_permit, hipStream_t stream);
-int l2_launch_frames(nffacl_l2engine *eng, const L2Table *t, const uint8_t *d_frames,
+int l2_launch_frames(nffacl_l2engine *eng, L2Table *t, const uint8_t *d_frames,
                      const uint64_t *d_desc, uint64_t n, uint32_t *d_port, uint64_t *d_permit,
                      hipStream_t stream);
 }  // namespace nffacl

@@ -7,7 +7,9 @@ real exchange is the rule file itself — rank 0 loads it and broadcasts its
 bytes once per rule swap (the reference's rule hot-swap, tutorial/step08.go:33-44,
 is a local pointer store; across GPUs it becomes this broadcast).  For the
 "root-scattered" deployment (packets arriving on one GPU) scatter_slots /
-gather_verdicts move packet shards and verdict shards over RCCL.
+gather_verdicts move packet shards and verdict shards with one RCCL
+collective each (dist.scatter / dist.gather: the root's peer transfers run
+concurrently over its xGMI links, not one recv at a time).
 """
 from __future__ import annotations
 
@@ -74,52 +76,62 @@ def shard(n_total: int, rank: int, world_size: int):
     return start, min(n_total, (first + cnt) * 64) - start
 
 
+def _even_shard(n_total: int, world_size: int) -> int:
+    """Packets per rank for the collectives: equal 64-aligned shards (the
+    last rank's tail is padding when n_total does not divide evenly)."""
+    waves = (n_total + 63) // 64
+    return (waves + world_size - 1) // world_size * 64
+
+
 def scatter_slots(slots: torch.Tensor | None, n_total: int, stride: int, device: torch.device | None,
                   src: int = 0) -> torch.Tensor:
     """Root-scattered ingest: rank `src` holds all n_total slots; every rank
-    receives its shard (point-to-point sends, one per peer)."""
+    receives its shard through ONE collective (dist.scatter — under RCCL the
+    root's sends to all peers run concurrently, one per xGMI link; ncclScatter
+    semantics, rccl.h:767).  Shards are equal 64-packet-aligned pieces;
+    returns this rank's slots trimmed to its real packets (shard_even())."""
     rank, ws = dist.get_rank(), dist.get_world_size()
     cd = comm_device(device)
-    start, cnt = shard(n_total, rank, ws)
+    per = _even_shard(n_total, ws)
+    start, cnt = shard_even(n_total, rank, ws)
+    out = torch.empty(per * stride, dtype=torch.uint8, device=cd)
+    pieces = None
     if rank == src:
-        reqs = []
-        for r in range(ws):
-            if r == src:
-                continue
-            s, c = shard(n_total, r, ws)
-            if c:
-                reqs.append(dist.isend(slots[s * stride:(s + c) * stride].to(cd).contiguous(), r))
-        for q in reqs:
-            q.wait()
-        return slots[start * stride:(start + cnt) * stride].to(cd)
-    buf = torch.empty(cnt * stride, dtype=torch.uint8, device=cd)
-    if cnt:
-        dist.recv(buf, src)
-    return buf
+        flat = slots.reshape(-1)
+        if flat.device != cd:
+            flat = flat.to(cd)
+        need = per * ws * stride
+        if flat.numel() < need:  # ragged batch: pad the root's copy (zero slots, never reported)
+            pad = torch.zeros(need, dtype=torch.uint8, device=cd)
+            pad[:n_total * stride] = flat[:n_total * stride]
+            flat = pad
+        pieces = list(flat[:need].view(ws, per * stride).unbind(0))
+    dist.scatter(out, pieces, src=src)
+    return out[:cnt * stride]
 
 
 def gather_verdicts(port: torch.Tensor, n_total: int, device: torch.device | None, dst: int = 0):
-    """Inverse of scatter_slots for the u32 verdict vector (returns the full
-    vector on `dst`, None elsewhere)."""
+    """Inverse of scatter_slots for the u32 verdict vector, through ONE
+    dist.gather (ncclGather semantics, rccl.h:745): returns the full vector
+    on `dst`, None elsewhere."""
     rank, ws = dist.get_rank(), dist.get_world_size()
     cd = comm_device(device)
+    per = _even_shard(n_total, ws)
+    buf = torch.zeros(per, dtype=port.dtype, device=cd)
+    buf[:port.numel()] = port.to(cd)
     if rank == dst:
-        out = torch.empty(n_total, dtype=port.dtype, device=cd)
-        s0, c0 = shard(n_total, rank, ws)
-        out[s0:s0 + c0] = port.to(cd)
-        for r in range(ws):
-            if r == dst:
-                continue
-            s, c = shard(n_total, r, ws)
-            if c:
-                tmp = torch.empty(c, dtype=port.dtype, device=cd)
-                dist.recv(tmp, r)
-                out[s:s + c] = tmp
-        return out
-    s, c = shard(n_total, rank, ws)
-    if c:
-        dist.send(port.to(cd).contiguous(), dst)
+        full = torch.empty(per * ws, dtype=port.dtype, device=cd)
+        dist.gather(buf, list(full.view(ws, per).unbind(0)), dst=dst)
+        return full[:n_total]
+    dist.gather(buf, None, dst=dst)
     return None
+
+
+def shard_even(n_total: int, rank: int, world_size: int):
+    """(start, count) of rank's piece under the equal-shard collectives."""
+    per = _even_shard(n_total, world_size)
+    start = min(n_total, rank * per)
+    return start, min(n_total, start + per) - start
 
 
 def scatter_classify_gather(slots_root, n_total: int, stride: int, classify, device, src: int = 0):
@@ -135,7 +147,7 @@ def scatter_classify_gather(slots_root, n_total: int, stride: int, classify, dev
         torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     mine = scatter_slots(slots_root, n_total, stride, device, src)
-    _, cnt = shard(n_total, dist.get_rank(), dist.get_world_size())
+    _, cnt = shard_even(n_total, dist.get_rank(), dist.get_world_size())
     port = classify(mine, cnt) if cnt else torch.empty(0, dtype=torch.int32, device=dev)
     full = gather_verdicts(port, n_total, device, src)
     if dev is not None and dev.type == "cuda":

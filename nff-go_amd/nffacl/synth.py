@@ -366,24 +366,52 @@ def write_frames(h, lengths: np.ndarray, width: int) -> np.ndarray:
     return buf
 
 
-def gen_slots(rules: GenRules, n: int, seed: int, stride: int = 64, chunk: int = 1 << 22) -> np.ndarray:
+def _parallel(fn, starts, workers):
+    """Run fn(c0) for every chunk start; chunks are independent (seeded by
+    their start), so the output does not depend on the worker count."""
+    if workers <= 1 or len(starts) <= 1:
+        for c0 in starts:
+            fn(c0)
+        return
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(min(workers, len(starts))) as ex:
+        for f in [ex.submit(fn, c0) for c0 in starts]:
+            f.result()
+
+
+def _workers() -> int:
+    try:
+        import os
+        return max(1, min(16, len(os.sched_getaffinity(0))))
+    except (AttributeError, OSError):
+        return 1
+
+
+def gen_slots(rules: GenRules, n: int, seed: int, stride: int = 64, chunk: int = 1 << 22,
+              workers: int | None = None) -> np.ndarray:
     """n packets of 64 B frames in dense slots (n*stride bytes, zero padded)."""
     out = np.zeros((n, stride), np.uint8)
-    for c0 in range(0, n, chunk):
+    w = min(stride, 64)
+
+    def one(c0):
         c1 = min(n, c0 + chunk)
         h = gen_headers(rules, c1 - c0, seed + c0)
-        out[c0:c1, :min(stride, 64)] = write_frames(h, np.full(c1 - c0, 64), 64)[:, :min(stride, 64)]
+        out[c0:c1, :w] = write_frames(h, np.full(c1 - c0, 64), 64)[:, :w]
+
+    _parallel(one, range(0, n, chunk), _workers() if workers is None else workers)
     return out.reshape(-1)
 
 
 IMIX = ((64, 7), (570, 4), (1518, 1))
 
 
-def gen_imix(rules: GenRules, n: int, seed: int, align: int = 64, chunk: int = 1 << 21):
+def gen_imix(rules: GenRules, n: int, seed: int, align: int = 64, chunk: int = 1 << 21,
+             workers: int | None = None):
     """Packed IMIX frames: returns (frames uint8, desc uint64 = offset<<16 | len).
 
     Frames start on `align`-byte boundaries like mbuf data rooms; the first
     128 bytes of each frame carry the headers, the rest is zero payload."""
+    assert align == 64
     rng = np.random.default_rng(seed ^ 0x1111)
     sizes = np.array([s for s, _ in IMIX])
     weights = np.array([w for _, w in IMIX], float)
@@ -393,13 +421,18 @@ def gen_imix(rules: GenRules, n: int, seed: int, align: int = 64, chunk: int = 1
     offs[1:] = np.cumsum(room)[:-1]
     total = int(offs[-1] + room[-1]) + 128  # slack so 80-byte reads stay in bounds
     frames = np.zeros(total, np.uint8)
-    for c0 in range(0, n, chunk):
+    rows = frames.reshape(-1, 64)  # 64-byte lines; frame i starts at line offs[i] / 64
+
+    def one(c0):
         c1 = min(n, c0 + chunk)
         h = gen_headers(rules, c1 - c0, seed + c0)
         img = write_frames(h, lengths[c0:c1], 128)
-        idx = offs[c0:c1, None] + np.arange(128)[None, :]
-        own = np.arange(128)[None, :] < room[c0:c1, None]  # never touch the next frame's room
-        frames[idx[own]] = img[own]
+        line = offs[c0:c1] // 64
+        rows[line] = img[:, :64]
+        two = room[c0:c1] > 64  # never touch the next frame's room
+        rows[line[two] + 1] = img[two, 64:]
+
+    _parallel(one, range(0, n, chunk), _workers() if workers is None else workers)
     desc = (offs.astype(np.uint64) << np.uint64(16)) | lengths.astype(np.uint64)
     return frames, desc
 

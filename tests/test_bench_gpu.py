@@ -1,0 +1,68 @@
+"""bench.py end to end on the GPU (-m gpu), at reduced sizes.
+
+* N = 1: the headline line plus the same-process C3 / C5 records, every
+  record bit-exact against the oracle sample and carrying its own metric,
+  roofline and CPU baseline.
+* N = 2 rehearsed on ONE GPU (NFFACL_BENCH_ONE_GPU=1, gloo — RCCL refuses two
+  ranks on one device): the root-scattered leg's dist.scatter / dist.gather
+  path, whose verdicts must equal rank 0's own classify of the whole batch.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def _json_line(stdout: str) -> dict:
+    lines = [ln for ln in stdout.splitlines() if ln.startswith("{")]
+    assert lines, stdout[-2000:]
+    return json.loads(lines[-1])
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_bench_n1_with_extra_configs(gpu_available):
+    if not gpu_available:
+        pytest.skip("no HIP device")
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--steps", "3", "--warmup", "1",
+                        "--packets", str(1 << 18), "--cpu-seconds", "1", "--no-host"],
+                       capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json_line(r.stdout)
+    assert d["metric"].startswith("Mpackets/s device-resident L3 ACL classify, 64B pkts @1k rules")
+    assert d["bit_exact_sample"] and d["cpu_baseline"]["bit_exact_vs_gpu"]
+    assert set(d["configs"]) == {"c3", "c5"}
+    for c, rec in d["configs"].items():
+        assert "@1k rules" not in rec["metric"], rec["metric"]  # labelled per config
+        assert rec["bit_exact_sample"] and rec["cpu_baseline"]["bit_exact_vs_gpu"], c
+        assert rec["roofline"]["frac"] > 0 and rec["value"] > 0
+    assert d["configs"]["c3"]["config"]["algorithmic_bytes_per_packet"] == 76
+    assert d["configs"]["c5"]["config"]["rules_ip4"] + d["configs"]["c5"]["config"]["rules_ip6"] == 100000
+
+
+def test_bench_two_ranks_one_gpu_scatter(gpu_available):
+    if not gpu_available:
+        pytest.skip("no HIP device")
+    env = dict(os.environ, NFFACL_BENCH_ONE_GPU="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(ROOT / "bench.py"),
+           "--gpus", "2", "--steps", "3", "--warmup", "1", "--packets", str((1 << 18) + 64 * 3),
+           "--backend", "gloo", "--no-host"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json_line(r.stdout)
+    assert d["n_gpus"] == 2 and d["rccl_ranks"] == 2 and d["backend"] == "gloo"
+    assert d["bit_exact_sample"]
+    sc = d["scatter_inclusive"]
+    assert sc["bit_exact_vs_local"] and sc["collectives"] == "dist.scatter + dist.gather"
