@@ -62,7 +62,7 @@
 extern "C" {
 #endif
 
-#define NFFACL_ABI_VERSION 2
+#define NFFACL_ABI_VERSION 3
 
 /* Only the entry points below are exported from libnffacl.so (built with
  * -fvisibility=hidden). */
@@ -183,7 +183,7 @@ NFFACL_API int nffacl_engine_table_bytes(const nffacl_engine *eng, uint64_t *byt
  * least that many dwords. */
 typedef struct nffacl_dim_info {
     uint32_t kind;       /* key: 0 src4, 1 dst4, 2 src6 (top 32 bits), 3 dst6, 4 sport, 5 dport */
-    uint32_t shift;      /* bucket = key >> shift */
+    uint32_t shift;      /* bucket = key >> shift (1-D); see kind2 */
     uint32_t n_buckets;  /* radix buckets */
     uint32_t off_dir;    /* dword offset of dir[n_buckets + 1] (bucket bounds, in entries) */
     uint32_t off_entries;/* dword offset of the bucket entries (inline rules, ascending per bucket) */
@@ -192,15 +192,25 @@ typedef struct nffacl_dim_info {
     uint32_t off_dir16;  /* 0, or (two-level directory) dword offset of u16 offsets dir16[n_buckets + 1];
                             then off_dir holds u32 group bases and dir[t] = base[t >> 6] + dir16[t] */
     uint64_t n_entries;  /* bucket entries (with replication) */
+    uint32_t kind2;      /* 6 = none (1-D slot); else a second key (kinds as above): the slot is a
+                            2-D grid, bucket = (key >> shift) << bits2 | key2 >> shift2 */
+    uint32_t shift2, bits2, reserved;
 } nffacl_dim_info;
+
+#define NFFACL_MAX_SLOTS 8
 
 typedef struct nffacl_family_info {
     uint32_t n_rec;        /* live rules of the family */
     uint32_t off_rec;      /* LINEAR: dword offset of the rule records (8 dwords IPv4, 20 IPv6);
-                              HYBRID: of the cold records (4 dwords IPv4, 16 IPv6) */
-    uint32_t entry_dwords; /* INDEXED: dwords per entry (8 IPv4, 20 IPv6); HYBRID: 4 */
+                              HYBRID flat forms: of the output array (one u32 per rule) */
+    uint32_t entry_dwords; /* INDEXED / lane form: dwords per entry (8 IPv4, 20 IPv6);
+                              HYBRID flat forms: 6 IPv4, 12 IPv6 (exact entries) */
     uint32_t off_resid, n_resid; /* INDEXED: entries scanned linearly (no selective key) */
-    nffacl_dim_info dims[4];     /* INDEXED: [dst addr, src addr, dst port, src port] */
+    nffacl_dim_info dims[NFFACL_MAX_SLOTS]; /* INDEXED: [dst addr, src addr, dst port, src port];
+                                               HYBRID global-directory form: any 1-D / 2-D keys */
+    uint32_t n_slots;            /* slots in use (dims[0, n_slots)) */
+    uint32_t off_ent_base;       /* HYBRID flat forms: dword offset of the family's first entry
+                                    (directory values are entry numbers counted from it) */
 } nffacl_family_info;
 
 typedef struct nffacl_table_info {

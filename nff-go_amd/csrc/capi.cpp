@@ -224,10 +224,12 @@ int nffacl_table_compile(const nffacl_rules *rules, int algo, uint32_t *blob, ui
         o.entry_dwords = fi[f]->entry_dwords;
         o.off_resid = fi[f]->off_resid;
         o.n_resid = fi[f]->n_resid;
-        for (int k = 0; k < 4; ++k) {
+        o.n_slots = ct.slots_g ? fi[f]->used_slots : 4u;
+        o.off_ent_base = fi[f]->off_ent_base;
+        for (uint32_t k = 0; k < kMaxSlots; ++k) {
             const DimInfo &d = fi[f]->dims[k];
             o.dims[k] = nffacl_dim_info{d.kind, d.shift, d.n_buckets, d.off_dir, d.off_ent, d.n_rules,
-                                        d.max_list, d.off_dir16, d.n_ent};
+                                        d.max_list, d.off_dir16, d.n_ent, d.kind2, d.shift2, d.bits2, 0};
         }
     }
     if (blob) {

@@ -367,54 +367,33 @@ bool hybrid_encodable(const std::vector<uint32_t> &rec4, uint32_t n4, const std:
     return true;
 }
 
-// Port-block bitmap of [mn, mx]: bit b set iff the range meets block b
-// (8192 ports per block); `exact` iff the range is a union of whole blocks.
-uint32_t port_blocks(uint32_t mn, uint32_t mx, bool &exact) {
-    const uint32_t b0 = mn >> kHybPortBlockShift, b1 = mx >> kHybPortBlockShift;
-    exact = (mn & kHybPortBlockMask) == 0 && (mx & kHybPortBlockMask) == kHybPortBlockMask;
-    return ((2u << b1) - 1u) & ~((1u << b0) - 1u);
-}
-
-// Compact entry of record r (table.hpp, "hybrid entry").
+// Exact flat-form entry of record r (table.hpp, "flat-form list entry"):
+// IPv4 6 dwords, IPv6 12.
 void emit_hyb_entry(const uint32_t *rec, bool v6, uint32_t r, std::vector<uint32_t> &blob) {
     const uint32_t *m = v6 ? rec + 16 : rec + 4;  // meta, lo, hi
-    uint32_t sa, da, sl, dl;
-    bool cold = false;
+    uint32_t sl, dl;
     if (v6) {
-        const int s = prefix128(rec + 4), d = prefix128(rec + 12);
-        sa = bswap32(rec[0]);
-        da = bswap32(rec[8]);
-        sl = static_cast<uint32_t>(std::min(s, 32));
-        dl = static_cast<uint32_t>(std::min(d, 32));
-        cold = s > 32 || d > 32;
+        sl = static_cast<uint32_t>(prefix128(rec + 4));
+        dl = static_cast<uint32_t>(prefix128(rec + 12));
     } else {
-        sa = bswap32(rec[0]);
-        da = bswap32(rec[2]);
         sl = static_cast<uint32_t>(__builtin_popcount(rec[1]));
         dl = static_cast<uint32_t>(__builtin_popcount(rec[3]));
     }
     const bool pc = (m[0] & kMetaPortCheck) != 0;
     const uint32_t lo = pc ? m[1] : 0u, hi = pc ? m[2] : 0xFFFFFFFFu;
-    bool es, ed;
-    const uint32_t sbm = port_blocks(lo & 0xFFFFu, hi & 0xFFFFu, es);
-    const uint32_t dbm = port_blocks(lo >> 16, hi >> 16, ed);
-    cold = cold || !es || !ed;
     const uint32_t exact = ((m[0] >> 8) & 0xFFu) ? kEntExact : 0u;
     const uint32_t output = v6 ? rec[19] : rec[7];
-    const uint32_t ocode = std::min(output, kHybOutCold);
-    blob.insert(blob.end(), {sa, da, (m[0] & 0xFFu) | exact | (r << kEntIndexShift),
-                             sl | dl << 6 | (cold ? kHybCold : 0u) | ocode << kHybOutShift | sbm << 16 | dbm << 24});
+    const uint32_t ocode = std::min(output, kHybOutEscape);
+    const uint32_t sa = v6 ? rec[0] : rec[0], da = v6 ? rec[8] : rec[2];
+    blob.insert(blob.end(), {bswap32(sa), bswap32(da), (m[0] & 0xFFu) | exact | (r << kEntIndexShift), lo, hi,
+                             sl | dl << 8 | ocode << kHybOutShift});
+    if (v6)
+        blob.insert(blob.end(), {bswap32(rec[1]), bswap32(rec[2]), bswap32(rec[3]),
+                                 bswap32(rec[9]), bswap32(rec[10]), bswap32(rec[11])});
 }
 
-// Cold record of record r: {lo, hi, output, 0} (+ IPv6 extension words).
-void emit_cold(const uint32_t *rec, bool v6, std::vector<uint32_t> &blob) {
-    const uint32_t *m = v6 ? rec + 16 : rec + 4;
-    const bool pc = (m[0] & kMetaPortCheck) != 0;
-    blob.insert(blob.end(), {pc ? m[1] : 0u, pc ? m[2] : 0xFFFFFFFFu, v6 ? rec[19] : rec[7], 0u});
-    if (v6)  // s1 s2 s3 sm1 | sm2 sm3 t1 t2 | t3 tm1 tm2 tm3 (entry_miss_ext layout)
-        blob.insert(blob.end(), {rec[1], rec[2], rec[3], rec[5], rec[6], rec[7],
-                                 rec[9], rec[10], rec[11], rec[13], rec[14], rec[15]});
-}
+// Output number of record r (the family's output array).
+void emit_cold(const uint32_t *rec, bool v6, std::vector<uint32_t> &blob) { blob.push_back(v6 ? rec[19] : rec[7]); }
 
 uint64_t entries_at(const DimBuild &d, uint32_t rb) {
     const uint32_t shift = d.key_bits - rb;
@@ -506,6 +485,395 @@ double size_and_fill(DimBuild *const *all, const double *weight, size_t budget, 
     return expect;
 }
 
+// ---------------------------------------------------------------------------
+// HYBRID global-directory form with generalized slots (table.hpp): each slot
+// keys on one field (1-D) or on the top bits of two fields (2-D grid), and
+// every rule goes to the slot where it costs the fewest expected candidates.
+// Rules whose best single field is wide (short prefixes on both addresses,
+// wide port ranges) dominate the candidate lists of 1-D slots — for C5 the
+// 4 % of rules whose best field covers >= 2^-12 of its key space account for
+// ~5.7 of ~6.2 candidates per packet even with unbounded directories — and a
+// 2-D key is selective for exactly those.
+// ---------------------------------------------------------------------------
+
+uint32_t ceil_log2(uint64_t x) {
+    uint32_t b = 0;
+    while ((uint64_t(1) << b) < x) ++b;
+    return b;
+}
+
+uint32_t field_bits(uint32_t f) { return f < 2 ? 32u : 16u; }
+
+uint32_t field_kind(uint32_t f, bool v6) {
+    static const uint32_t k4[4] = {kKeyDst4, kKeySrc4, kKeyDport, kKeySport};
+    static const uint32_t k6[4] = {kKeyDst6, kKeySrc6, kKeyDport, kKeySport};
+    return f >= kFZero ? kKeyNone : (v6 ? k6[f] : k4[f]);
+}
+
+struct GSlot {
+    uint32_t f1 = kFDst, b1 = 1, f2 = kFZero, b2 = 0;  // fields (SlotField) and radix bits
+    std::vector<uint32_t> rules;                       // ascending rule order
+    std::vector<uint32_t> dir, ents;
+    uint32_t max_list = 0;
+    uint64_t n_buckets() const { return uint64_t(1) << (b1 + b2); }
+    // bucket index ranges [l1, h1] x [l2, h2] a rule with field ranges kr covers
+    void span(const std::array<KeyRange, 4> &kr, uint64_t &l1, uint64_t &h1, uint64_t &l2, uint64_t &h2) const {
+        const uint32_t s1 = field_bits(f1) - b1;
+        l1 = kr[f1].lo >> s1;
+        h1 = kr[f1].hi >> s1;
+        l2 = h2 = 0;
+        if (f2 < kFZero) {
+            const uint32_t s2 = field_bits(f2) - b2;
+            l2 = kr[f2].lo >> s2;
+            h2 = kr[f2].hi >> s2;
+        }
+    }
+    uint64_t count(const std::array<KeyRange, 4> &kr) const {
+        uint64_t l1, h1, l2, h2;
+        span(kr, l1, h1, l2, h2);
+        return (h1 - l1 + 1) * (h2 - l2 + 1);
+    }
+    // bucket lists, ascending rule order within each
+    void fill(const std::vector<std::array<KeyRange, 4>> &rr) {
+        const size_t nb = n_buckets();
+        std::vector<uint32_t> len(nb, 0);
+        auto each = [&](uint32_t r, auto &&fn) {
+            uint64_t l1, h1, l2, h2;
+            span(rr[r], l1, h1, l2, h2);
+            for (uint64_t t1 = l1; t1 <= h1; ++t1)
+                for (uint64_t t2 = l2; t2 <= h2; ++t2) fn((t1 << b2) | t2);
+        };
+        for (uint32_t r : rules) each(r, [&](uint64_t t) { ++len[t]; });
+        dir.assign(nb + 1, 0);
+        max_list = 0;
+        for (size_t t = 0; t < nb; ++t) {
+            dir[t + 1] = dir[t] + len[t];
+            max_list = std::max(max_list, len[t]);
+        }
+        ents.assign(dir[nb], 0);
+        std::vector<uint32_t> at(dir.begin(), dir.end() - 1);
+        for (uint32_t r : rules) each(r, [&](uint64_t t) { ents[at[t]++] = r; });
+    }
+};
+
+// Candidates for a family of n rules: 1-D slots on every field, and (when
+// `two_d` and the family is large) 2-D grids of the address pair and of an
+// address with a port.  Radix widths: ~2 buckets per rule for the addresses
+// (shrunk per slot once its rules are known).
+std::vector<GSlot> slot_candidates(uint32_t n, bool two_d) {
+    const uint32_t ba = std::min(17u, std::max(6u, ceil_log2(std::max<uint32_t>(n, 1)) + 1));
+    const uint32_t bp = std::min(16u, ba - 2);
+    std::vector<GSlot> c;
+    auto add = [&](uint32_t f1, uint32_t b1, uint32_t f2, uint32_t b2) {
+        GSlot g;
+        g.f1 = f1, g.b1 = b1, g.f2 = f2, g.b2 = b2;
+        c.push_back(g);
+    };
+    add(kFDst, ba, kFZero, 0);
+    add(kFSrc, ba, kFZero, 0);
+    add(kFDport, bp, kFZero, 0);
+    add(kFSport, bp, kFZero, 0);
+    if (two_d && n >= 1024) {
+        const uint32_t a = std::min(9u, std::max(4u, ba / 2));
+        add(kFDst, a, kFSrc, a);
+        add(kFDst, a + 1, kFDport, 6);
+        add(kFSrc, a + 1, kFDport, 6);
+        add(kFDst, a + 1, kFSport, 6);
+        add(kFSrc, a + 1, kFSport, 6);
+    }
+    return c;
+}
+
+// Expected candidates per packet above which a rule is scanned
+// wave-uniformly (the residual list) instead of being listed: one uniform
+// test per 64 packets beats ~64 * cost per-lane candidates past about this.
+constexpr double kResidCost = 0.2;
+
+// Assign rules (field ranges rr) to the slots: argmin over slots of
+// span / buckets (expected candidates for a uniform packet) + mu * span
+// (memory), mu the smallest keeping the lists within `budget` entries.
+// choice[r] = slot index or -1 (residual).
+void assign_g(const std::vector<std::array<KeyRange, 4>> &rr, const std::vector<GSlot> &slots, uint64_t budget,
+              std::vector<int> &choice) {
+    const size_t n = rr.size(), S = slots.size();
+    std::vector<double> span(n * S), cost(n * S);
+    for (size_t r = 0; r < n; ++r)
+        for (size_t s = 0; s < S; ++s) {
+            span[r * S + s] = double(slots[s].count(rr[r]));
+            cost[r * S + s] = span[r * S + s] / double(slots[s].n_buckets());
+        }
+    auto run = [&](double mu) {
+        uint64_t mem = 0;
+        for (size_t r = 0; r < n; ++r) {
+            int best = -1;
+            double bv = 0, bc = 1e300;
+            for (size_t s = 0; s < S; ++s) {
+                const double v = cost[r * S + s] + mu * span[r * S + s];
+                if (best < 0 || v < bv) { best = int(s); bv = v; }
+                bc = std::min(bc, cost[r * S + s]);
+            }
+            if (bc >= kResidCost) best = -1;
+            choice[r] = best;
+            if (best >= 0) mem += uint64_t(span[r * S + best]);
+        }
+        return mem;
+    };
+    choice.assign(n, -1);
+    if (run(0.0) <= budget) return;
+    double lo = 0, hi = 1e-9;
+    while (run(hi) > budget && hi < 1.0) hi *= 4;
+    for (int it = 0; it < 40; ++it) {
+        const double mid = 0.5 * (lo + hi);
+        if (run(mid) > budget) lo = mid; else hi = mid;
+    }
+    run(hi);
+}
+
+// Slots of one family: assign, drop empty slots (at most kMaxSlots kept: the
+// least used is dropped and the rules re-assigned until they fit), then
+// narrow each slot's radix to ~4 buckets per rule.
+// Rules of each slot (and the residual list) from `choice`; empty slots dropped.
+void distribute(const std::vector<int> &choice, std::vector<GSlot> &slots, std::vector<uint32_t> &resid) {
+    resid.clear();
+    for (auto &g : slots) g.rules.clear();
+    for (uint32_t r = 0; r < choice.size(); ++r)
+        if (choice[r] >= 0) slots[choice[r]].rules.push_back(r);
+        else resid.push_back(r);
+    slots.erase(std::remove_if(slots.begin(), slots.end(), [](const GSlot &g) { return g.rules.empty(); }),
+                slots.end());
+}
+
+void plan_g(const std::vector<uint32_t> &recs, uint32_t rw, bool v6, uint32_t n, bool two_d, double slot_cost,
+            bool global_dirs, std::vector<GSlot> &slots, std::vector<uint32_t> &resid,
+            std::vector<std::array<KeyRange, 4>> &rr) {
+    rr.assign(n, {});
+    for (uint32_t r = 0; r < n; ++r) {
+        KeyRange kr[4];
+        rec_ranges(recs.data() + size_t(r) * rw, v6, kr);
+        for (int k = 0; k < 4; ++k) rr[r][k] = kr[k];
+    }
+    slots = slot_candidates(n, two_d);
+    const uint64_t budget = 4ull * n + 65536ull;
+    std::vector<int> choice;
+    while (true) {
+        assign_g(rr, slots, budget, choice);
+        std::vector<size_t> cnt(slots.size(), 0);
+        for (int c : choice)
+            if (c >= 0) ++cnt[c];
+        std::vector<GSlot> kept;
+        std::vector<size_t> kept_cnt;
+        std::vector<int> remap(slots.size(), -1);
+        for (size_t s = 0; s < slots.size(); ++s)
+            if (cnt[s]) {
+                remap[s] = int(kept.size());
+                kept.push_back(slots[s]);
+                kept_cnt.push_back(cnt[s]);
+            }
+        if (kept.size() <= kMaxSlots) {
+            for (int &c : choice) c = c >= 0 ? remap[c] : -1;
+            slots.swap(kept);
+            break;
+        }
+        // too many slots in use: drop the least used one and re-assign
+        const size_t worst = size_t(std::min_element(kept_cnt.begin(), kept_cnt.end()) - kept_cnt.begin());
+        kept.erase(kept.begin() + long(worst));
+        slots.swap(kept);
+    }
+    // A slot costs every packet of the family a directory read and a list
+    // head: drop (cheapest first) slots whose rules would cost fewer than
+    // `slot_cost` extra expected candidates per packet in their next-best slot.
+    while (slot_cost > 0 && slots.size() > 1) {
+        const size_t S = slots.size();
+        std::vector<double> delta(S, 0.0);
+        for (uint32_t r = 0; r < n; ++r) {
+            const int c = choice[r];
+            if (c < 0) continue;
+            const double own = double(slots[c].count(rr[r])) / double(slots[c].n_buckets());
+            double next = kResidCost;  // or the residual scan
+            for (size_t s = 0; s < S; ++s)
+                if (int(s) != c) next = std::min(next, double(slots[s].count(rr[r])) / double(slots[s].n_buckets()));
+            delta[c] += std::max(0.0, next - own);
+        }
+        const size_t worst = size_t(std::min_element(delta.begin(), delta.end()) - delta.begin());
+        if (delta[worst] >= slot_cost) break;
+        slots.erase(slots.begin() + long(worst));
+        assign_g(rr, slots, budget, choice);
+    }
+    distribute(choice, slots, resid);
+    if (!global_dirs) return;  // LDS directories: fit_lds() sizes, re-assigns and fills
+    for (auto &g : slots) {
+        const uint32_t want = std::max(4u, ceil_log2(4ull * g.rules.size()));
+        while (g.b1 + g.b2 > want) {
+            if (g.f2 < kFZero && g.b2 > 1 && (g.b2 >= g.b1 || g.b1 <= 1)) --g.b2;
+            else if (g.b1 > 1) --g.b1;
+            else break;
+        }
+        g.fill(rr);
+    }
+}
+
+// Bytes of a directory of nb buckets: plain u32, or two-level (table.hpp:
+// a u32 base per 64 buckets + a u16 offset per bucket).
+size_t gdir_bytes(uint64_t nb, bool dir16) {
+    return dir16 ? 2 * (nb + 4) + 4 * ((nb >> kDir16GroupShift) + 2) : 4 * (nb + 1);
+}
+
+// Expected candidates per uniform packet of slot g at radix bits (b1, b2).
+double gexpect(const GSlot &g, const std::vector<std::array<KeyRange, 4>> &rr, uint32_t b1, uint32_t b2) {
+    GSlot t;
+    t.f1 = g.f1, t.b1 = b1, t.f2 = g.f2, t.b2 = b2;
+    double sum = 0;
+    for (uint32_t r : g.rules) sum += double(t.count(rr[r]));
+    return sum / double(t.n_buckets());
+}
+
+// LDS directories: narrow radix bits, one at a time, where a byte saved costs
+// the fewest expected candidates (family-weighted), until both families'
+// directories fit `budget`; then re-assign the rules to the final slots and
+// build the lists.
+void fit_lds(std::vector<GSlot> (&slots)[2], std::vector<uint32_t> (&resid)[2],
+             const std::vector<std::array<KeyRange, 4>> (&rr)[2], const double (&weight)[2], size_t budget,
+             bool dir16) {
+    auto total = [&] {
+        size_t b = 8;  // the empty directory
+        for (int f = 0; f < 2; ++f)
+            for (const auto &g : slots[f]) b += gdir_bytes(g.n_buckets(), dir16);
+        return b;
+    };
+    std::vector<double> cur[2];
+    for (int f = 0; f < 2; ++f)
+        for (const auto &g : slots[f]) cur[f].push_back(gexpect(g, rr[f], g.b1, g.b2));
+    while (total() > budget) {
+        int bf = -1, bs = -1, bd = 0;
+        double bscore = 0, bval = 0;
+        for (int f = 0; f < 2; ++f)
+            for (size_t s = 0; s < slots[f].size(); ++s) {
+                const GSlot &g = slots[f][s];
+                for (int d = 1; d <= (g.f2 < kFZero ? 2 : 1); ++d) {
+                    const uint32_t b1 = g.b1 - (d == 1), b2 = g.b2 - (d == 2);
+                    if ((d == 1 && g.b1 <= 1) || (d == 2 && g.b2 <= 1)) continue;
+                    const double e = gexpect(g, rr[f], b1, b2);
+                    const double saved = double(gdir_bytes(g.n_buckets(), dir16)) -
+                                         double(gdir_bytes(uint64_t(1) << (b1 + b2), dir16));
+                    const double score = weight[f] * (e - cur[f][s]) / std::max(saved, 1.0);
+                    if (bf < 0 || score < bscore) { bf = f; bs = int(s); bd = d; bscore = score; bval = e; }
+                }
+            }
+        if (bf < 0) break;  // every slot at one bucket bit
+        GSlot &g = slots[bf][bs];
+        if (bd == 1) --g.b1; else --g.b2;
+        cur[bf][bs] = bval;
+    }
+    for (int f = 0; f < 2; ++f) {
+        if (slots[f].empty()) continue;
+        const size_t n = rr[f].size();
+        std::vector<int> choice;
+        assign_g(rr[f], slots[f], 4ull * n + 65536ull, choice);  // the final radix widths
+        distribute(choice, slots[f], resid[f]);
+        for (auto &g : slots[f]) g.fill(rr[f]);
+    }
+}
+
+// Two-level directories are possible iff no 64-bucket group spans 65536+ entries.
+bool gdir16_ok(const std::vector<GSlot> (&slots)[2]) {
+    for (int f = 0; f < 2; ++f)
+        for (const auto &g : slots[f])
+            for (size_t t = 0; t < g.dir.size(); ++t)
+                if (g.dir[t] - g.dir[(t >> kDir16GroupShift) << kDir16GroupShift] > 0xFFFFu) return false;
+    return true;
+}
+
+void build_hybrid_g(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vector<uint32_t> &rec6, uint32_t n6,
+                    const CompileOptions &opt, size_t lds_budget, CompiledTable &out) {
+    std::vector<GSlot> slots[2];
+    std::vector<uint32_t> resid[2];
+    std::vector<std::array<KeyRange, 4>> rr[2];
+    const std::vector<uint32_t> *recs[2] = {&rec4, &rec6};
+    const uint32_t rw[2] = {kRec4Dwords, kRec6Dwords}, nn[2] = {n4, n6};
+    const bool lds = lds_budget > 0;
+    for (int f = 0; f < 2; ++f)
+        plan_g(*recs[f], rw[f], f == 1, nn[f], opt.slots2d != 0, opt.slot_cost, !lds, slots[f], resid[f], rr[f]);
+    bool dir16 = false;
+    if (lds) {  // directories staged in LDS: two-level when possible
+        const double tot = std::max(1.0, double(n4) + double(n6));
+        const double weight[2] = {double(n4) / tot, double(n6) / tot};
+        const std::vector<GSlot> s0[2] = {slots[0], slots[1]};
+        dir16 = opt.dir16;
+        fit_lds(slots, resid, rr, weight, lds_budget, dir16);
+        if (dir16 && !gdir16_ok(slots)) {
+            dir16 = false;
+            slots[0] = s0[0];
+            slots[1] = s0[1];
+            fit_lds(slots, resid, rr, weight, lds_budget, false);
+        }
+    }
+    std::vector<uint32_t> &blob = out.blob;
+    FamilyIndex *fi[2] = {&out.idx4, &out.idx6};
+    // an empty directory {0, 0} for the kernels' unused slots, then the
+    // directories (values: family-relative entry numbers; two-level: in the
+    // group bases)
+    out.off_empty_dir = 0;
+    blob.insert(blob.end(), {0u, 0u});
+    uint32_t dir_words[2][kMaxSlots] = {};
+    for (int f = 0; f < 2; ++f)
+        for (size_t k = 0; k < slots[f].size(); ++k) {
+            const GSlot &g = slots[f][k];
+            DimInfo &di = fi[f]->dims[k];
+            di.off_dir = static_cast<uint32_t>(blob.size());
+            if (!dir16) {
+                blob.insert(blob.end(), g.dir.begin(), g.dir.end());
+                dir_words[f][k] = static_cast<uint32_t>(g.dir.size());
+                continue;
+            }
+            const size_t nb = g.dir.size() - 1;
+            const size_t groups = (nb >> kDir16GroupShift) + 2;  // base[g + 1] stays readable
+            for (size_t q = 0; q < groups; ++q) blob.push_back(g.dir[std::min(q << kDir16GroupShift, nb)]);
+            dir_words[f][k] = static_cast<uint32_t>(groups);
+            di.off_dir16 = static_cast<uint32_t>(blob.size());
+            auto rel = [&](size_t t) -> uint32_t {
+                return t <= nb ? g.dir[t] - g.dir[(t >> kDir16GroupShift) << kDir16GroupShift] : 0u;
+            };
+            const size_t words = (nb + 2) / 2 + 1;  // dword (t >> 1) + 1 stays readable
+            for (size_t w = 0; w < words; ++w) blob.push_back(rel(2 * w) | rel(2 * w + 1) << 16);
+        }
+    while (blob.size() % 4) blob.push_back(0);
+    out.lds_dwords = lds ? static_cast<uint32_t>(blob.size()) : 0u;
+    for (int f = 0; f < 2; ++f) {
+        const bool v6 = f == 1;
+        const uint32_t ew = v6 ? kHybEnt6Dwords : kHybEnt4Dwords;
+        fi[f]->entry_dwords = ew;
+        fi[f]->off_ent_base = static_cast<uint32_t>(blob.size());
+        fi[f]->used_slots = static_cast<uint32_t>(slots[f].size());
+        for (size_t k = 0; k < slots[f].size(); ++k) {
+            const GSlot &g = slots[f][k];
+            DimInfo &di = fi[f]->dims[k];
+            di.kind = field_kind(g.f1, v6);
+            di.shift = field_bits(g.f1) - g.b1;
+            di.kind2 = field_kind(g.f2, v6);
+            di.bits2 = g.f2 < kFZero ? g.b2 : 0u;
+            di.shift2 = g.f2 < kFZero ? field_bits(g.f2) - g.b2 : 0u;
+            di.n_buckets = static_cast<uint32_t>(g.n_buckets());
+            di.n_rules = static_cast<uint32_t>(g.rules.size());
+            di.n_ent = g.ents.size();
+            di.max_list = g.max_list;
+            di.off_ent = static_cast<uint32_t>(blob.size());
+            const uint32_t first = (di.off_ent - fi[f]->off_ent_base) / ew;  // family-relative entry numbers
+            for (uint32_t t = 0; t < dir_words[f][k]; ++t) blob[di.off_dir + t] += first;
+            for (uint32_t r : g.ents) emit_hyb_entry(recs[f]->data() + size_t(r) * rw[f], v6, r, blob);
+        }
+        fi[f]->off_resid = static_cast<uint32_t>(blob.size());
+        fi[f]->n_resid = static_cast<uint32_t>(resid[f].size());
+        for (uint32_t r : resid[f]) emit_hyb_entry(recs[f]->data() + size_t(r) * rw[f], v6, r, blob);
+        while (blob.size() % 4) blob.push_back(0);
+    }
+    out.slots_g = true;
+    out.flat_rounds = 4;
+    out.off_rec4 = static_cast<uint32_t>(blob.size());
+    for (uint32_t r = 0; r < n4; ++r) emit_cold(rec4.data() + size_t(r) * kRec4Dwords, false, blob);
+    out.off_rec6 = static_cast<uint32_t>(blob.size());
+    for (uint32_t r = 0; r < n6; ++r) emit_cold(rec6.data() + size_t(r) * kRec6Dwords, true, blob);
+}
+
 void build_hybrid(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vector<uint32_t> &rec6, uint32_t n6,
                   const CompileOptions &opt, CompiledTable &out) {
     FamilyPlan plan[2];
@@ -529,6 +897,14 @@ void build_hybrid(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vec
     const size_t tuned = opt.dir_bytes;
     const int force = opt.flat;
     const bool want16 = opt.dir16;
+    if (force == 1 && !tuned) {  // global directories: generalized (1-D / 2-D) slots
+        build_hybrid_g(rec4, n4, rec6, n6, opt, 0, out);
+        return;
+    }
+    if (force == 2 && opt.slots2d == 2) {  // LDS directories, generalized slots (experiment)
+        build_hybrid_g(rec4, n4, rec6, n6, opt, tuned ? tuned : kHybFlat4DirBytes, out);
+        return;
+    }
     size_t budget = tuned ? tuned : (force == 1 ? kHybFlatDirBytes : kHybLaneDirBytes);
     const bool lds_dirs = force != 1 && budget <= kHybLdsDirMaxBytes;
     const bool flat = force != 0 || !lds_dirs;
@@ -538,8 +914,11 @@ void build_hybrid(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vec
     if (flat && lds_dirs && !tuned && expect > kHybFlat4Candidates) {
         budget = kHybFlat4DirBytes;
         size_and_fill(all, weight, budget, want16);
-        out.flat_rounds = 4;
     }
+    // 4 rounds of candidate loads in flight whenever their scratch fits beside
+    // the directories (indexed_launch checks; exact entries, C3: 0.507 vs
+    // 0.540 ms at 2 rounds, profiles/r2_exact/)
+    if (flat && lds_dirs) out.flat_rounds = 4;
     // LDS directories: two-level unless some 64-bucket group holds 65536+
     // entries (then plain u32, re-sized for the same budget)
     bool dir16 = lds_dirs && want16;
@@ -582,8 +961,9 @@ void build_hybrid(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vec
         const bool v6 = f == 1;
         // lane form: INDEXED's inline entries (exact, output inline — a hit
         // costs no further read); flat form: compact entries + cold records
-        const uint32_t ew = flat ? kHybEntDwords : (v6 ? kEnt6Dwords : kEnt4Dwords);
+        const uint32_t ew = flat ? (v6 ? kHybEnt6Dwords : kHybEnt4Dwords) : (v6 ? kEnt6Dwords : kEnt4Dwords);
         fi[f]->entry_dwords = ew;
+        fi[f]->off_ent_base = static_cast<uint32_t>(blob.size());
         for (int k = 0; k < 4; ++k) {
             DimBuild &d = *all[4 * f + k];
             DimInfo &di = fi[f]->dims[k];
@@ -594,8 +974,8 @@ void build_hybrid(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vec
             di.n_ent = d.ents.size();
             di.max_list = d.max_list;
             di.off_ent = static_cast<uint32_t>(blob.size());
-            if (flat) {  // directory values: absolute entry numbers (16-byte units)
-                const uint32_t first = di.off_ent / kHybEntDwords;
+            if (flat) {  // directory values: family-relative entry numbers
+                const uint32_t first = (di.off_ent - fi[f]->off_ent_base) / ew;
                 for (uint32_t t = 0; t < dir_words[4 * f + k]; ++t) blob[di.off_dir + t] += first;
                 for (uint32_t r : d.ents) emit_hyb_entry(recs[f]->data() + size_t(r) * rw[f], v6, r, blob);
             } else {     // relative to off_ent, as INDEXED
@@ -656,6 +1036,10 @@ bool CompileOptions::from_env(CompileOptions &o, std::string &err) {
     if (set) o.dir_bytes = size_t(v) * 1024;
     if (!env_knob("NFFACL_TUNE_DIR16", 0, 1, v, set, err)) return false;
     if (set) o.dir16 = v != 0;
+    if (!env_knob("NFFACL_TUNE_SLOTS2D", 0, 2, v, set, err)) return false;
+    if (set) o.slots2d = static_cast<int>(v);
+    if (!env_knob("NFFACL_TUNE_SLOT_COST", 0, 1000, v, set, err)) return false;
+    if (set) o.slot_cost = double(v) / 100.0;
     return true;
 }
 

@@ -15,7 +15,9 @@ namespace nffacl {
 // One key dimension ("slot") of the indexed table of a family (table.hpp).
 struct DimInfo {
     uint32_t kind = 0;       // KeyKind
-    uint32_t shift = 0;      // bucket = key >> shift
+    uint32_t shift = 0;      // bucket = key >> shift (1-D)
+    uint32_t kind2 = kKeyNone;  // 2-D slots: bucket = (key >> shift) << bits2 | key2 >> shift2
+    uint32_t shift2 = 0, bits2 = 0;
     uint32_t n_buckets = 0;  // 2^(key bits - shift)
     uint32_t off_dir = 0;    // dword offset of dir[n_buckets + 1] (or, with off_dir16, of the
                              // 2-level directory's group bases base[n_buckets / 64 + 2])
@@ -27,11 +29,14 @@ struct DimInfo {
     uint32_t max_list = 0;   // longest bucket list
 };
 
-// Indexed view of one address family: always 4 slots in the order
-// [dst address, src address, dst port, src port] (empty slots allowed).
+// Indexed view of one address family.  INDEXED and the LDS-directory HYBRID
+// forms: 4 slots in the order [dst address, src address, dst port, src port]
+// (empty slots allowed).  HYBRID global-directory form: up to kMaxSlots
+// slots of any 1-D / 2-D key, all non-empty.
 struct FamilyIndex {
-    uint32_t entry_dwords = 0;  // 8 (IPv4) or 20 (IPv6)
-    DimInfo dims[4];
+    uint32_t entry_dwords = 0;  // INDEXED / lane form: 8 (IPv4) or 20 (IPv6); flat forms 6 / 12
+    uint32_t off_ent_base = 0;  // flat forms: dword offset of the family's first entry (directory values count from it)
+    DimInfo dims[kMaxSlots];
     uint32_t off_resid = 0, n_resid = 0;  // residual entries (scanned linearly)
     uint32_t used_slots = 0;              // 1 + last non-empty slot (kernels walk that many)
 };
@@ -50,12 +55,19 @@ struct CompiledTable {
     uint32_t lds_dwords = 0;
     // HYBRID flat-LDS: rounds of candidate loads in flight (2 or 4)
     uint32_t flat_rounds = 2;
+    // HYBRID global-directory form with generalized slots (dims[k].kind2 etc.;
+    // idx*.used_slots = slots in use, all non-empty)
+    bool slots_g = false;
+    uint32_t off_empty_dir = 0;  // slots_g: dword offset of an empty directory {0, 0}
 };
 
 // Table-layout overrides for tuning experiments (unset in production).
 struct CompileOptions {
     int flat = 2;           // NFFACL_TUNE_FLAT: HYBRID form 0 lane, 1 flat (global dirs), 2 flat-LDS
     size_t dir_bytes = 0;   // NFFACL_TUNE_DIR_KB: HYBRID directory budget (0 = policy)
+    int slots2d = 1;        // NFFACL_TUNE_SLOTS2D: global-directory form may use 2-D slots;
+                            // 2: flat-LDS with generalized 1-D / 2-D slots
+    double slot_cost = 0.1; // NFFACL_TUNE_SLOT_COST (1/100): expected candidates per packet a slot must save
     bool dir16 = true;      // NFFACL_TUNE_DIR16: two-level u16 LDS directories allowed
     // false (+ `err`) if a set variable is out of range
     static bool from_env(CompileOptions &o, std::string &err);

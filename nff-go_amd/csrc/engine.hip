@@ -357,11 +357,15 @@ k_linear_frames(const uint8_t *__restrict__ frames, const uint64_t *__restrict__
 
 struct SlotArgs {
     uint32_t shift, off_dir, off_ent, off_dir16;  // off_dir16: 0 = plain u32 directory
+    // flat kernels (generalized slots, table.hpp SlotField): bucket =
+    // (key[f1] >> shift) << bits2 | key[f2] >> shift2, key[kFZero] = 0
+    uint32_t f1, f2, shift2, bits2;
 };
 struct FamArgs {
-    SlotArgs slot[4];  // [dst addr, src addr, dst port, src port]
+    SlotArgs slot[kMaxSlots];  // INDEXED / LDS forms: [dst addr, src addr, dst port, src port]
     uint32_t off_resid, n_resid;
-    uint32_t off_cold;  // HYBRID: cold records
+    uint32_t off_cold;      // HYBRID flat forms: output array (one u32 per rule)
+    uint32_t off_ent_base;  // HYBRID flat forms: the family's first entry
 };
 struct IndexedArgs {
     const uint32_t *tab;    // device table (global memory)
@@ -571,26 +575,31 @@ __device__ __forceinline__ uint32_t prefix_mask(uint32_t L) {
     return static_cast<uint32_t>(0xFFFFFFFF00000000ull >> L);
 }
 
-// Common test of a compact entry: addresses under their prefix lengths,
-// protocol, port blocks.  ks/kd: big-endian src/dst (top) words; pb: the
-// packet's port-block bits (1 << 16 + sport/8192 | 1 << 24 + dport/8192).
-__device__ __forceinline__ bool hyb_pass(const u32x4 &E, uint32_t ks, uint32_t kd, uint32_t proto, uint32_t pb) {
-    const uint32_t w = E.w;
-    const uint32_t pm = ((proto ^ E.z) & 0xFFu) & (0u - ((E.z >> 8) & 1u));
-    const uint32_t m = ((ks ^ E.x) & prefix_mask(w & 63u)) | ((kd ^ E.y) & prefix_mask((w >> 6) & 63u)) | pm;
-    const uint32_t q = w & pb;
-    return m == 0u && (q & 0x00FF0000u) != 0u && (q & 0xFF000000u) != 0u;
+// 12-byte pieces of the exact flat-form entries (table.hpp): an IPv4 entry
+// is two (the compiler issues dwordx4 + dwordx2), an IPv6 entry four.
+typedef uint32_t u32x3 __attribute__((ext_vector_type(3), aligned(4)));
+
+__device__ __forceinline__ u32x3 ld3(const uint32_t *__restrict__ p) { return *reinterpret_cast<const u32x3 *>(p); }
+
+// Mismatch bits of an exact entry's first six words (both families): top
+// address words under their prefix lengths (IPv6: capped at 32), protocol,
+// ports — acl.go:526-539 / 546-557 for IPv4 completely, for IPv6 up to the
+// low address words.  ks/kd: big-endian src/dst (top) words.
+__device__ __forceinline__ uint32_t hyb_miss(const u32x3 &A, const u32x3 &B, uint32_t ks, uint32_t kd, uint32_t proto,
+                                             uint32_t ports) {
+    const uint32_t sl = min(B.z & 0xFFu, 32u), dl = min((B.z >> 8) & 0xFFu, 32u);
+    const uint32_t pm = ((proto ^ A.z) & 0xFFu) & (0u - ((A.z >> 8) & 1u));
+    return ((ks ^ A.x) & prefix_mask(sl)) | ((kd ^ A.y) & prefix_mask(dl)) | pm | port_miss(ports, B.x, B.y);
 }
 
-// Exact confirmation on the cold record of rule `idx`: ports (l4ACL) and,
-// for IPv6, address words 1..3.
-__device__ __forceinline__ bool hyb_cold_ok(const IndexedArgs &a, bool v6, uint32_t idx, const Fields &f) {
-    const GlobalTab g{a.tab};
-    const uint32_t off = v6 ? a.f6.off_cold + idx * kHybCold6Dwords : a.f4.off_cold + idx * kHybCold4Dwords;
-    const u32x4 C = g.ld4(off);
-    uint32_t m = port_miss(f.ports, C.x, C.y);
-    if (v6) m |= entry_miss_ext(g, off + 4, f);
-    return m == 0u;
+// IPv6 address words 1..3 of an exact entry (C = src1 src2 src3, D = dst1
+// dst2 dst3) against big-endian packet words s[1..3], t[1..3].
+__device__ __forceinline__ uint32_t hyb_miss6(const u32x3 &C, const u32x3 &D, uint32_t lens, const uint32_t (&s)[4],
+                                              const uint32_t (&t)[4]) {
+    const int sl = static_cast<int>(lens & 0xFFu), dl = static_cast<int>((lens >> 8) & 0xFFu);
+    auto pm = [](int L, int k) { return prefix_mask(static_cast<uint32_t>(min(max(L - 32 * k, 0), 32))); };
+    return ((s[1] ^ C.x) & pm(sl, 1)) | ((s[2] ^ C.y) & pm(sl, 2)) | ((s[3] ^ C.z) & pm(sl, 3)) |
+           ((t[1] ^ D.x) & pm(dl, 1)) | ((t[2] ^ D.y) & pm(dl, 2)) | ((t[3] ^ D.z) & pm(dl, 3));
 }
 
 // ---- FLAT: a wave's candidates, 64 at a time --------------------------------
@@ -611,8 +620,8 @@ __device__ __forceinline__ bool hyb_cold_ok(const IndexedArgs &a, bool v6, uint3
 template <int R>
 struct FlatScratch {
     uint32_t mark[64 * R];   // window position -> (list id << 8 | position) + 1, 0 = none
-    uint32_t delta[64 * R];  // window position -> entry number - candidate number
-    uint32_t best[64];       // per packet (lane): lowest passing rule index
+    uint32_t delta[64 * R];  // window position -> (entry number - candidate number) << 1 | IPv6
+    uint64_t best[64];       // per packet (lane): lowest passing rule index << 32 | output code
 };
 
 // Order this wave's LDS writes before its following LDS reads of other lanes'
@@ -663,23 +672,31 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
     const bool mine = f.is4 || f.is6;
     const uint32_t ks = __builtin_bswap32(f.s[0]), kd = __builtin_bswap32(f.t[0]);
     const uint32_t sport = f.ports & 0xFFFFu, dport = f.ports >> 16;
-    const uint32_t key[4] = {kd, ks, dport, sport};
-    const u32x4 *G = reinterpret_cast<const u32x4 *>(a.tab);
-    // list bounds of this packet in every slot (directories in global memory)
+    // key[f] of a slot field f (SlotField; kFZero and unused slots: 0)
+    auto pick = [&](uint32_t fld) -> uint32_t {
+        return fld == kFDst ? kd : fld == kFSrc ? ks : fld == kFDport ? dport : fld == kFSport ? sport : 0u;
+    };
+    // list bounds of this packet in every slot (family-relative entry numbers)
     uint32_t st[NS], ln[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
         const SlotArgs &s4 = a.f4.slot[s], &s6 = a.f6.slot[s];
         const uint32_t shift = v6 ? s6.shift : s4.shift;
         const uint32_t dir = v6 ? s6.off_dir : s4.off_dir;
-        const uint32_t t = key[s] >> shift;
+        const uint32_t t = ((pick(v6 ? s6.f1 : s4.f1) >> shift) << (v6 ? s6.bits2 : s4.bits2)) |
+                           (pick(v6 ? s6.f2 : s4.f2) >> (v6 ? s6.shift2 : s4.shift2));
         if (LDS_DIRS) {
             uint32_t hi;
             SplitTab{a.tab}.bounds(dir, v6 ? s6.off_dir16 : s4.off_dir16, t, st[s], hi);
             ln[s] = mine ? hi - st[s] : 0u;
         } else {
-            st[s] = a.tab[dir + t];
-            ln[s] = mine ? a.tab[dir + t + 1] - st[s] : 0u;
+            // generalized slots: a family's unused slots (f1 == kFZero) read nothing
+            st[s] = 0u;
+            ln[s] = 0u;
+            if (mine && (v6 ? s6.f1 : s4.f1) != kFZero) {
+                st[s] = a.tab[dir + t];
+                ln[s] = a.tab[dir + t + 1] - st[s];
+            }
         }
     }
     uint32_t total = 0;
@@ -688,8 +705,10 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
     const uint32_t incl = wave_incl_sum(total);
     const uint32_t off = incl - total;  // first candidate number of this packet
     const uint32_t T = __builtin_amdgcn_readlane(incl, 63);
-    W.best[lane] = kNone;
+    W.best[lane] = ~0ull;
     const uint32_t proto_fam = f.proto | (v6 ? 0x100u : 0u);
+    const uint32_t *__restrict__ E4 = a.tab + a.f4.off_ent_base;
+    const uint32_t *__restrict__ E6 = a.tab + a.f6.off_ent_base;
     for (uint32_t win = 0; win < T; win += 64 * R) {
 #pragma unroll
         for (int j = 0; j < R; ++j) W.mark[64 * j + lane] = 0u;
@@ -700,15 +719,16 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
             if (ln[s] != 0u && so < win + 64u * R && so + ln[s] > win) {
                 const uint32_t pos = so > win ? so - win : 0u;
                 W.mark[pos] = (((lane * NS + s) << 8) | pos) + 1u;
-                W.delta[pos] = st[s] - so;
+                W.delta[pos] = ((st[s] - so) << 1) | (v6 ? 1u : 0u);
             }
             so += ln[s];
         }
         wave_lds_sync();
-        // R rounds: locate every candidate's list, then issue all R loads
-        uint32_t owner[R];
-        bool valid[R];
-        u32x4 E[R];
+        // R rounds: locate every candidate's list, then issue every round's
+        // entry loads (IPv6 candidates: all four pieces) before testing any
+        uint32_t owner[R], idx[R];
+        bool valid[R], six[R];
+        u32x3 A[R], B[R], C[R], D[R];
         uint32_t carry = 0;
 #pragma unroll
         for (int j = 0; j < R; ++j) {
@@ -717,94 +737,91 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
             const uint32_t k = win + 64u * j + lane;
             valid[j] = k < T;
             owner[j] = ((m - 1u) >> 8) / NS;
-            const uint32_t ent = k + W.delta[(m - 1u) & 0xFFu];
-            E[j] = G[valid[j] ? ent : 0u];
+            const uint32_t dp = W.delta[(m - 1u) & 0xFFu];
+            six[j] = (dp & 1u) != 0u;
+            const uint32_t ent = k + static_cast<uint32_t>(static_cast<int32_t>(dp) >> 1);
+            const uint32_t *e = six[j] ? E6 + ent * kHybEnt6Dwords : E4 + ent * kHybEnt4Dwords;
+            A[j] = B[j] = C[j] = D[j] = u32x3{0, 0, 0};
+            if (valid[j]) {
+                A[j] = ld3(e);
+                B[j] = ld3(e + 3);
+            }
+            if (valid[j] && six[j]) {
+                C[j] = ld3(e + 6);
+                D[j] = ld3(e + 9);
+            }
         }
-        // coarse test of every round, then the cold confirmations of all
-        // rounds together (one dependent round trip per window, not per round)
-        bool pass[R], cold[R];
-        uint32_t opt[R], opf[R];
+        bool pass[R];
+        bool any6 = false;
 #pragma unroll
         for (int j = 0; j < R; ++j) {
             // the owner packet's fields
             const uint32_t o = owner[j];
             const uint32_t oks = bperm(ks, o), okd = bperm(kd, o);
-            opf[j] = bperm(proto_fam, o);
-            opt[j] = bperm(f.ports, o);
-            const uint32_t osp = opt[j] & 0xFFFFu, odp = opt[j] >> 16;
-            const uint32_t pb = (1u << (16 + (osp >> kHybPortBlockShift))) | (1u << (24 + (odp >> kHybPortBlockShift)));
-            pass[j] = valid[j] && hyb_pass(E[j], oks, okd, opf[j] & 0xFFu, pb);
-            cold[j] = pass[j] && (E[j].w & kHybCold);
+            const uint32_t opf = bperm(proto_fam, o), opt = bperm(f.ports, o);
+            pass[j] = valid[j] && hyb_miss(A[j], B[j], oks, okd, opf & 0xFFu, opt) == 0u;
+            idx[j] = A[j].z >> kEntIndexShift;
+            any6 |= pass[j] && six[j];
         }
-        bool any_cold = false;
+        if (ballot(any6)) {  // IPv6 candidates: address words 1..3 of the owner
+            uint32_t sb[4], tb[4];
 #pragma unroll
-        for (int j = 0; j < R; ++j) any_cold |= cold[j];
-        if (ballot(any_cold)) {
-            const GlobalTab g{a.tab};
-            u32x4 C[R];
-#pragma unroll
-            for (int j = 0; j < R; ++j) {  // first 16 bytes of every needed cold record
-                const uint32_t idx = E[j].z >> kEntIndexShift;
-                const bool six = (opf[j] & 0x100u) != 0u;
-                const uint32_t off = six ? a.f6.off_cold + idx * kHybCold6Dwords : a.f4.off_cold + idx * kHybCold4Dwords;
-                C[j] = u32x4{0, 0xFFFFFFFFu, 0xFFFFFFFFu, 0};
-                if (cold[j]) C[j] = g.ld4(off);
+            for (int q = 1; q < 4; ++q) {
+                sb[q] = __builtin_bswap32(f.s[q]);
+                tb[q] = __builtin_bswap32(f.t[q]);
             }
 #pragma unroll
             for (int j = 0; j < R; ++j) {
-                const bool six = (opf[j] & 0x100u) != 0u;
-                if (cold[j]) pass[j] = port_miss(opt[j], C[j].x, C[j].y) == 0u;
-                if (ballot(cold[j] && six && pass[j])) {
-                    // owner's IPv6 address words 1..3 (whole wave: bpermute reads every lane)
-                    Fields of;
-                    const uint32_t o = owner[j];
+                if (ballot(pass[j] && six[j])) {  // whole wave: bpermute reads every lane
+                    uint32_t os[4] = {0, 0, 0, 0}, ot[4] = {0, 0, 0, 0};
 #pragma unroll
                     for (int q = 1; q < 4; ++q) {
-                        of.s[q] = bperm(f.s[q], o);
-                        of.t[q] = bperm(f.t[q], o);
+                        os[q] = bperm(sb[q], owner[j]);
+                        ot[q] = bperm(tb[q], owner[j]);
                     }
-                    if (cold[j] && six && pass[j]) {
-                        const uint32_t idx = E[j].z >> kEntIndexShift;
-                        pass[j] = entry_miss_ext(g, a.f6.off_cold + idx * kHybCold6Dwords + 4, of) == 0u;
-                    }
+                    if (pass[j] && six[j]) pass[j] = hyb_miss6(C[j], D[j], B[j].z, os, ot) == 0u;
                 }
             }
         }
 #pragma unroll
-        for (int j = 0; j < R; ++j) {
-            // rule index << 3 | output code: the minimum carries the winner's output
-            const uint32_t idx = E[j].z >> kEntIndexShift;
-            if (pass[j]) atomicMin(&W.best[owner[j]], (idx << 3) | ((E[j].w >> kHybOutShift) & 7u));
-        }
+        for (int j = 0; j < R; ++j)  // rule index << 32 | output code: the minimum carries the winner's output
+            if (pass[j]) atomicMin(reinterpret_cast<unsigned long long *>(&W.best[owner[j]]),
+                                   static_cast<unsigned long long>(idx[j]) << 32 | (B[j].z >> kHybOutShift));
         wave_lds_sync();
     }
-    uint32_t best = W.best[lane];  // kNone or rule index << 3 | output code
+    uint64_t best = W.best[lane];  // ~0 or rule index << 32 | output code
     // rules with no selective key: wave-uniform scan in rule order per family
-    const uint32_t pb = (1u << (16 + (sport >> kHybPortBlockShift))) | (1u << (24 + (dport >> kHybPortBlockShift)));
 #pragma unroll
     for (int fam = 0; fam < 2; ++fam) {
         const FamArgs &fa = fam ? a.f6 : a.f4;
         const bool in_fam = fam ? f.is6 : f.is4;
+        const uint32_t ew = fam ? kHybEnt6Dwords : kHybEnt4Dwords;
         for (uint32_t i = 0; i < fa.n_resid; ++i) {
-            const u32x4 E = G[(fa.off_resid >> 2) + i];
-            const uint32_t idx = E.z >> kEntIndexShift;
-            const bool want = in_fam && idx < (best >> 3);
+            const uint32_t *e = a.tab + fa.off_resid + i * ew;
+            const u32x3 RA = ld3(e), RB = ld3(e + 3);
+            const uint32_t ri = RA.z >> kEntIndexShift;
+            const bool want = in_fam && ri < uint32_t(best >> 32);
             if (!ballot(want)) break;  // residual list ascends too
-            bool pass = want && hyb_pass(E, ks, kd, f.proto, pb);
-            const bool cold = pass && (E.w & kHybCold);
-            if (ballot(cold)) {
-                if (cold) pass = hyb_cold_ok(a, fam == 1, idx, f);
+            bool ok = want && hyb_miss(RA, RB, ks, kd, f.proto, f.ports) == 0u;
+            if (fam && ballot(ok)) {
+                uint32_t sb[4] = {0, 0, 0, 0}, tb[4] = {0, 0, 0, 0};
+#pragma unroll
+                for (int q = 1; q < 4; ++q) {
+                    sb[q] = __builtin_bswap32(f.s[q]);
+                    tb[q] = __builtin_bswap32(f.t[q]);
+                }
+                if (ok) ok = hyb_miss6(ld3(e + 6), ld3(e + 9), RB.z, sb, tb) == 0u;
             }
-            best = pass ? (idx << 3) | ((E.w >> kHybOutShift) & 7u) : best;
+            best = ok ? (uint64_t(ri) << 32 | (RB.z >> kHybOutShift)) : best;
         }
     }
-    // output numbers below 7 travel in the entry; others come from the cold record
-    const bool hit = best != kNone;
-    uint32_t out = hit ? best & 7u : 0u;
-    const bool rd = hit && out == kHybOutCold;
+    // output numbers below kHybOutEscape travel in the entry; others come from the output array
+    const bool hit = best != ~0ull;
+    uint32_t out = hit ? static_cast<uint32_t>(best) : 0u;
+    const bool rd = hit && out == kHybOutEscape;
     if (ballot(rd)) {
-        const uint32_t r = best >> 3;
-        if (rd) out = a.tab[v6 ? a.f6.off_cold + r * kHybCold6Dwords + 2 : a.f4.off_cold + r * kHybCold4Dwords + 2];
+        const uint32_t r = static_cast<uint32_t>(best >> 32);
+        if (rd) out = a.tab[(v6 ? a.f6.off_cold : a.f4.off_cold) + r];
     }
     return out;
 }
@@ -823,9 +840,12 @@ __device__ __forceinline__ uint32_t classify_any(const IndexedArgs &a, const Fie
         const uint32_t lane = lane_id();
         return classify_flat<NS, R, true>(a, f, W[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)], lane);
     }
-    if (TM == kTabLds) return classify_indexed<NS, 1>(LdsTab{}, a, f);
-    if (TM == kTabSplit) return classify_indexed<NS, 1>(SplitTab{a.tab}, a, f);
-    return classify_indexed<NS, 1>(GlobalTab{a.tab}, a, f);
+    if constexpr (NS <= 4) {  // per-lane walks: the positional four slots
+        if (TM == kTabLds) return classify_indexed<NS, 1>(LdsTab{}, a, f);
+        if (TM == kTabSplit) return classify_indexed<NS, 1>(SplitTab{a.tab}, a, f);
+        return classify_indexed<NS, 1>(GlobalTab{a.tab}, a, f);
+    }
+    return 0u;
 }
 
 // Grid-stride over 64-packet batches.
@@ -1037,19 +1057,39 @@ static uint32_t grid_for(const nffacl_engine *eng, uint64_t n, uint32_t block, u
     return static_cast<uint32_t>(std::max<uint64_t>(1, std::min(blocks_needed, cap)));
 }
 
+// SlotField of a KeyKind (kernel key[] index).
+static uint32_t field_of(uint32_t kind) {
+    switch (kind) {
+    case kKeyDst4: case kKeyDst6: return kFDst;
+    case kKeySrc4: case kKeySrc6: return kFSrc;
+    case kKeyDport: return kFDport;
+    case kKeySport: return kFSport;
+    default: return kFZero;
+    }
+}
+
 static dev::IndexedArgs indexed_args(const DevTable *t) {
     dev::IndexedArgs a{};
     a.tab = t->d_blob;
     const bool hyb = t->meta.algo == NFFACL_ALGO_HYBRID;
     a.stage_dwords = hyb ? t->meta.lds_dwords : static_cast<uint32_t>(t->meta.blob.size());
     auto fam = [&](const FamilyIndex &fi, uint32_t off_cold, dev::FamArgs &fa) {
-        for (uint32_t k = 0; k < 4; ++k) {
+        for (uint32_t k = 0; k < kMaxSlots; ++k) {
             const DimInfo &d = fi.dims[k];
-            fa.slot[k] = dev::SlotArgs{d.shift, d.off_dir, d.off_ent, d.off_dir16};
+            if (t->meta.slots_g && k >= fi.used_slots) {  // unused: key 0 into an empty directory
+                fa.slot[k] = dev::SlotArgs{0, t->meta.off_empty_dir, 0, 0, kFZero, kFZero, 0, 0};
+                continue;
+            }
+            // positional forms: slot k keys on field k ([dst, src, dport, sport]);
+            // generalized slots (global-directory HYBRID): the fields compiled
+            const uint32_t f1 = t->meta.slots_g ? field_of(d.kind) : k;
+            const uint32_t f2 = t->meta.slots_g ? field_of(d.kind2) : uint32_t(kFZero);
+            fa.slot[k] = dev::SlotArgs{d.shift, d.off_dir, d.off_ent, d.off_dir16, f1, f2, d.shift2, d.bits2};
         }
         fa.off_resid = fi.off_resid;
         fa.n_resid = fi.n_resid;
         fa.off_cold = off_cold;
+        fa.off_ent_base = fi.off_ent_base;
     };
     fam(t->meta.idx4, t->meta.off_rec4, a.f4);
     fam(t->meta.idx6, t->meta.off_rec6, a.f6);
@@ -1072,8 +1112,8 @@ struct IndexedLaunch {
 static bool table_consistent(const DevTable *t) {
     const CompiledTable &m = t->meta;
     const size_t dw = m.blob.size();
-    if (m.algo == NFFACL_ALGO_HYBRID && (m.lds_dwords == 0 || m.idx4.entry_dwords == kHybEntDwords))
-        return m.idx4.entry_dwords == kHybEntDwords && m.idx6.entry_dwords == kHybEntDwords &&
+    if (m.algo == NFFACL_ALGO_HYBRID && (m.lds_dwords == 0 || m.idx4.entry_dwords == kHybEnt4Dwords))
+        return m.idx4.entry_dwords == kHybEnt4Dwords && m.idx6.entry_dwords == kHybEnt6Dwords &&
                m.off_rec4 <= dw && m.off_rec6 <= dw &&
                size_t(m.lds_dwords) * sizeof(uint32_t) <= kHybLdsDirMaxBytes && m.lds_dwords <= dw;
     if (m.algo == NFFACL_ALGO_HYBRID)
@@ -1100,7 +1140,7 @@ static IndexedLaunch indexed_launch(const nffacl_engine *eng, const DevTable *t)
         L.lds_bytes = (r2 ? sizeof(dev::FlatScratch<2>) : sizeof(dev::FlatScratch<4>)) * (L.block / 64);
         return L;
     }
-    if (t->meta.algo == NFFACL_ALGO_HYBRID && t->meta.idx4.entry_dwords == kHybEntDwords) {  // flat-LDS
+    if (t->meta.algo == NFFACL_ALGO_HYBRID && t->meta.idx4.entry_dwords == kHybEnt4Dwords) {  // flat-LDS
         L.block = tu.block ? static_cast<uint32_t>(tu.block) : 1024u;
         L.per_cu = tu.per_cu ? static_cast<uint32_t>(tu.per_cu) : 1u;
         const size_t image = size_t(t->meta.lds_dwords) * sizeof(uint32_t);
@@ -1173,21 +1213,36 @@ static void dispatch_indexed(int ns, int tm, F &&f) {
         default: f(nsc, std::integral_constant<int, dev::kTabGlobal>{}); break;
         }
     };
+    // generalized slots (global-directory flat kernels only): up to kMaxSlots
+    auto with_ns_flat = [&](auto nsc) {
+        switch (tm) {
+        case dev::kTabFlat: f(nsc, std::integral_constant<int, dev::kTabFlat>{}); break;
+        case dev::kTabFlatLds: f(nsc, std::integral_constant<int, dev::kTabFlatLds>{}); break;
+        case dev::kTabFlatLds4: f(nsc, std::integral_constant<int, dev::kTabFlatLds4>{}); break;
+        default: f(nsc, std::integral_constant<int, dev::kTabFlat4>{}); break;
+        }
+    };
     if (ns == 2) with_ns(std::integral_constant<int, 2>{});
     else if (ns == 3) with_ns(std::integral_constant<int, 3>{});
-    else with_ns(std::integral_constant<int, 4>{});
+    else if (ns == 4) with_ns(std::integral_constant<int, 4>{});
+    else if (ns == 5) with_ns_flat(std::integral_constant<int, 5>{});
+    else if (ns == 6) with_ns_flat(std::integral_constant<int, 6>{});
+    else if (ns == 7) with_ns_flat(std::integral_constant<int, 7>{});
+    else with_ns_flat(std::integral_constant<int, 8>{});
 }
 
 int prepare_kernels() {
     static std::once_flag once;
     static hipError_t err = hipSuccess;
     std::call_once(once, [] {
-        for (int ns = 2; ns <= 4; ++ns)
-            for (int tm : {int(dev::kTabLds), int(dev::kTabSplit), int(dev::kTabFlatLds), int(dev::kTabFlatLds4)})
+        for (int ns = 2; ns <= int(kMaxSlots); ++ns)
+            for (int tm : {int(dev::kTabLds), int(dev::kTabSplit), int(dev::kTabFlatLds), int(dev::kTabFlatLds4)}) {
+                if (ns > 4 && tm != dev::kTabFlatLds && tm != dev::kTabFlatLds4) continue;  // flat walks only
                 dispatch_indexed(ns, tm, [&](auto nsc, auto tmc) {
                     const hipError_t e = allow_lds_modes<decltype(nsc)::value, decltype(tmc)::value>();
                     if (e != hipSuccess) err = e;
                 });
+            }
     });
     if (err != hipSuccess) {
         set_last_error(std::string("hipFuncSetAttribute(LDS): ") + hipGetErrorString(err));
@@ -1202,12 +1257,12 @@ static void launch_slots_tm(int mode, const IndexedLaunch &L, uint32_t grid, hip
                             uint32_t *d_port, uint64_t *d_permit) {
     const dim3 g(grid), b(L.block);
     const size_t lds = TM == dev::kTabGlobal ? 0 : L.lds_bytes;
-    if (TM == dev::kTabFlat || TM == dev::kTabFlat4 || TM == dev::kTabFlatLds || TM == dev::kTabFlatLds4) {  // built with load modes 0 and 4 only
+    if constexpr (TM != dev::kTabLds) {  // built with load modes 0 and 4 only
         if (mode == 0)
             hipLaunchKernelGGL((dev::k_indexed_slots<NS, TM, 0>), g, b, lds, stream, d_slots, stride, n, a, d_port, d_permit);
         else
             hipLaunchKernelGGL((dev::k_indexed_slots<NS, TM, 4>), g, b, lds, stream, d_slots, stride, n, a, d_port, d_permit);
-    } else if (TM == dev::kTabLds && mode >= 1 && mode <= 3) {
+    } else if (mode >= 1 && mode <= 3) {
         if (mode == 1)
             hipLaunchKernelGGL((dev::k_indexed_slots<NS, dev::kTabLds, 1>), g, b, lds, stream, d_slots, stride, n, a, d_port, d_permit);
         else if (mode == 2)

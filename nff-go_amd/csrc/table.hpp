@@ -67,58 +67,54 @@ constexpr uint32_t kMaxIndexedRules = 1u << 23;
 // Same slot assignment and ascending bucket lists as the indexed table, with
 // the eight directories (both families) first in the blob, in one of three
 // forms:
-//  * flat-LDS (default; lds_dwords > 0, entry_dwords == kHybEntDwords): the
+//  * flat-LDS (default; lds_dwords > 0, entry_dwords == kHybEnt4Dwords): the
 //    directories, radix widths chosen to fit kHybLaneDirBytes, are the LDS
 //    image — two-level (kDir16GroupShift) when every group fits u16
-//    offsets — holding absolute entry numbers (16-byte units of the blob;
-//    two-level: in the base words); a wave tests its packets' candidates 64
-//    at a time, list entries compact (below);
+//    offsets — holding family-relative entry numbers (two-level: in the base
+//    words); a wave tests its packets' candidates 64 at a time, list entries
+//    exact (below);
 //  * lane form (forced; lds_dwords > 0, INDEXED entry sizes): the same LDS
 //    directories, values relative to the slot's entries; the lists hold
 //    INDEXED's inline entries read from global memory, each lane walking its
 //    own lists;
 //  * flat form (forced, or directory budgets past LDS; lds_dwords == 0):
-//    plain u32 directories sized to kHybFlatDirBytes read from global
-//    memory, values and entries as flat-LDS.
-// A compact list entry is 16 bytes:
-//      [0] src word, big-endian value (IPv6: top 32 bits)
-//      [1] dst word, big-endian value
+//    plain u32 directories read from global memory, values and entries as
+//    flat-LDS; with generalized slots (CompiledTable::slots_g) each slot keys
+//    on one field or on a 2-D grid of two fields' top bits.
+// A flat-form list entry is EXACT — a candidate needs no second read:
+//   IPv4, 6 dwords (24 B):
+//      [0] src word, big-endian value   [1] dst word, big-endian value
 //      [2] meta = id | exact << 8 | rule_index << 9          (as inline)
-//      [3] src_len | dst_len << 6 | cold << 12 | out << 13 | sport_blocks << 16 | dport_blocks << 24
-//    with prefix lengths (IPv6: capped at 32), the output number when < 7
-//    (7: read it from the cold record) and 8-bit port-block bitmaps (bit b:
-//    the rule's range meets ports [8192 b, 8192 b + 8191]); cold records,
-//    one per rule in rule order, hold what the entry cannot:
-//      IPv4 (4 dwords): lo, hi, output_number, 0
-//      IPv6 (16 dwords): lo, hi, output_number, 0, then the 12 extension words
-//      of the inline entry (src[1..3], src_mask[1..3], dst[1..3], dst_mask[1..3]).
-//    An entry with the cold bit (port ranges not made of whole blocks, IPv6
-//    prefixes longer than 32) is confirmed against its cold record.
+//      [3] lo = sport_min | dport_min << 16   [4] hi = sport_max | dport_max << 16
+//          (IPv4 rules without a port check: 0 / 0xffffffff)
+//      [5] src_len | dst_len << 8 | out << 16
+//   IPv6, 12 dwords (48 B): the same six words with the top 32 address bits
+//      and prefix lengths 0..128, then [6..8] src words 1..3, [9..11] dst
+//      words 1..3 (big-endian values).
+// `out` is the OutputNumber when < kHybOutEscape; otherwise it is read from
+// the family's output array (one u32 per rule, in rule order; off_rec4 /
+// off_rec6).  Loads are 12-byte (dwordx3): two per IPv4 entry, four per IPv6.
 // The hybrid forms encode only CIDR masks and id_mask in {0, 0xff} (what
 // the parsers produce); other rule sets compile INDEXED.
-constexpr uint32_t kHybEntDwords = 4;
-constexpr uint32_t kHybCold = 1u << 12;
-constexpr uint32_t kHybOutShift = 13;
-constexpr uint32_t kHybOutCold = 7;  // output number >= 7: read from the cold record
-constexpr uint32_t kHybPortBlockShift = 13;
-constexpr uint32_t kHybPortBlockMask = (1u << kHybPortBlockShift) - 1u;
-constexpr uint32_t kHybCold4Dwords = 4;
-constexpr uint32_t kHybCold6Dwords = 16;
+constexpr uint32_t kHybEnt4Dwords = 6;
+constexpr uint32_t kHybEnt6Dwords = 12;
+constexpr uint32_t kHybOutShift = 16;
+constexpr uint32_t kHybOutEscape = 0xFFFFu;  // output number >= this: read from the output array
 // Directory budgets (both families), see above.  128 KiB of LDS directories
 // leave one 1024-thread workgroup per CU; measured faster than 64 KiB with
 // two (C3: 0.64 vs 0.69 ms, profiles/r1_hybrid/).
 constexpr size_t kHybLaneDirBytes = 128 * 1024;
 constexpr size_t kHybFlatDirBytes = 1024 * 1024;
 // Largest LDS directory image of the flat-LDS form: 160 KiB minus the 16
-// waves' candidate scratch (engine.hip FlatScratch<2>, 1280 B each) and 1 KiB.
-constexpr size_t kHybLdsDirMaxBytes = 139 * 1024;
+// waves' candidate scratch (engine.hip FlatScratch<2>, 1536 B each) and 1 KiB.
+constexpr size_t kHybLdsDirMaxBytes = 135 * 1024;
 // Rounds of candidate loads in flight in the flat-LDS walk: 4 when the
 // expected candidates per packet exceed kHybFlat4Candidates (C5: E ≈ 10,
 // 0.855 vs 0.895 ms), else 2 (C3: E ≈ 1.3, 0.526 vs 0.541 ms;
-// profiles/r1_flat_lds/tune/).  4 rounds need 2304 B of scratch per wave,
+// profiles/r1_flat_lds/tune/).  4 rounds need 2560 B of scratch per wave,
 // so their directories get kHybFlat4DirBytes.
 constexpr double kHybFlat4Candidates = 6.0;
-constexpr size_t kHybFlat4DirBytes = 120 * 1024;
+constexpr size_t kHybFlat4DirBytes = 116 * 1024;
 // Lane-form directories are two-level: a u32 base per group of 64 buckets +
 // a u16 offset per bucket (2.06 B per bucket instead of 4), so the LDS budget
 // holds twice the buckets.  A group whose lists exceed 65535 entries keeps
@@ -134,6 +130,13 @@ enum KeyKind : uint32_t {
     kKeyDst6 = 3,   // IPv6 destination address, top 32 bits
     kKeySport = 4,  // L4 source port
     kKeyDport = 5,  // L4 destination port
+    kKeyNone = 6,   // no second key (1-D slot)
 };
+
+// Slots per family in the HYBRID global-directory form (nffacl.h NFFACL_MAX_SLOTS).
+constexpr uint32_t kMaxSlots = 8;
+// Packet-side key fields of a slot (kernel key[] order): destination address
+// (IPv6: top 32 bits), source address, destination port, source port, zero.
+enum SlotField : uint32_t { kFDst = 0, kFSrc = 1, kFDport = 2, kFSport = 3, kFZero = 4 };
 
 }  // namespace nffacl

@@ -18,12 +18,19 @@ from oracle import oracle, rules_oracle as ro
 class DimInfo(ctypes.Structure):
     _fields_ = [("kind", ctypes.c_uint32), ("shift", ctypes.c_uint32), ("n_buckets", ctypes.c_uint32),
                 ("off_dir", ctypes.c_uint32), ("off_entries", ctypes.c_uint32), ("n_rules", ctypes.c_uint32),
-                ("max_list", ctypes.c_uint32), ("off_dir16", ctypes.c_uint32), ("n_entries", ctypes.c_uint64)]
+                ("max_list", ctypes.c_uint32), ("off_dir16", ctypes.c_uint32), ("n_entries", ctypes.c_uint64),
+                ("kind2", ctypes.c_uint32), ("shift2", ctypes.c_uint32), ("bits2", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32)]
+
+
+MAX_SLOTS = 8
+KIND_NONE = 6
 
 
 class FamInfo(ctypes.Structure):
     _fields_ = [("n_rec", ctypes.c_uint32), ("off_rec", ctypes.c_uint32), ("entry_dwords", ctypes.c_uint32),
-                ("off_resid", ctypes.c_uint32), ("n_resid", ctypes.c_uint32), ("dims", DimInfo * 4)]
+                ("off_resid", ctypes.c_uint32), ("n_resid", ctypes.c_uint32), ("dims", DimInfo * MAX_SLOTS),
+                ("n_slots", ctypes.c_uint32), ("off_ent_base", ctypes.c_uint32)]
 
 
 class TableInfo(ctypes.Structure):
@@ -85,6 +92,15 @@ def match(blob, offs, v6, F, sel):
 
 KEYS = {0: lambda F: bswap(F["s"][0]), 1: lambda F: bswap(F["t"][0]), 2: lambda F: bswap(F["s"][0]),
         3: lambda F: bswap(F["t"][0]), 4: lambda F: F["sp"], 5: lambda F: F["dp"]}
+
+
+def bucket_of(di, F):
+    """Bucket index of every packet in slot di: key >> shift, or for a 2-D
+    slot (kind2 != none) (key >> shift) << bits2 | key2 >> shift2."""
+    t = KEYS[di.kind](F).astype(np.uint64) >> np.uint64(di.shift)
+    if di.kind2 != KIND_NONE:
+        t = (t << np.uint64(di.bits2)) | (KEYS[di.kind2](F).astype(np.uint64) >> np.uint64(di.shift2))
+    return t.astype(np.int64)
 
 
 def dir_values(blob, di):
@@ -224,83 +240,69 @@ def pmask(L):
 
 
 def hyb_test(blob, info, offs, v6, F, sel):
-    """Common test of the compact entries at dword offsets offs[i] against
-    packet sel[i], confirmed on the cold record where the cold bit is set;
-    returns (ok, rule index)."""
-    e = blob[offs[:, None] + np.arange(4)[None, :]]
-    ks, kd = bswap(F["s"][0][sel]), bswap(F["t"][0][sel])
-    w = e[:, 3]
-    m = ((ks ^ e[:, 0]) & pmask(w & 63)) | ((kd ^ e[:, 1]) & pmask((w >> 6) & 63))
+    """Exact flat-form entries (table.hpp) at dword offsets offs[i] against
+    packet sel[i]: addresses under their prefix lengths, protocol, ports;
+    returns (ok, rule index, output code)."""
+    ew = 12 if v6 else 6
+    e = blob[offs[:, None] + np.arange(ew)[None, :]]
+    lens = e[:, 5]
+    sl, dl = (lens & 0xFF).astype(np.int64), ((lens >> 8) & 0xFF).astype(np.int64)
+    m = np.zeros(len(sel), np.uint32)
+    for k in range(4 if v6 else 1):
+        rs = e[:, 0] if k == 0 else e[:, 5 + k]
+        rd = e[:, 1] if k == 0 else e[:, 8 + k]
+        m |= (bswap(F["s"][k][sel]) ^ rs) & pmask(np.clip(sl - 32 * k, 0, 32))
+        m |= (bswap(F["t"][k][sel]) ^ rd) & pmask(np.clip(dl - 32 * k, 0, 32))
     meta = e[:, 2]
-    m |= np.where((meta >> 8) & 1 == 1, (F["proto"][sel] ^ meta) & 0xFF, 0)
+    m |= np.where((meta >> 8) & 1 == 1, (F["proto"][sel] ^ meta) & 0xFF, 0).astype(np.uint32)
     sp, dp = F["sp"][sel].astype(np.uint32), F["dp"][sel].astype(np.uint32)
-    pb = (np.uint32(1) << (16 + (sp >> 13))) | (np.uint32(1) << (24 + (dp >> 13)))
-    q = w & pb
-    ok = (m == 0) & ((q & 0x00FF0000) != 0) & ((q & 0xFF000000) != 0)
-    idx = (meta >> 9).astype(np.uint64)
-    cold = ok & ((w >> 12) & 1 == 1)
-    if cold.any():
-        c = np.nonzero(cold)[0]
-        cw = 16 if v6 else 4
-        off = info.fam[int(v6)].off_rec + idx[c].astype(np.int64) * cw
-        C = blob[off[:, None] + np.arange(cw)[None, :]]
-        lo, hi = C[:, 0], C[:, 1]
-        s2, d2 = sp[c], dp[c]
-        okc = (s2 >= (lo & 0xFFFF)) & (s2 <= (hi & 0xFFFF)) & (d2 >= (lo >> 16)) & (d2 <= (hi >> 16))
-        if v6:  # s1 s2 s3 sm1 sm2 sm3 t1 t2 t3 tm1 tm2 tm3
-            sc = sel[c]
-            x = np.zeros(len(c), np.uint32)
-            for k in range(3):
-                x |= (F["s"][k + 1][sc] ^ C[:, 4 + k]) & C[:, 7 + k]
-                x |= (F["t"][k + 1][sc] ^ C[:, 10 + k]) & C[:, 13 + k]
-            okc &= x == 0
-        ok[c] = okc
-    return ok, idx
+    lo, hi = e[:, 3], e[:, 4]
+    ok = (m == 0) & (sp >= (lo & 0xFFFF)) & (sp <= (hi & 0xFFFF)) & (dp >= (lo >> 16)) & (dp <= (hi >> 16))
+    return ok, (meta >> 9).astype(np.uint64), (lens >> 16).astype(np.uint32)
 
 
 def emulate_hybrid(blob, info, F, n):
-    """Flat form: every candidate of every list (no early exit), the minimum
-    passing rule index wins; its output number from the entry's 3-bit code,
-    or from the cold record when the code is 7."""
+    """Flat forms: every candidate of every list (no early exit), the minimum
+    passing rule index wins; its output number from the entry's 16-bit code,
+    or from the family's output array when the code is 0xFFFF."""
     best = np.full(n, 0xFFFFFFFF, np.uint64)
     code = np.zeros(n, np.uint32)
 
-    def post(sel, ok, idx, w):
+    def post(sel, ok, idx, out):
         better = ok & (idx < best[sel])
         best[sel[better]] = idx[better]
-        code[sel[better]] = (w[better] >> 13) & 7
+        code[sel[better]] = out[better]
 
     for fam, v6 in ((0, False), (1, True)):
         fi = info.fam[fam]
+        ew = fi.entry_dwords
+        assert ew == (12 if v6 else 6)
         mine = F["is6"] if v6 else F["is4"]
-        for d in range(4):
+        for d in range(fi.n_slots):
             di = fi.dims[d]
             if di.n_rules == 0:
                 continue
-            key = KEYS[di.kind](F).astype(np.uint64)
             dirv = dir_values(blob, di)  # global (flat) or LDS image (flat-LDS)
-            t = (key >> np.uint64(di.shift)).astype(np.int64)
+            t = bucket_of(di, F)
+            assert (t < di.n_buckets).all()
             start, end = dirv[t], dirv[t + 1]
             for k in range(di.max_list):
                 live = mine & (start + k < end)
                 if not live.any():
                     break
                 sel = np.nonzero(live)[0]
-                offs = (start[sel] + k) * 4
-                ok, idx = hyb_test(blob, info, offs, v6, F, sel)
-                post(sel, ok, idx, blob[offs + 3])
+                offs = fi.off_ent_base + (start[sel] + k) * ew
+                post(sel, *hyb_test(blob, info, offs, v6, F, sel))
         for i in range(fi.n_resid):
             sel = np.nonzero(mine)[0]
-            offs = np.full(len(sel), fi.off_resid + 4 * i)
-            ok, idx = hyb_test(blob, info, offs, v6, F, sel)
-            post(sel, ok, idx, blob[offs + 3])
+            offs = np.full(len(sel), fi.off_resid + ew * i)
+            post(sel, *hyb_test(blob, info, offs, v6, F, sel))
     out = np.zeros(n, np.uint32)
     hit = best != 0xFFFFFFFF
     out[hit] = code[hit]
     for fam, v6 in ((0, False), (1, True)):
-        rd = (F["is6"] if v6 else F["is4"]) & hit & (code == 7)
-        cw = 16 if v6 else 4
-        out[rd] = blob[info.fam[fam].off_rec + best[rd].astype(np.int64) * cw + 2]
+        rd = (F["is6"] if v6 else F["is4"]) & hit & (code == 0xFFFF)
+        out[rd] = blob[info.fam[fam].off_rec + best[rd].astype(np.int64)]
     return best, out
 
 
@@ -313,8 +315,8 @@ def check_hybrid(text: str, slots: np.ndarray, n: int, dir_kb=None, monkeypatch=
     a4, a6 = ro.parse_text_table(text.encode()).arrays()
     want, _ = oracle.classify_slots_which(slots, 64, n, a4, a6)
     F = fields(slots, n)
-    # lane form (directories in LDS): INDEXED's inline entries; flat form: compact + cold
-    lane = info.fam[0].entry_dwords != 4  # compact 16-byte entries: a flat form
+    # lane form (directories in LDS): INDEXED's inline entries; flat forms: exact 6/12-dword entries
+    lane = info.fam[0].entry_dwords == 8
     best, out = emulate(blob, info, F, n) if lane else emulate_hybrid(blob, info, F, n)
     sel = ~F["skip"]
     got = np.where(best != 0xFFFFFFFF, out, 0)
@@ -341,7 +343,7 @@ def test_hybrid_lds_forms_u32_directories(monkeypatch, flat):
     n = 1 << 14
     info = check_hybrid(g.text, synth.gen_slots(g, n, 41), n)
     assert info.lds_dwords > 0 and info.fam[0].dims[0].off_dir16 == 0
-    assert (info.fam[0].entry_dwords == 4) == (flat == 2)
+    assert (info.fam[0].entry_dwords == 6) == (flat == 2)
 
 
 @pytest.mark.parametrize("cfg", ["c2", "c3", "c5"])
@@ -393,7 +395,7 @@ def test_hybrid_flat_form_synthetic(cfg, monkeypatch):
     g = synth.gen_rules(synth.SPECS[cfg], synth.RULE_SEEDS[cfg])
     n = 1 << 14
     info = check_hybrid(g.text, synth.gen_slots(g, n, 31), n, dir_kb=1024, monkeypatch=monkeypatch)
-    assert info.lds_dwords == 0 and info.fam[0].entry_dwords == 4
+    assert info.lds_dwords == 0 and info.fam[0].entry_dwords == 6
 
 
 def test_hybrid_falls_back_on_non_cidr_masks():
@@ -405,18 +407,37 @@ def test_hybrid_falls_back_on_non_cidr_masks():
 
 
 def test_hybrid_policy_c5_flat(monkeypatch):
-    """C5 (100k rules): the default is the flat-LDS form (compact entries,
-    LDS directories); NFFACL_TUNE_FLAT=1 gives wide global directories
-    (lds_dwords == 0).  Both give the oracle's first match."""
+    """C5 (100k rules): the flat-LDS form (compact entries, LDS directories)
+    and, with NFFACL_TUNE_FLAT=1, global directories with generalized 1-D /
+    2-D slots (lds_dwords == 0).  Both give the oracle's first match."""
     g = synth.gen_rules(synth.SPECS["c5"], synth.RULE_SEEDS["c5"])
     n = 1 << 12
     slots = synth.gen_slots(g, n, synth.PACKET_SEEDS["c5"])
+    monkeypatch.setenv("NFFACL_TUNE_FLAT", "2")
     info = check_hybrid(g.text, slots, n)
-    assert 0 < info.lds_dwords * 4 <= 139 * 1024 and info.fam[0].entry_dwords == 4
+    assert 0 < info.lds_dwords * 4 <= 135 * 1024 and info.fam[0].entry_dwords == 6
     assert info.fam[0].dims[3].n_rules == 0  # sparse source-port slot folded away
     monkeypatch.setenv("NFFACL_TUNE_FLAT", "1")
     info = check_hybrid(g.text, slots, n)
-    assert info.lds_dwords == 0 and info.fam[0].entry_dwords == 4
+    assert info.lds_dwords == 0 and info.fam[0].entry_dwords == 6
+    assert any(info.fam[0].dims[k].kind2 != KIND_NONE for k in range(info.fam[0].n_slots))  # 2-D slots
+
+
+@pytest.mark.parametrize("cfg", ["c2", "c3", "c5"])
+@pytest.mark.parametrize("flat,slots2d", [("1", "0"), ("1", "1"), ("2", "2")])
+def test_hybrid_generalized_slots(cfg, flat, slots2d, monkeypatch):
+    """Generalized slots (global directories, or LDS-budgeted two-level ones):
+    every rule listed in every bucket of its 1-D or 2-D slot that its ranges
+    meet; first match == oracle."""
+    monkeypatch.setenv("NFFACL_TUNE_FLAT", flat)
+    monkeypatch.setenv("NFFACL_TUNE_SLOTS2D", slots2d)
+    g = synth.gen_rules(synth.SPECS[cfg], synth.RULE_SEEDS[cfg])
+    n = 1 << 13
+    info = check_hybrid(g.text, synth.gen_slots(g, n, 61), n)
+    for fam in info.fam:
+        assert 1 <= fam.n_slots <= MAX_SLOTS
+        for k in range(fam.n_slots):
+            assert fam.dims[k].n_rules > 0
 
 
 @pytest.mark.parametrize("cfg", ["c3", "c5"])
@@ -428,5 +449,23 @@ def test_hybrid_flat_lds_form(cfg, monkeypatch):
     g = synth.gen_rules(synth.SPECS[cfg], synth.RULE_SEEDS[cfg])
     n = 1 << 13
     info = check_hybrid(g.text, synth.gen_slots(g, n, 51), n)
-    assert 0 < info.lds_dwords * 4 <= 139 * 1024
-    assert info.fam[0].entry_dwords == 4 and info.fam[0].dims[0].off_dir16 != 0
+    assert 0 < info.lds_dwords * 4 <= 135 * 1024
+    assert info.fam[0].entry_dwords == 6 and info.fam[0].dims[0].off_dir16 != 0
+
+
+@pytest.mark.parametrize("flat", ["1", "2"])
+def test_hybrid_large_output_numbers(flat, monkeypatch):
+    """OutputNumbers past the entries' 16-bit code (65535 and up, to the u32
+    maximum parseRuleResult accepts) come from the output arrays."""
+    monkeypatch.setenv("NFFACL_TUNE_FLAT", flat)
+    g = synth.gen_rules(synth.SPECS["c3"], synth.RULE_SEEDS["c3"])
+    lines = g.text.splitlines()
+    big = [65534, 65535, 65536, 70000, 4294967295]
+    for i in range(1, len(lines)):
+        if i % 3 == 0:
+            f = lines[i].split()
+            f[5] = str(big[i % len(big)])
+            lines[i] = " ".join(f)
+    text = "\n".join(lines) + "\n"
+    n = 1 << 13
+    check_hybrid(text, synth.gen_slots(synth.gen_rules(synth.SPECS["c3"], synth.RULE_SEEDS["c3"]), n, 71), n)
