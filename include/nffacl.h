@@ -272,11 +272,16 @@ NFFACL_API int nffacl_classify_host_ex(nffacl_engine *eng, const uint8_t *h_slot
 /* ---- burst aggregator (host ingest) ----------------
  *
  * Many threads (the reference's flow-function clones, each with a burst of
- * <= 32 packets) submit bursts; the library copies each packet's first
- * `stride` bytes into a shared pinned slot ring, ships a batch to the GPU when
- * `max_batch` packets are queued or the oldest queued burst has waited
- * `max_delay_us`, and wakes every submitter of that batch when its verdicts
- * are back.  Thread-safe: any number of concurrent submitters per batcher.
+ * <= 32 packets, or single packets from a SetSeparator-style scalar call)
+ * submit bursts; the library copies each packet's first `stride` bytes into a
+ * shared pinned slot ring and ships the open batch as soon as fewer than two
+ * batches are on the GPU — so batches grow while the GPU is busy, up to
+ * `max_batch` packets — and every submitter of that batch spins until its
+ * verdicts are back.  `max_delay_us` bounds how long a batch waits behind a
+ * full pipeline before it takes a further stream.  Thread-safe: any number of
+ * concurrent submitters per batcher.  Every ticket must be waited for (its
+ * batch buffer is reused only then); tickets not yet waited for may hold up
+ * to (nbuf - 1) * max_batch packets before submit blocks for a buffer.
  */
 typedef struct nffacl_batcher nffacl_batcher;
 
@@ -289,7 +294,7 @@ typedef struct nffacl_batcher_stats {
     uint64_t batches;  /* GPU launches */
     uint64_t packets;  /* packets classified */
     uint64_t bursts;   /* submit calls */
-    uint64_t timeouts; /* batches shipped by max_delay_us rather than full */
+    uint64_t timeouts; /* batches shipped before max_batch filled */
 } nffacl_batcher_stats;
 
 /* stride: slot bytes per packet (multiple of 16, >= 64; 80 keeps IPv4 with IHL

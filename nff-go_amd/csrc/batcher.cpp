@@ -1,12 +1,29 @@
 // batcher.cpp — nffacl_batcher: multi-producer burst aggregation onto the GPU
 // (see batcher.hpp).  One launcher thread seals and ships batches in ring
-// order; one completer thread waits on their events in launch order and wakes
-// the bursts' submitters.
+// order; one completer thread waits on their events in launch order and
+// publishes each batch's sequence number, on which the bursts' submitters spin.
+//
+// Launch policy (adaptive batching): a batch ships as soon as it holds a burst,
+// fewer than kEagerInflight batches are on the GPU and at least two buffers
+// stay free, so an idle GPU costs a burst one launch round trip, while a busy
+// one lets the open batch grow (up to max_batch) until a batch completes.
+// (Buffers held by tickets nobody has waited for yet count as busy: a thread
+// that submits many bursts before waiting gets full batches, as before.)
+// The reference's clones submit synchronously (segmentProcess waits for its
+// separator's answers, flow/flow.go:1487-1520), so the open batch collects
+// exactly the bursts of the clones whose previous batch came back — no timer
+// has to guess when the last clone has submitted.  max_delay_us only bounds
+// how long a batch may wait behind a full pipeline before it takes one more
+// stream.  Waiters spin without locks while the process has CPUs to spare
+// (spin_limit) and block on their batch's own condition variable otherwise.
 #include "batcher.hpp"
 
+#include <sched.h>
 #include <sys/prctl.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -23,6 +40,25 @@ namespace {
 // maintenance between batches.
 constexpr unsigned kHostFlags = hipHostMallocMapped | hipHostMallocCoherent;
 
+// Batches on the GPU before an open batch waits for one to complete.
+constexpr uint32_t kEagerInflight = 2;
+
+// CPUs this process may keep busy: its affinity set, capped by a cgroup v2
+// CPU quota (a GPU box's share of the host).
+uint32_t cpu_share() {
+    cpu_set_t set;
+    uint32_t n = std::thread::hardware_concurrency();
+    if (sched_getaffinity(0, sizeof set, &set) == 0) n = static_cast<uint32_t>(CPU_COUNT(&set));
+    if (FILE *f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+        char q[32] = {0};
+        unsigned long period = 0;
+        if (std::fscanf(f, "%31s %lu", q, &period) == 2 && std::strcmp(q, "max") != 0 && period > 0)
+            n = std::min<uint32_t>(n, static_cast<uint32_t>(std::max(1.0, std::atof(q) / double(period))));
+        std::fclose(f);
+    }
+    return std::max(1u, n);
+}
+
 void release_buffers(nffacl_batcher *b) {
     if (!b->bufs) return;
     for (uint32_t i = 0; i < b->nbuf; ++i) {
@@ -36,32 +72,40 @@ void release_buffers(nffacl_batcher *b) {
 
 // Under b->mu.  Seal the open buffer and move producers to the next one.
 void seal_open(nffacl_batcher *b) {
-    b->bufs[b->open_idx].state = BatchBuf::SEALED;
+    BatchBuf &x = b->bufs[b->open_idx];
+    x.state = BatchBuf::SEALED;
+    if (x.count < b->max_batch) ++b->timeouts;  // shipped before it filled
     b->open_idx = (b->open_idx + 1) % b->nbuf;
     b->cv_work.notify_one();
     b->cv_free.notify_all();  // producers parked on the old open_idx re-check
 }
 
-// Under b->mu: ship bufs[launch_idx] (SEALED).  Drops the lock while copying.
+// Under b->mu: ship bufs[launch_idx] (SEALED).  Drops the lock while launching.
 void launch_one(nffacl_batcher *b, std::unique_lock<std::mutex> &lk) {
     const uint32_t i = b->launch_idx;
     BatchBuf &x = b->bufs[i];
     const uint32_t n = x.count;
     b->launch_idx = (i + 1) % b->nbuf;
+    ++b->inflight_n;
     lk.unlock();
     while (x.written.load(std::memory_order_acquire) < n) std::this_thread::yield();  // copies in progress
     // zero-copy: the kernel reads the mapped slots and writes the mapped ports
     hipError_t e = hipSuccess;
-    const TablePtr t = acquire_table(b->eng);  // held while enqueued; the launch records its use
-    int st = launch_slots(b->eng, t.get(), x.d_slots, b->stride, n, x.d_port, nullptr, x.stream);
+    int st;
+    {
+        const TablePtr t = acquire_table(b->eng);  // held while enqueued; the launch records its use
+        st = launch_slots(b->eng, t.get(), x.d_slots, b->stride, n, x.d_port, nullptr, x.stream);
+    }
     if (st == NFFACL_OK) e = hipEventRecord(x.done, x.stream);
     lk.lock();
     if (e != hipSuccess || st != NFFACL_OK) {
         if (e != hipSuccess) set_last_error(std::string("batcher launch: ") + hipGetErrorString(e));
         b->error = st != NFFACL_OK ? st : NFFACL_ERR_HIP;
+        --b->inflight_n;
         x.state = BatchBuf::DONE;  // wake the waiters with the error
         x.done_seq.store(x.seq, std::memory_order_release);
-        b->cv_done.notify_all();
+        std::lock_guard<std::mutex> w(x.wmu);
+        x.wcv.notify_all();
         return;
     }
     x.state = BatchBuf::LAUNCHED;
@@ -82,21 +126,14 @@ void launcher_main(nffacl_batcher *b) {
             continue;
         }
         if (x.state == BatchBuf::OPEN && x.count > 0) {
-            // ship when the batch is old enough or its producers went quiet
-            const auto deadline = std::min(x.opened + b->max_delay, b->last_submit + b->idle);
-            const auto now = Clock::now();
-            if (b->stop || now >= deadline) {
-                if (!b->stop) ++b->timeouts;
-                seal_open(b);  // open_idx == launch_idx here
+            // open_idx == launch_idx here
+            const bool room = b->inflight_n < kEagerInflight && b->busy + 2 <= b->nbuf;
+            const bool late = Clock::now() >= x.opened + b->max_delay && b->busy + 2 <= b->nbuf;
+            if (b->stop || room || late) {
+                seal_open(b);
                 continue;
             }
-            if (deadline - now < std::chrono::microseconds(50)) {  // short: spin, no sleep
-                lk.unlock();
-                std::this_thread::yield();
-                lk.lock();
-            } else {
-                b->cv_work.wait_until(lk, deadline);
-            }
+            b->cv_work.wait_until(lk, x.opened + b->max_delay);  // a completion, or the deadline
             continue;
         }
         if (b->stop) break;
@@ -117,20 +154,28 @@ void completer_main(nffacl_batcher *b) {
         lk.unlock();
         hipError_t e;
         while ((e = hipEventQuery(b->bufs[i].done)) == hipErrorNotReady) std::this_thread::yield();  // poll: no interrupt wake-up latency
-        lk.lock();
-        b->inflight.pop_front();
+        BatchBuf &x = b->bufs[i];
         if (e != hipSuccess) {
+            lk.lock();
             set_last_error(std::string("batcher completion: ") + hipGetErrorString(e));
             b->error = NFFACL_ERR_HIP;
+            lk.unlock();
         }
-        BatchBuf &x = b->bufs[i];
+        x.done_seq.store(x.seq, std::memory_order_release);  // spinning waiters go now
+        {
+            std::lock_guard<std::mutex> w(x.wmu);  // blocked waiters
+            x.wcv.notify_all();
+        }
+        lk.lock();
+        b->inflight.pop_front();
+        --b->inflight_n;
         x.state = BatchBuf::DONE;
-        x.done_seq.store(x.seq, std::memory_order_release);
-        if (x.readers == 0) {
+        if (x.readers.load(std::memory_order_acquire) == 0) {
             x.state = BatchBuf::FREE;
+            --b->busy;
             b->cv_free.notify_all();
         }
-        b->cv_done.notify_all();
+        b->cv_work.notify_one();  // the pipeline has room: the open batch may ship
     }
 }
 
@@ -149,8 +194,9 @@ int nffacl_batcher_create(nffacl_engine *eng, uint32_t stride, uint32_t max_batc
     b->stride = stride;
     b->max_batch = max_batch;
     b->max_delay = std::chrono::microseconds(max_delay_us);
-    b->idle = std::chrono::microseconds(std::max<uint32_t>(2, max_delay_us / 8));
     b->nbuf = nbuf;
+    const uint32_t cpus = cpu_share();
+    b->spin_limit = cpus > 3 ? cpus - 3 : 1;  // the launcher, the completer and one spare
     b->bufs.reset(new (std::nothrow) BatchBuf[nbuf]);
     if (!b->bufs) {
         delete b;
@@ -191,9 +237,10 @@ int nffacl_batcher_submit(nffacl_batcher *b, const uint8_t *const *frames, const
         BatchBuf &cur = b->bufs[b->open_idx];
         if (cur.state == BatchBuf::FREE) {
             cur.state = BatchBuf::OPEN;
+            ++b->busy;
             cur.seq = b->next_seq++;
             cur.count = 0;
-            cur.readers = 0;
+            cur.readers.store(0, std::memory_order_relaxed);
             cur.written.store(0, std::memory_order_relaxed);
         } else if (cur.state != BatchBuf::OPEN) {
             b->cv_free.wait(lk);  // every buffer in flight: back-pressure
@@ -205,14 +252,13 @@ int nffacl_batcher_submit(nffacl_batcher *b, const uint8_t *const *frames, const
         }
         x = &cur;
         off = cur.count;
-        b->last_submit = Clock::now();
-        if (off == 0) cur.opened = b->last_submit;
+        if (off == 0) cur.opened = Clock::now();
         cur.count += n;
-        ++cur.readers;
+        cur.readers.fetch_add(1, std::memory_order_relaxed);
         ++b->bursts;
         *ticket = nffacl_ticket{cur.seq, b->open_idx, off, n, 0};
         if (cur.count == b->max_batch) seal_open(b);
-        else if (off == 0) b->cv_work.notify_one();  // start the max_delay clock
+        else if (off == 0) b->cv_work.notify_one();  // a batch to ship
         break;
     }
     lk.unlock();
@@ -231,21 +277,33 @@ int nffacl_batcher_wait(nffacl_batcher *b, const nffacl_ticket *t, uint32_t *por
     if (t->n == 0) return NFFACL_OK;
     if (t->buf >= b->nbuf) return NFFACL_ERR_INVALID_ARG;
     BatchBuf &x = b->bufs[t->buf];
-    // spin first (the reference's flow-function clones busy-poll their cores),
-    // then block
-    const auto spin_until = Clock::now() + std::chrono::microseconds(500);
-    while (x.done_seq.load(std::memory_order_acquire) != t->seq && Clock::now() < spin_until)
-        std::this_thread::yield();
-    std::unique_lock<std::mutex> lk(b->mu);
-    if (x.seq != t->seq || x.state == BatchBuf::FREE) return NFFACL_ERR_INVALID_ARG;
-    b->cv_done.wait(lk, [&] { return x.state == BatchBuf::DONE; });
+    auto done = [&] { return x.done_seq.load(std::memory_order_acquire) == t->seq; };
+    // spin first, without locks (the reference's flow-function clones
+    // busy-poll their cores) while the host has CPUs to spare; then block
+    if (!done()) {
+        if (b->spinners.fetch_add(1, std::memory_order_acq_rel) < b->spin_limit) {
+            const auto spin_until = Clock::now() + std::chrono::microseconds(200);
+            while (!done() && Clock::now() < spin_until) std::this_thread::yield();
+        }
+        b->spinners.fetch_sub(1, std::memory_order_acq_rel);
+    }
+    if (!done()) {
+        {
+            std::lock_guard<std::mutex> g(b->mu);
+            if (x.seq != t->seq || x.state == BatchBuf::FREE) return NFFACL_ERR_INVALID_ARG;  // stale ticket
+        }
+        std::unique_lock<std::mutex> w(x.wmu);
+        x.wcv.wait(w, done);
+    }
     const int st = b->error;
-    lk.unlock();
     if (ports && st == NFFACL_OK) std::memcpy(ports, x.h_port + t->off, size_t(t->n) * 4);
-    lk.lock();
-    if (--x.readers == 0) {
-        x.state = BatchBuf::FREE;
-        b->cv_free.notify_all();
+    if (x.readers.fetch_sub(1, std::memory_order_acq_rel) == 1) {  // the batch's last burst
+        std::lock_guard<std::mutex> g(b->mu);
+        if (x.state == BatchBuf::DONE) {  // else the completer frees it once it marks it DONE
+            x.state = BatchBuf::FREE;
+            --b->busy;
+            b->cv_free.notify_all();
+        }
     }
     return st;
 }

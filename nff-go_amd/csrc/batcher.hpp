@@ -4,9 +4,10 @@
 // packets at a time (segmentProcess, flow/flow.go:1487-1520, calling the
 // VectorSeparateFunction of flow.go:131).  A GPU launch per burst is latency
 // bound, so the batcher lets every clone (thread) submit its burst into a
-// shared pinned slot ring; one launcher thread ships a batch to the GPU when it
-// is full or its oldest burst has waited `max_delay_us`, and each clone blocks
-// only until its own batch's verdicts are back.
+// shared pinned slot ring; one launcher thread ships the open batch as soon as
+// fewer than two batches are on the GPU (adaptive batching: it grows while the
+// GPU is busy, up to max_batch; batcher.cpp), and each clone spins only until
+// its own batch's verdicts are back.
 //
 // Buffers: `nbuf` batch buffers, each = mapped pinned slots + ports on the host
 // (the kernel reads the slots and writes the verdicts over PCIe directly:
@@ -37,9 +38,11 @@ struct BatchBuf {
     State state = FREE;
     uint64_t seq = 0;       // batch sequence number while not FREE
     uint32_t count = 0;     // packets reserved
-    uint32_t readers = 0;   // bursts that have not collected their verdicts yet
+    std::atomic<uint32_t> readers{0};  // bursts that have not collected their verdicts yet
     std::atomic<uint32_t> written{0};  // packets whose bytes are in h_slots
     std::atomic<uint64_t> done_seq{0}; // == seq once the verdicts are in h_port
+    std::mutex wmu;                    // waiters that stopped spinning block on wcv
+    std::condition_variable wcv;
     std::chrono::steady_clock::time_point opened;
     uint8_t *h_slots = nullptr;   // mapped pinned host memory
     uint32_t *h_port = nullptr;
@@ -55,16 +58,13 @@ struct nffacl_batcher {
     nffacl_engine *eng = nullptr;
     uint32_t stride = 64;
     uint32_t max_batch = 0;
-    std::chrono::microseconds max_delay{100};  // since the batch's first burst
-    std::chrono::microseconds idle{10};        // since the batch's last burst
-    std::chrono::steady_clock::time_point last_submit;
+    std::chrono::microseconds max_delay{100};  // longest wait behind a full pipeline
     uint32_t nbuf = 0;
     std::unique_ptr<nffacl::BatchBuf[]> bufs;
 
     std::mutex mu;
     std::condition_variable cv_work;  // launcher: a batch sealed / opened
     std::condition_variable cv_free;  // producers: a buffer became FREE
-    std::condition_variable cv_done;  // waiters: a batch finished
     uint32_t open_idx = 0;            // buffer producers append to
     uint32_t launch_idx = 0;          // next buffer the launcher ships
     uint64_t next_seq = 1;
@@ -73,9 +73,16 @@ struct nffacl_batcher {
     int error = NFFACL_OK;            // sticky launch error
 
     std::deque<uint32_t> inflight;    // launched buffers, FIFO
+    uint32_t inflight_n = 0;          // batches launched (or launching) and not completed
+    uint32_t busy = 0;                // buffers not FREE
+    // Waiters spin (no syscalls) only while fewer than spin_limit of them do:
+    // past the host's CPU share, spinning submitters would starve the
+    // launcher and completer threads (batcher.cpp)
+    std::atomic<uint32_t> spinners{0};
+    uint32_t spin_limit = 1;
     std::condition_variable cv_inflight;
     std::thread launcher, completer;
 
     // stats
-    uint64_t batches = 0, packets = 0, bursts = 0, timeouts = 0;
+    uint64_t batches = 0, packets = 0, bursts = 0, timeouts = 0;  // timeouts: shipped before full
 };

@@ -10,13 +10,18 @@
 //   nffgo::packet::GetL3ACLFromJSON              packet/acl.go:121-134
 //   nffgo::packet::L3Rules                       packet/acl.go:451-455
 //   nffgo::packet::Packet::L3ACLPermit / Port    packet/acl.go:495-506
+//   nffgo::flow::SeparateFunction / SplitFunction flow/flow.go:128, 134
+//   nffgo::flow::ACLSeparator / ACLSplitter      the scalar separator of
+//                                                examples/firewall/firewall.go:54-57
 //   nffgo::flow::VectorSeparateFunction          flow/flow.go:131
 //   nffgo::flow::ACLVectorSeparator              the vector separator body of
 //                                                testSingleWorkingFF.go:538-546
 //   nffgo::flow::Aggregator                      burst aggregation for GPU-size batches
 //
 // Every verdict is computed by the HIP kernels of libnffacl; there is no CPU
-// path.  Per-packet calls are one-packet GPU batches (latency-bound); batch
+// path.  The scalar separator ACLSeparator sends each packet through a
+// shared batcher, so the calls of concurrent clones ride in common GPU
+// batches; one call alone costs a GPU round trip.  Batch
 // through ACLVectorSeparator / Aggregator for throughput.
 #pragma once
 
@@ -188,6 +193,9 @@ inline void L3ACLPortBatch(const Packet *const *pkts, size_t n, uint32_t *ports,
                                  nffacl_last_error());
 }
 
+// acl.go:504 for one packet: a synchronous one-packet GPU call (latency
+// bound).  Clones classifying concurrently should share a
+// flow::SharedBatcher (flow::ACLSeparator) so their packets coalesce.
 inline uint32_t Packet::L3ACLPort(const L3Rules &rules) const {
     const Packet *p = this;
     uint32_t port = 0;
@@ -297,6 +305,10 @@ namespace flow {
 
 constexpr int vBurstSize = 32;  // flow/flow.go:465-469
 
+// flow.go:128 / 134: the per-packet user functions SetSeparator / SetSplitter call.
+using SeparateFunction = std::function<bool(packet::Packet *pkt)>;
+using SplitFunction = std::function<uint32_t(packet::Packet *pkt)>;
+
 // flow.go:131: VectorSeparateFunction(pkts, mask, answers, ctx)
 using VectorSeparateFunction =
     std::function<void(packet::Packet *const *pkts, const bool *mask, bool *answers)>;
@@ -373,6 +385,27 @@ private:
     std::shared_ptr<const packet::L3Rules> rules_;  // keeps the engine alive
     nffacl_batcher *b_ = nullptr;
 };
+
+// firewall.go:54-57's l3Separator (pkt.L3ACLPermit(rules)) for SetSeparator:
+// each call is a one-packet burst on the shared batcher, so the calls of all
+// clones running the separator coalesce into common GPU batches.
+inline SeparateFunction ACLSeparator(std::shared_ptr<SharedBatcher> batcher) {
+    return [batcher](packet::Packet *pkt) {
+        uint32_t port = 0;
+        const packet::Packet *p = pkt;
+        batcher->Classify(&p, 1, &port);
+        return port > 0;
+    };
+}
+// SetSplitter's per-packet L3ACLPort (examples/forwarding/forwarding.go:49-67).
+inline SplitFunction ACLSplitter(std::shared_ptr<SharedBatcher> batcher) {
+    return [batcher](packet::Packet *pkt) {
+        uint32_t port = 0;
+        const packet::Packet *p = pkt;
+        batcher->Classify(&p, 1, &port);
+        return port;
+    };
+}
 
 // The vector separator of every clone, backed by one shared batcher.
 inline VectorSeparateFunction ACLVectorSeparator(std::shared_ptr<SharedBatcher> batcher) {

@@ -593,6 +593,46 @@ static void TestVectorSeparatorSharedBatcher(T &t) {
                                           (unsigned long long)st.batches, (unsigned long long)st.bursts);
 }
 
+// SetSeparator's scalar call shape (firewall.go:54-57, flow.go:128) through the
+// shared batcher: clones classifying one packet per call coalesce into common
+// GPU batches; every answer must be the single-packet verdict.
+static void TestScalarSeparatorSharedBatcher(T &t) {
+    const char *dir = std::getenv("NFFACL_GOLDEN");
+    const std::string g = dir ? dir : "tests/golden";
+    auto split = packet::GetL3ACLFromTextTable(g + "/rules/test-split.conf");
+    if (split.second) { t.Errorf("cannot load rules"); return; }
+    std::vector<TestPacket> tp;
+    for (int i = 0; i < 3; ++i) {
+        TestPacket p{ipv4Packet(types::UDPNumber, types::UDPLen, true)};
+        const uint16_t dport = i == 0 ? 111 : i == 1 ? 222 : 333;
+        p.bytes[36] = uint8_t(dport >> 8);
+        p.bytes[37] = uint8_t(dport);
+        tp.push_back(p);
+    }
+    std::vector<packet::Packet> pk;
+    for (auto &p : tp) pk.push_back(p.pkt());
+    auto batcher = std::make_shared<flow::SharedBatcher>(split.first, 4096, 50, 4);
+    auto sep = flow::ACLSeparator(batcher);
+    auto spl = flow::ACLSplitter(batcher);
+    constexpr int kClones = 16, kCalls = 400;
+    std::atomic<int> bad{0};
+    std::vector<std::thread> clones;
+    for (int c = 0; c < kClones; ++c)
+        clones.emplace_back([&, c] {
+            for (int k = 0; k < kCalls; ++k) {
+                const int i = (k + c) % 3;
+                if (spl(&pk[i]) != uint32_t(i + 1)) ++bad;  // test-split.conf: 111 -> 1, 222 -> 2, 333 -> 3
+                if (!sep(&pk[i])) ++bad;
+            }
+        });
+    for (auto &th : clones) th.join();
+    const auto st = batcher->Stats();
+    if (bad) t.Errorf("%d wrong answers", bad.load());
+    if (st.bursts != uint64_t(kClones) * kCalls * 2) t.Errorf("bursts %llu", (unsigned long long)st.bursts);
+    if (st.batches >= st.bursts) t.Errorf("no aggregation: %llu batches for %llu calls",
+                                          (unsigned long long)st.batches, (unsigned long long)st.bursts);
+}
+
 int main(int argc, char **argv) {
     const std::string which = argc > 1 ? argv[1] : "parse";
     if (which == "parse" || which == "all") {
@@ -614,6 +654,7 @@ int main(int argc, char **argv) {
         run("TestInternal_l2ACL_packetIPv4", TestInternal_l2ACL_packetIPv4);
         run("TestInternal_l2ACL_packetARP", TestInternal_l2ACL_packetARP);
         run("TestVectorSeparatorSharedBatcher", TestVectorSeparatorSharedBatcher);
+        run("TestScalarSeparatorSharedBatcher", TestScalarSeparatorSharedBatcher);
     }
     std::printf(g_failed ? "FAIL\n" : "ok\n");
     return g_failed ? 1 : 0;
