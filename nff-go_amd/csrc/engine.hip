@@ -710,6 +710,10 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
     const uint32_t *__restrict__ E4 = a.tab + a.f4.off_ent_base;
     const uint32_t *__restrict__ E6 = a.tab + a.f6.off_ent_base;
     for (uint32_t win = 0; win < T; win += 64 * R) {
+        // (every round runs, empty or not: straight-line rounds let the
+        // compiler interleave their loads; skipping the empty rounds of a
+        // partial window behind wave-uniform branches measured 4 % slower on
+        // C5, profiles/r2_exact/skip/)
 #pragma unroll
         for (int j = 0; j < R; ++j) W.mark[64 * j + lane] = 0u;
         wave_lds_sync();
@@ -864,8 +868,9 @@ k_indexed_slots(const uint8_t *__restrict__ slots, uint32_t stride, uint64_t n, 
     const uint32_t wpb = blockDim.x >> 6;
     const uint64_t wave0 = uint64_t(blockIdx.x) * wpb + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t step = uint64_t(gridDim.x) * wpb * 64;
-    constexpr bool RS = MODE == 4;            // lane-contiguous loads + permlane row swaps
-    constexpr bool COAL = MODE != 0 && !RS;   // lane-contiguous loads + quad DPP transpose
+    constexpr bool RS = MODE == 4 || MODE == 5;  // lane-contiguous loads + permlane row swaps
+    constexpr bool RSPF = MODE == 5;             // RS + the next batch's loads in flight (16 VGPRs)
+    constexpr bool COAL = MODE != 0 && !RS;      // lane-contiguous loads + quad DPP transpose
     constexpr bool NT = MODE >= 2;
     constexpr bool PF = MODE == 3;  // coalesced + next-batch register prefetch
     const uint32_t mine = COAL ? coal_packet(lane) : lane;  // packet of this lane within the batch
@@ -874,6 +879,7 @@ k_indexed_slots(const uint8_t *__restrict__ slots, uint32_t stride, uint64_t n, 
     u32x4 nv[4];
     if (!COAL && !RS && base < n) load16(slots + (base + lane < n ? base + lane : 0) * stride, d);
     if (PF && base + 64 <= n) load_coal<NT>(slots + base * 64, lane, nv);
+    if (RSPF && base + 64 <= n) load_rowswap<NT>(slots + base * 64, lane, nv);
     for (; base < n; base += step) {
         const uint64_t idx = base + mine;
         const bool live = idx < n;
@@ -882,7 +888,14 @@ k_indexed_slots(const uint8_t *__restrict__ slots, uint32_t stride, uint64_t n, 
         if (RS) {
             if (base + 64 <= n) {
                 u32x4 cv[4];
-                load_rowswap<NT>(slots + base * 64, lane, cv);
+                if (RSPF) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) cv[j] = nv[j];
+                    const uint64_t nb = base + step;
+                    if (nb + 64 <= n) load_rowswap<NT>(slots + nb * 64, lane, nv);
+                } else {
+                    load_rowswap<NT>(slots + base * 64, lane, cv);
+                }
                 rowswap_batch(cv, cur);
             } else {
                 load16(pkt, cur);
@@ -1012,7 +1025,7 @@ bool Tune::from_env(Tune &t, std::string &err) {
     t = Tune{};
     long v = 0;
     bool set = false;
-    if (!env_knob("NFFACL_TUNE_COAL", 0, 4, v, set, err)) return false;
+    if (!env_knob("NFFACL_TUNE_COAL", 0, 5, v, set, err)) return false;
     if (set) t.coal = static_cast<int>(v);
     if (!env_knob("NFFACL_TUNE_BLOCK", 64, 1024, v, set, err)) return false;
     if (set && v % 64 != 0) {
@@ -1190,6 +1203,8 @@ template <int NS, int TM>
 static hipError_t allow_lds_modes() {
     hipError_t e = allow_lds(dev::k_indexed_slots<NS, TM, 0>);
     if (e == hipSuccess) e = allow_lds(dev::k_indexed_slots<NS, TM, 4>);
+    if (TM == dev::kTabFlatLds || TM == dev::kTabFlatLds4)
+        if (e == hipSuccess) e = allow_lds(dev::k_indexed_slots<NS, TM, 5>);
     if (TM == dev::kTabLds) {
         if (e == hipSuccess) e = allow_lds(dev::k_indexed_slots<NS, dev::kTabLds, 1>);
         if (e == hipSuccess) e = allow_lds(dev::k_indexed_slots<NS, dev::kTabLds, 2>);
@@ -1257,7 +1272,14 @@ static void launch_slots_tm(int mode, const IndexedLaunch &L, uint32_t grid, hip
                             uint32_t *d_port, uint64_t *d_permit) {
     const dim3 g(grid), b(L.block);
     const size_t lds = TM == dev::kTabGlobal ? 0 : L.lds_bytes;
-    if constexpr (TM != dev::kTabLds) {  // built with load modes 0 and 4 only
+    if constexpr (TM == dev::kTabFlatLds || TM == dev::kTabFlatLds4) {  // load modes 0, 4, 5
+        if (mode == 0)
+            hipLaunchKernelGGL((dev::k_indexed_slots<NS, TM, 0>), g, b, lds, stream, d_slots, stride, n, a, d_port, d_permit);
+        else if (mode == 5)
+            hipLaunchKernelGGL((dev::k_indexed_slots<NS, TM, 5>), g, b, lds, stream, d_slots, stride, n, a, d_port, d_permit);
+        else
+            hipLaunchKernelGGL((dev::k_indexed_slots<NS, TM, 4>), g, b, lds, stream, d_slots, stride, n, a, d_port, d_permit);
+    } else if constexpr (TM != dev::kTabLds) {  // built with load modes 0 and 4 only
         if (mode == 0)
             hipLaunchKernelGGL((dev::k_indexed_slots<NS, TM, 0>), g, b, lds, stream, d_slots, stride, n, a, d_port, d_permit);
         else

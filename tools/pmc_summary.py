@@ -10,7 +10,7 @@ from pathlib import Path
 d = Path(sys.argv[1])
 key = sys.argv[2] if len(sys.argv) > 2 and not sys.argv[2].startswith("--") else "k_indexed_slots"
 out = {}
-for sub in ("fetch", "write", "sq", "sq2", "tcc"):
+for sub in ("fetch", "write", "sq", "sq2", "tcc", "ta"):
     f = d / sub / "run_counter_collection.csv"
     if not f.exists():
         continue
