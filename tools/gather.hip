@@ -61,6 +61,38 @@ __global__ void __launch_bounds__(1024) k_gather(const uint32_t *__restrict__ ta
     if (acc == 0x12345678u) out[wave] = acc;
 }
 
+// 24-byte entries at random entry numbers (the flat walk's candidate loads):
+// PAIR = 0: each lane one entry, words 0..2 and 3..5 (dwordx4 + dwordx2);
+// PAIR = 1: two lanes per entry, each one 12-byte half (one dwordx3), so one
+// instruction covers 32 entries.  Timed per 64 entries.
+typedef uint32_t u32x3 __attribute__((ext_vector_type(3), aligned(4)));
+template <int PAIR>
+__global__ void __launch_bounds__(1024) k_ent24(const uint32_t *__restrict__ tab, uint32_t ents, uint32_t *out) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    uint32_t acc = 0, seed = wave * 7919u;
+    for (int i = 0; i < ITERS; i += 4) {
+        uint32_t v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (PAIR) {
+                // instruction j covers entries of 32 lane pairs
+                const uint32_t e = mix(seed + (i + j) * 131u + (lane >> 1) * 977u) % ents;
+                const u32x3 q = *reinterpret_cast<const u32x3 *>(tab + e * 6u + 3u * (lane & 1u));
+                v[j] = q.x ^ q.y ^ q.z;
+            } else {
+                const uint32_t e = mix(seed + (i + j) * 131u + lane * 977u) % ents;
+                const u32x3 a = *reinterpret_cast<const u32x3 *>(tab + e * 6u);
+                const u32x3 b = *reinterpret_cast<const u32x3 *>(tab + e * 6u + 3u);
+                v[j] = a.x ^ a.y ^ a.z ^ b.x ^ b.y ^ b.z;
+            }
+        }
+        acc += v[0] ^ v[1] ^ v[2] ^ v[3];
+        seed ^= acc & 1u;
+    }
+    if (acc == 0x12345678u) out[wave] = acc;
+}
+
 // LDS: 64 KiB table, each lane a random dword (K = 64) or 64/K lanes per 128 B.
 __global__ void __launch_bounds__(1024) k_lds(uint32_t k, uint32_t *out) {
     extern __shared__ uint32_t lds[];
@@ -120,6 +152,16 @@ int main() {
                             first ? "" : ",\n", bytes, 4 * w, k, ms, ns);
                 first = false;
             }
+    for (size_t bytes : {size_t(2) << 20, size_t(5) << 20, size_t(16) << 20})
+        for (int pair : {0, 1}) {
+            const uint32_t ents = uint32_t(bytes / 24);
+            double ms = pair ? timed([&] { hipLaunchKernelGGL(k_ent24<1>, blocks, threads, 0, 0, tab, ents, out); return 0; })
+                             : timed([&] { hipLaunchKernelGGL(k_ent24<0>, blocks, threads, 0, 0, tab, ents, out); return 0; });
+            // entries loaded: PAIR 0: 64 per instruction step, PAIR 1: 32
+            const double per64 = ms * 1e6 * cus / (double(waves) * ITERS * (pair ? 0.5 : 1.0));
+            std::printf(",\n {\"entries24\": true, \"table_bytes\": %zu, \"pair\": %d, \"ms\": %.4f, \"ns_per_64_entries_per_cu\": %.3f}",
+                        bytes, pair, ms, per64);
+        }
     CK(hipFuncSetAttribute(reinterpret_cast<const void *>(k_lds), hipFuncAttributeMaxDynamicSharedMemorySize, 65536));
     for (uint32_t k : {1u, 8u, 64u}) {
         double ms = timed([&] { hipLaunchKernelGGL(k_lds, blocks, threads, 65536, 0, k, out); return 0; });
