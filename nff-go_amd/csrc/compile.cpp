@@ -914,6 +914,7 @@ void build_hybrid(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vec
     if (flat && lds_dirs && !tuned && expect > kHybFlat4Candidates) {
         budget = kHybFlat4DirBytes;
         size_and_fill(all, weight, budget, want16);
+        out.flat_uncond = 1;
     }
     // 4 rounds of candidate loads in flight whenever their scratch fits beside
     // the directories (indexed_launch checks; exact entries, C3: 0.507 vs

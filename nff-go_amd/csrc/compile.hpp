@@ -55,6 +55,9 @@ struct CompiledTable {
     uint32_t lds_dwords = 0;
     // HYBRID flat-LDS: rounds of candidate loads in flight (2 or 4)
     uint32_t flat_rounds = 2;
+    // flat-LDS walk with many expected candidates per packet: its entry
+    // loads are issued without a per-lane branch (engine.hip kTabFlatLds4U)
+    uint32_t flat_uncond = 0;
     // HYBRID global-directory form with generalized slots (dims[k].kind2 etc.;
     // idx*.used_slots = slots in use, all non-empty)
     bool slots_g = false;

@@ -392,6 +392,9 @@ enum TableMode : int {
                      // over directories staged in LDS, one 1024-thread
                      // workgroup per CU, candidate scratch after the image
     kTabFlatLds4 = 7,  // the same, 4 rounds in flight (larger scratch)
+    kTabFlatLds4U = 8, // the same, entry loads of every non-empty round issued
+                       // without a per-lane branch (tables with many candidates
+                       // per packet: CompiledTable::flat_uncond)
 };
 
 extern __shared__ __attribute__((aligned(16))) uint32_t lds_tab[];
@@ -665,7 +668,7 @@ __device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
     return x;
 }
 
-template <int NS, int R, bool LDS_DIRS>
+template <int NS, int R, bool LDS_DIRS, bool UNCOND = false>
 __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fields &f, FlatScratch<R> &W,
                                                   uint32_t lane) {
     const bool v6 = f.is6;
@@ -743,10 +746,14 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
             owner[j] = ((m - 1u) >> 8) / NS;
             const uint32_t dp = W.delta[(m - 1u) & 0xFFu];
             six[j] = (dp & 1u) != 0u;
-            const uint32_t ent = k + static_cast<uint32_t>(static_cast<int32_t>(dp) >> 1);
-            const uint32_t *e = six[j] ? E6 + ent * kHybEnt6Dwords : E4 + ent * kHybEnt4Dwords;
+            // UNCOND: lanes past the wave's candidates load entry 0 of the
+            // IPv4 list (untested) instead of branching around the load —
+            // C5 0.750 vs 0.782 ms, but C3, whose last rounds are mostly
+            // empty, 0.59 vs 0.54 ms (profiles/r2_exact/uncond/)
+            const uint32_t ent = !UNCOND || valid[j] ? k + static_cast<uint32_t>(static_cast<int32_t>(dp) >> 1) : 0u;
+            const uint32_t *e = six[j] && (!UNCOND || valid[j]) ? E6 + ent * kHybEnt6Dwords : E4 + ent * kHybEnt4Dwords;
             A[j] = B[j] = C[j] = D[j] = u32x3{0, 0, 0};
-            if (valid[j]) {
+            if (UNCOND || valid[j]) {
                 A[j] = ld3(e);
                 B[j] = ld3(e + 3);
             }
@@ -838,11 +845,12 @@ __device__ __forceinline__ uint32_t classify_any(const IndexedArgs &a, const Fie
         const uint32_t lane = lane_id();
         return classify_flat<NS, R, false>(a, f, W[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)], lane);
     }
-    if (TM == kTabFlatLds || TM == kTabFlatLds4) {  // scratch after the staged directories (stage_dwords: multiple of 4)
-        constexpr int R = TM == kTabFlatLds4 ? 4 : 2;
+    if (TM == kTabFlatLds || TM == kTabFlatLds4 || TM == kTabFlatLds4U) {  // scratch after the staged directories (stage_dwords: multiple of 4)
+        constexpr int R = TM == kTabFlatLds ? 2 : 4;
         FlatScratch<R> *W = reinterpret_cast<FlatScratch<R> *>(lds_tab + a.stage_dwords);
         const uint32_t lane = lane_id();
-        return classify_flat<NS, R, true>(a, f, W[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)], lane);
+        return classify_flat<NS, R, true, TM == kTabFlatLds4U>(a, f, W[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)],
+                                                               lane);
     }
     if constexpr (NS <= 4) {  // per-lane walks: the positional four slots
         if (TM == kTabLds) return classify_indexed<NS, 1>(LdsTab{}, a, f);
@@ -863,7 +871,7 @@ template <int NS, int TM, int MODE>
 __global__ void __launch_bounds__(1024)
 k_indexed_slots(const uint8_t *__restrict__ slots, uint32_t stride, uint64_t n, IndexedArgs a,
                 uint32_t *__restrict__ port_out, uint64_t *__restrict__ permit_out) {
-    if (TM == kTabLds || TM == kTabSplit || TM == kTabFlatLds || TM == kTabFlatLds4) stage_table(a);
+    if (TM == kTabLds || TM == kTabSplit || TM == kTabFlatLds || TM == kTabFlatLds4 || TM == kTabFlatLds4U) stage_table(a);
     const uint32_t lane = lane_id();
     const uint32_t wpb = blockDim.x >> 6;
     const uint64_t wave0 = uint64_t(blockIdx.x) * wpb + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -943,7 +951,7 @@ template <int NS, int TM>
 __global__ void __launch_bounds__(1024)
 k_indexed_frames(const uint8_t *__restrict__ frames, const uint64_t *__restrict__ desc, uint64_t n,
                  IndexedArgs a, uint32_t *__restrict__ port_out, uint64_t *__restrict__ permit_out) {
-    if (TM == kTabLds || TM == kTabSplit || TM == kTabFlatLds || TM == kTabFlatLds4) stage_table(a);
+    if (TM == kTabLds || TM == kTabSplit || TM == kTabFlatLds || TM == kTabFlatLds4 || TM == kTabFlatLds4U) stage_table(a);
     const uint32_t lane = lane_id();
     const uint32_t wpb = blockDim.x >> 6;
     const uint64_t S = uint64_t(gridDim.x) * wpb * 64;  // grid stride in packets
@@ -1160,7 +1168,7 @@ static IndexedLaunch indexed_launch(const nffacl_engine *eng, const DevTable *t)
         const size_t lds4 = image + sizeof(dev::FlatScratch<4>) * (L.block / 64);
         const int rounds = tu.rounds ? tu.rounds : static_cast<int>(t->meta.flat_rounds);
         const bool r4 = rounds == 4 && lds4 <= kLdsBytes;
-        L.tm = r4 ? dev::kTabFlatLds4 : dev::kTabFlatLds;
+        L.tm = r4 ? (t->meta.flat_uncond ? dev::kTabFlatLds4U : dev::kTabFlatLds4) : dev::kTabFlatLds;
         L.lds_bytes = r4 ? lds4 : image + sizeof(dev::FlatScratch<2>) * (L.block / 64);
         return L;
     }
@@ -1203,7 +1211,7 @@ template <int NS, int TM>
 static hipError_t allow_lds_modes() {
     hipError_t e = allow_lds(dev::k_indexed_slots<NS, TM, 0>);
     if (e == hipSuccess) e = allow_lds(dev::k_indexed_slots<NS, TM, 4>);
-    if (TM == dev::kTabFlatLds || TM == dev::kTabFlatLds4)
+    if (TM == dev::kTabFlatLds || TM == dev::kTabFlatLds4 || TM == dev::kTabFlatLds4U)
         if (e == hipSuccess) e = allow_lds(dev::k_indexed_slots<NS, TM, 5>);
     if (TM == dev::kTabLds) {
         if (e == hipSuccess) e = allow_lds(dev::k_indexed_slots<NS, dev::kTabLds, 1>);
@@ -1225,6 +1233,7 @@ static void dispatch_indexed(int ns, int tm, F &&f) {
         case dev::kTabFlat4: f(nsc, std::integral_constant<int, dev::kTabFlat4>{}); break;
         case dev::kTabFlatLds: f(nsc, std::integral_constant<int, dev::kTabFlatLds>{}); break;
         case dev::kTabFlatLds4: f(nsc, std::integral_constant<int, dev::kTabFlatLds4>{}); break;
+        case dev::kTabFlatLds4U: f(nsc, std::integral_constant<int, dev::kTabFlatLds4U>{}); break;
         default: f(nsc, std::integral_constant<int, dev::kTabGlobal>{}); break;
         }
     };
@@ -1234,6 +1243,7 @@ static void dispatch_indexed(int ns, int tm, F &&f) {
         case dev::kTabFlat: f(nsc, std::integral_constant<int, dev::kTabFlat>{}); break;
         case dev::kTabFlatLds: f(nsc, std::integral_constant<int, dev::kTabFlatLds>{}); break;
         case dev::kTabFlatLds4: f(nsc, std::integral_constant<int, dev::kTabFlatLds4>{}); break;
+        case dev::kTabFlatLds4U: f(nsc, std::integral_constant<int, dev::kTabFlatLds4U>{}); break;
         default: f(nsc, std::integral_constant<int, dev::kTabFlat4>{}); break;
         }
     };
@@ -1251,8 +1261,10 @@ int prepare_kernels() {
     static hipError_t err = hipSuccess;
     std::call_once(once, [] {
         for (int ns = 2; ns <= int(kMaxSlots); ++ns)
-            for (int tm : {int(dev::kTabLds), int(dev::kTabSplit), int(dev::kTabFlatLds), int(dev::kTabFlatLds4)}) {
-                if (ns > 4 && tm != dev::kTabFlatLds && tm != dev::kTabFlatLds4) continue;  // flat walks only
+            for (int tm : {int(dev::kTabLds), int(dev::kTabSplit), int(dev::kTabFlatLds), int(dev::kTabFlatLds4),
+                           int(dev::kTabFlatLds4U)}) {
+                if (ns > 4 && tm != dev::kTabFlatLds && tm != dev::kTabFlatLds4 && tm != dev::kTabFlatLds4U)
+                    continue;  // flat walks only
                 dispatch_indexed(ns, tm, [&](auto nsc, auto tmc) {
                     const hipError_t e = allow_lds_modes<decltype(nsc)::value, decltype(tmc)::value>();
                     if (e != hipSuccess) err = e;
@@ -1272,7 +1284,7 @@ static void launch_slots_tm(int mode, const IndexedLaunch &L, uint32_t grid, hip
                             uint32_t *d_port, uint64_t *d_permit) {
     const dim3 g(grid), b(L.block);
     const size_t lds = TM == dev::kTabGlobal ? 0 : L.lds_bytes;
-    if constexpr (TM == dev::kTabFlatLds || TM == dev::kTabFlatLds4) {  // load modes 0, 4, 5
+    if constexpr (TM == dev::kTabFlatLds || TM == dev::kTabFlatLds4 || TM == dev::kTabFlatLds4U) {  // load modes 0, 4, 5
         if (mode == 0)
             hipLaunchKernelGGL((dev::k_indexed_slots<NS, TM, 0>), g, b, lds, stream, d_slots, stride, n, a, d_port, d_permit);
         else if (mode == 5)
