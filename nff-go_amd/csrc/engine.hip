@@ -794,13 +794,12 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
                 }
             }
         }
-        // rule index << 32 | output code: the minimum carries the winner's
-        // output.  Every lane posts (no branch): a lane without a passing
-        // candidate posts ~0 to its own packet's word, which it cannot lower.
+        // (posting from every lane, ~0 to its own word when nothing passed,
+        // instead of the branch: C5 0.757 vs 0.750 ms, profiles/r2_exact/uncond/am_*)
 #pragma unroll
-        for (int j = 0; j < R; ++j)
-            atomicMin(reinterpret_cast<unsigned long long *>(&W.best[pass[j] ? owner[j] : lane]),
-                      pass[j] ? static_cast<unsigned long long>(idx[j]) << 32 | (B[j].z >> kHybOutShift) : ~0ull);
+        for (int j = 0; j < R; ++j)  // rule index << 32 | output code: the minimum carries the winner's output
+            if (pass[j]) atomicMin(reinterpret_cast<unsigned long long *>(&W.best[owner[j]]),
+                                   static_cast<unsigned long long>(idx[j]) << 32 | (B[j].z >> kHybOutShift));
         wave_lds_sync();
     }
     uint64_t best = W.best[lane];  // ~0 or rule index << 32 | output code
