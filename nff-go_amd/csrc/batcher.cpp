@@ -14,12 +14,15 @@
 // exactly the bursts of the clones whose previous batch came back — no timer
 // has to guess when the last clone has submitted.  max_delay_us only bounds
 // how long a batch may wait behind a full pipeline before it takes one more
-// stream.  Waiters spin without locks while the process has CPUs to spare
-// (spin_limit) and block on their batch's own condition variable otherwise.
+// stream.  Waiters sleep on their batch's generation word (futex: one
+// wake-up releases every waiter of the batch together, no mutex to re-take);
+// NFFACL_TUNE_BATCH_SPIN lets up to that many spin first (experiments).
 #include "batcher.hpp"
 
-#include <sched.h>
+#include <linux/futex.h>
 #include <sys/prctl.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <cstdio>
@@ -28,6 +31,7 @@
 #include <new>
 #include <string>
 
+#include "compile.hpp"
 #include "devutil.hpp"
 
 using namespace nffacl;
@@ -43,20 +47,18 @@ constexpr unsigned kHostFlags = hipHostMallocMapped | hipHostMallocCoherent;
 // Batches on the GPU before an open batch waits for one to complete.
 constexpr uint32_t kEagerInflight = 2;
 
-// CPUs this process may keep busy: its affinity set, capped by a cgroup v2
-// CPU quota (a GPU box's share of the host).
-uint32_t cpu_share() {
-    cpu_set_t set;
-    uint32_t n = std::thread::hardware_concurrency();
-    if (sched_getaffinity(0, sizeof set, &set) == 0) n = static_cast<uint32_t>(CPU_COUNT(&set));
-    if (FILE *f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
-        char q[32] = {0};
-        unsigned long period = 0;
-        if (std::fscanf(f, "%31s %lu", q, &period) == 2 && std::strcmp(q, "max") != 0 && period > 0)
-            n = std::min<uint32_t>(n, static_cast<uint32_t>(std::max(1.0, std::atof(q) / double(period))));
-        std::fclose(f);
-    }
-    return std::max(1u, n);
+// Futex on a batch's generation word (process-private).
+void gen_wait(std::atomic<uint32_t> &g, uint32_t seen) {
+    static_assert(sizeof(std::atomic<uint32_t>) == sizeof(uint32_t), "futex word");
+    (void)syscall(SYS_futex, reinterpret_cast<uint32_t *>(&g), FUTEX_WAIT_PRIVATE, seen, nullptr, nullptr, 0);
+}
+
+// The batch's verdicts are in (or it failed): release its spinning and its
+// sleeping waiters.
+void publish_done(BatchBuf &x) {
+    x.done_seq.store(x.seq, std::memory_order_release);
+    x.gen.fetch_add(1, std::memory_order_release);
+    (void)syscall(SYS_futex, reinterpret_cast<uint32_t *>(&x.gen), FUTEX_WAKE_PRIVATE, INT32_MAX, nullptr, nullptr, 0);
 }
 
 void release_buffers(nffacl_batcher *b) {
@@ -103,9 +105,7 @@ void launch_one(nffacl_batcher *b, std::unique_lock<std::mutex> &lk) {
         b->error = st != NFFACL_OK ? st : NFFACL_ERR_HIP;
         --b->inflight_n;
         x.state = BatchBuf::DONE;  // wake the waiters with the error
-        x.done_seq.store(x.seq, std::memory_order_release);
-        std::lock_guard<std::mutex> w(x.wmu);
-        x.wcv.notify_all();
+        publish_done(x);
         return;
     }
     x.state = BatchBuf::LAUNCHED;
@@ -161,11 +161,7 @@ void completer_main(nffacl_batcher *b) {
             b->error = NFFACL_ERR_HIP;
             lk.unlock();
         }
-        x.done_seq.store(x.seq, std::memory_order_release);  // spinning waiters go now
-        {
-            std::lock_guard<std::mutex> w(x.wmu);  // blocked waiters
-            x.wcv.notify_all();
-        }
+        publish_done(x);
         lk.lock();
         b->inflight.pop_front();
         --b->inflight_n;
@@ -195,8 +191,23 @@ int nffacl_batcher_create(nffacl_engine *eng, uint32_t stride, uint32_t max_batc
     b->max_batch = max_batch;
     b->max_delay = std::chrono::microseconds(max_delay_us);
     b->nbuf = nbuf;
-    const uint32_t cpus = cpu_share();
-    b->spin_limit = cpus > 3 ? cpus - 3 : 1;  // the launcher, the completer and one spare
+    // Waiters sleep on the batch's futex word at once by default: spinning
+    // (sched_yield loops) was slower at every fan-in measured on a 16-CPU
+    // share — one thread × 32: 0.98-1.09 Mpps spinning (up to share − 3
+    // spinners) vs 1.25-1.35 sleeping (p50 22-24 µs); 32 × 32: 6.9-7.0 vs
+    // 8.7-9.1; 64 × 32: 3.9-5.0 vs 5.6-5.8 (profiles/r2_batcher/spin*.jsonl).
+    b->spin_limit = 0;
+    {  // NFFACL_TUNE_BATCH_SPIN: spinning waiters at most (experiments; read once, here)
+        long v = 0;
+        bool set = false;
+        std::string err;
+        if (!env_knob("NFFACL_TUNE_BATCH_SPIN", 0, 1024, v, set, err)) {
+            set_last_error(err);
+            delete b;
+            return NFFACL_ERR_INVALID_ARG;
+        }
+        if (set) b->spin_limit = static_cast<uint32_t>(v);
+    }
     b->bufs.reset(new (std::nothrow) BatchBuf[nbuf]);
     if (!b->bufs) {
         delete b;
@@ -278,8 +289,7 @@ int nffacl_batcher_wait(nffacl_batcher *b, const nffacl_ticket *t, uint32_t *por
     if (t->buf >= b->nbuf) return NFFACL_ERR_INVALID_ARG;
     BatchBuf &x = b->bufs[t->buf];
     auto done = [&] { return x.done_seq.load(std::memory_order_acquire) == t->seq; };
-    // spin first, without locks (the reference's flow-function clones
-    // busy-poll their cores) while the host has CPUs to spare; then block
+    // optionally spin first, without locks (NFFACL_TUNE_BATCH_SPIN); then sleep
     if (!done()) {
         if (b->spinners.fetch_add(1, std::memory_order_acq_rel) < b->spin_limit) {
             const auto spin_until = Clock::now() + std::chrono::microseconds(200);
@@ -292,8 +302,11 @@ int nffacl_batcher_wait(nffacl_batcher *b, const nffacl_ticket *t, uint32_t *por
             std::lock_guard<std::mutex> g(b->mu);
             if (x.seq != t->seq || x.state == BatchBuf::FREE) return NFFACL_ERR_INVALID_ARG;  // stale ticket
         }
-        std::unique_lock<std::mutex> w(x.wmu);
-        x.wcv.wait(w, done);
+        while (true) {
+            const uint32_t g = x.gen.load(std::memory_order_acquire);
+            if (done()) break;
+            gen_wait(x.gen, g);  // returns at once if the generation moved on
+        }
     }
     const int st = b->error;
     if (ports && st == NFFACL_OK) std::memcpy(ports, x.h_port + t->off, size_t(t->n) * 4);

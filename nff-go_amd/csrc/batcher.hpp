@@ -41,8 +41,9 @@ struct BatchBuf {
     std::atomic<uint32_t> readers{0};  // bursts that have not collected their verdicts yet
     std::atomic<uint32_t> written{0};  // packets whose bytes are in h_slots
     std::atomic<uint64_t> done_seq{0}; // == seq once the verdicts are in h_port
-    std::mutex wmu;                    // waiters that stopped spinning block on wcv
-    std::condition_variable wcv;
+    // bumped after done_seq: waiters that stopped spinning sleep on it
+    // (futex; one wake releases all of them at once, no mutex to re-take)
+    std::atomic<uint32_t> gen{0};
     std::chrono::steady_clock::time_point opened;
     uint8_t *h_slots = nullptr;   // mapped pinned host memory
     uint32_t *h_port = nullptr;
