@@ -194,7 +194,9 @@ typedef struct nffacl_dim_info {
     uint64_t n_entries;  /* bucket entries (with replication) */
     uint32_t kind2;      /* 6 = none (1-D slot); else a second key (kinds as above): the slot is a
                             2-D grid, bucket = (key >> shift) << bits2 | key2 >> shift2 */
-    uint32_t shift2, bits2, reserved;
+    uint32_t shift2, bits2;
+    uint32_t dir8;       /* 1: off_dir16 holds u8 offsets dir8[n_buckets + 1] and off_dir the u32 bases
+                            of 16-bucket groups: dir[t] = base[t >> 4] + dir8[t] */
 } nffacl_dim_info;
 
 #define NFFACL_MAX_SLOTS 8

@@ -229,7 +229,7 @@ int nffacl_table_compile(const nffacl_rules *rules, int algo, uint32_t *blob, ui
         for (uint32_t k = 0; k < kMaxSlots; ++k) {
             const DimInfo &d = fi[f]->dims[k];
             o.dims[k] = nffacl_dim_info{d.kind, d.shift, d.n_buckets, d.off_dir, d.off_ent, d.n_rules,
-                                        d.max_list, d.off_dir16, d.n_ent, d.kind2, d.shift2, d.bits2, 0};
+                                        d.max_list, d.off_dir16, d.n_ent, d.kind2, d.shift2, d.bits2, d.dir8};
         }
     }
     if (blob) {

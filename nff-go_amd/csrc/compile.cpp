@@ -407,13 +407,20 @@ uint64_t entries_at(const DimBuild &d, uint32_t rb) {
 // one bit at a time, the slot whose mean list grows least per byte saved
 // (weighted by its family's share of the rules, a proxy for its share of
 // the traffic).
-void size_directories(DimBuild *const *all, const double *weight, int nd, size_t budget, bool dir16) {
+// LDS bytes of a directory of nb buckets in form fmt: 0 plain u32, 16 two-level
+// u16 (groups of 64), 8 two-level u8 (groups of 16).
+double dir_form_bytes(double nb, int fmt) {
+    if (fmt == 8) return 1.0 * (nb + 8) + 4.0 * (std::floor(nb / (1u << kDir8GroupShift)) + 2);
+    if (fmt == 16) return 2.0 * (nb + 4) + 4.0 * (std::floor(nb / (1u << kDir16GroupShift)) + 2);
+    return 4.0 * (nb + 1);
+}
+
+void size_directories(DimBuild *const *all, const double *weight, int nd, size_t budget, int fmt) {
     std::vector<uint32_t> rb(nd);
     std::vector<std::vector<double>> mean(nd);
     auto bytes = [&](int i, uint32_t b) {
         if (all[i]->rules.empty()) return 16.0;
-        const double nb = double(1u << b);
-        return dir16 ? 2.0 * (nb + 4) + 4.0 * (std::floor(nb / (1u << kDir16GroupShift)) + 2) : 4.0 * (nb + 1);
+        return dir_form_bytes(double(1u << b), fmt);
     };
     for (int i = 0; i < nd; ++i) {
         const DimBuild &d = *all[i];
@@ -466,8 +473,8 @@ void fill_lists(DimBuild &d) {
 // Radix widths for `budget` bytes of directories, then the bucket lists;
 // returns the expected candidates per packet (mean list length summed over
 // the slots, families weighted by their share of the rules).
-double size_and_fill(DimBuild *const *all, const double *weight, size_t budget, bool dir16 = false) {
-    size_directories(all, weight, 8, budget, dir16);
+double size_and_fill(DimBuild *const *all, const double *weight, size_t budget, int fmt = 0) {
+    size_directories(all, weight, 8, budget, fmt);
     double expect = 0;
     for (int i = 0; i < 8; ++i) {
         DimBuild &d = *all[i];
@@ -897,6 +904,7 @@ void build_hybrid(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vec
     const size_t tuned = opt.dir_bytes;
     const int force = opt.flat;
     const bool want16 = opt.dir16;
+    const bool want8 = opt.dir8 && want16;
     if (force == 1 && !tuned) {  // global directories: generalized (1-D / 2-D) slots
         build_hybrid_g(rec4, n4, rec6, n6, opt, 0, out);
         return;
@@ -908,27 +916,38 @@ void build_hybrid(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vec
     size_t budget = tuned ? tuned : (force == 1 ? kHybFlatDirBytes : kHybLaneDirBytes);
     const bool lds_dirs = force != 1 && budget <= kHybLdsDirMaxBytes;
     const bool flat = force != 0 || !lds_dirs;
-    const double expect = size_and_fill(all, weight, budget, lds_dirs && want16);
+    // LDS directories: two-level, u8 offsets when every group fits (else u16, else plain u32)
+    int fmt = lds_dirs ? (want8 ? 8 : want16 ? 16 : 0) : 0;
+    const double expect = size_and_fill(all, weight, budget, fmt);
     // flat-LDS with many candidates per packet: 4 rounds in flight, whose
     // larger scratch takes some of the directory budget
     if (flat && lds_dirs && !tuned && expect > kHybFlat4Candidates) {
         budget = kHybFlat4DirBytes;
-        size_and_fill(all, weight, budget, want16);
+        size_and_fill(all, weight, budget, fmt);
         out.flat_uncond = 1;
     }
     // 4 rounds of candidate loads in flight whenever their scratch fits beside
     // the directories (indexed_launch checks; exact entries, C3: 0.507 vs
     // 0.540 ms at 2 rounds, profiles/r2_exact/)
     if (flat && lds_dirs) out.flat_rounds = 4;
-    // LDS directories: two-level unless some 64-bucket group holds 65536+
-    // entries (then plain u32, re-sized for the same budget)
-    bool dir16 = lds_dirs && want16;
-    for (int i = 0; i < 8 && dir16; ++i) {
-        const std::vector<uint32_t> &dir = all[i]->dir;
-        for (size_t t = 0; t < dir.size(); ++t)
-            if (dir[t] - dir[(t >> kDir16GroupShift) << kDir16GroupShift] > 0xFFFFu) { dir16 = false; break; }
+    // a group whose lists overflow its offsets: the next wider form, re-sized for the same budget
+    auto form_fits = [&](int f) {
+        if (f == 0) return true;
+        const uint32_t gs = f == 8 ? kDir8GroupShift : kDir16GroupShift;
+        const uint32_t lim = f == 8 ? 0xFFu : 0xFFFFu;
+        for (int i = 0; i < 8; ++i) {
+            const std::vector<uint32_t> &dir = all[i]->dir;
+            for (size_t t = 0; t < dir.size(); ++t)
+                if (dir[t] - dir[(t >> gs) << gs] > lim) return false;
+        }
+        return true;
+    };
+    while (!form_fits(fmt)) {
+        fmt = fmt == 8 && want16 ? 16 : 0;
+        size_and_fill(all, weight, budget, fmt);
     }
-    if (lds_dirs && want16 && !dir16) size_and_fill(all, weight, budget, false);
+    const bool dir16 = fmt != 0;
+    out.dir8 = fmt == 8 ? 1u : 0u;
     std::vector<uint32_t> &blob = out.blob;
     FamilyIndex *fi[2] = {&out.idx4, &out.idx6};
     const std::vector<uint32_t> *recs[2] = {&rec4, &rec6};
@@ -946,13 +965,19 @@ void build_hybrid(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vec
                 continue;
             }
             const size_t nb = dir.size() - 1;
-            const size_t groups = (nb >> kDir16GroupShift) + 2;  // base[g + 1] stays readable
-            for (size_t g = 0; g < groups; ++g) blob.push_back(dir[std::min(g << kDir16GroupShift, nb)]);
+            const uint32_t gs = out.dir8 ? kDir8GroupShift : kDir16GroupShift;
+            const size_t groups = (nb >> gs) + 2;  // base[g + 1] stays readable
+            for (size_t g = 0; g < groups; ++g) blob.push_back(dir[std::min(g << gs, nb)]);
             dir_words[4 * f + k] = static_cast<uint32_t>(groups);
             di.off_dir16 = static_cast<uint32_t>(blob.size());
-            auto rel = [&](size_t t) -> uint32_t {
-                return t <= nb ? dir[t] - dir[(t >> kDir16GroupShift) << kDir16GroupShift] : 0u;
-            };
+            di.dir8 = out.dir8;
+            auto rel = [&](size_t t) -> uint32_t { return t <= nb ? dir[t] - dir[(t >> gs) << gs] : 0u; };
+            if (out.dir8) {
+                const size_t words = (nb + 4) / 4 + 1;  // dword (t >> 2) + 1 stays readable
+                for (size_t w = 0; w < words; ++w)
+                    blob.push_back(rel(4 * w) | rel(4 * w + 1) << 8 | rel(4 * w + 2) << 16 | rel(4 * w + 3) << 24);
+                continue;
+            }
             const size_t words = (nb + 2) / 2 + 1;  // dword (t >> 1) + 1 stays readable
             for (size_t w = 0; w < words; ++w) blob.push_back(rel(2 * w) | rel(2 * w + 1) << 16);
         }
@@ -1037,6 +1062,8 @@ bool CompileOptions::from_env(CompileOptions &o, std::string &err) {
     if (set) o.dir_bytes = size_t(v) * 1024;
     if (!env_knob("NFFACL_TUNE_DIR16", 0, 1, v, set, err)) return false;
     if (set) o.dir16 = v != 0;
+    if (!env_knob("NFFACL_TUNE_DIR8", 0, 1, v, set, err)) return false;
+    if (set) o.dir8 = v != 0;
     if (!env_knob("NFFACL_TUNE_SLOTS2D", 0, 2, v, set, err)) return false;
     if (set) o.slots2d = static_cast<int>(v);
     if (!env_knob("NFFACL_TUNE_SLOT_COST", 0, 1000, v, set, err)) return false;

@@ -23,6 +23,7 @@ struct DimInfo {
                              // 2-level directory's group bases base[n_buckets / 64 + 2])
     uint32_t off_dir16 = 0;  // 0, or dword offset of the u16 offsets dir16[n_buckets + 1]:
                              // dir[t] = base[t >> 6] + dir16[t]
+    uint32_t dir8 = 0;       // 1: off_dir16 holds u8 offsets instead, dir[t] = base[t >> 4] + dir8[t]
     uint32_t off_ent = 0;    // dword offset of the bucket entries (inline rule entries)
     uint32_t n_rules = 0;    // rules assigned to this dimension
     uint64_t n_ent = 0;      // bucket entries (with replication)
@@ -58,6 +59,9 @@ struct CompiledTable {
     // flat-LDS walk with many expected candidates per packet: its entry
     // loads are issued without a per-lane branch (engine.hip kTabFlatLds4U)
     uint32_t flat_uncond = 0;
+    // two-level LDS directories with u8 offsets per 16-bucket group (every
+    // slot of the table; DimInfo::dir8)
+    uint32_t dir8 = 0;
     // HYBRID global-directory form with generalized slots (dims[k].kind2 etc.;
     // idx*.used_slots = slots in use, all non-empty)
     bool slots_g = false;
@@ -72,6 +76,7 @@ struct CompileOptions {
                             // 2: flat-LDS with generalized 1-D / 2-D slots
     double slot_cost = 0.1; // NFFACL_TUNE_SLOT_COST (1/100): expected candidates per packet a slot must save
     bool dir16 = true;      // NFFACL_TUNE_DIR16: two-level u16 LDS directories allowed
+    bool dir8 = true;       // NFFACL_TUNE_DIR8: two-level u8 LDS directories allowed (HYBRID)
     // false (+ `err`) if a set variable is out of range
     static bool from_env(CompileOptions &o, std::string &err);
 };

@@ -371,6 +371,7 @@ struct IndexedArgs {
     const uint32_t *tab;    // device table (global memory)
     uint32_t stage_dwords;  // leading dwords staged in LDS (multiple of 4)
     uint32_t flags;         // NFFACL_PARSE_*
+    uint32_t dir8;          // HYBRID: two-level directories carry u8 offsets (SplitTab::bounds)
     FamArgs f4, f6;
 };
 
@@ -413,7 +414,8 @@ __device__ __forceinline__ void bounds32(const T &tab, uint32_t dir, uint32_t t,
 
 struct LdsTab {
     __device__ __forceinline__ uint32_t ld(uint32_t i) const { return lds_tab[i]; }
-    __device__ __forceinline__ void bounds(uint32_t dir, uint32_t, uint32_t t, uint32_t &lo, uint32_t &hi) const {
+    __device__ __forceinline__ void bounds(uint32_t dir, uint32_t, uint32_t t, uint32_t &lo, uint32_t &hi,
+                                           bool = false) const {
         bounds32(*this, dir, t, lo, hi);
     }
     __device__ __forceinline__ u32x4 ld4(uint32_t i) const {
@@ -423,7 +425,8 @@ struct LdsTab {
 struct GlobalTab {
     const uint32_t *__restrict__ p;
     __device__ __forceinline__ uint32_t ld(uint32_t i) const { return p[i]; }
-    __device__ __forceinline__ void bounds(uint32_t dir, uint32_t, uint32_t t, uint32_t &lo, uint32_t &hi) const {
+    __device__ __forceinline__ void bounds(uint32_t dir, uint32_t, uint32_t t, uint32_t &lo, uint32_t &hi,
+                                           bool = false) const {
         bounds32(*this, dir, t, lo, hi);
     }
     __device__ __forceinline__ u32x4 ld4(uint32_t i) const {
@@ -434,11 +437,21 @@ struct GlobalTab {
 struct SplitTab {
     const uint32_t *__restrict__ p;
     __device__ __forceinline__ uint32_t ld(uint32_t i) const { return lds_tab[i]; }
-    // two-level directory (table.hpp): dir[t] = base[t >> 6] + dir16[t]
-    __device__ __forceinline__ void bounds(uint32_t dir, uint32_t dir16, uint32_t t, uint32_t &lo,
-                                           uint32_t &hi) const {
+    // two-level directory (table.hpp): dir[t] = base[t >> 6] + dir16[t], or
+    // with dir8 (wave-uniform) base[t >> 4] + dir8[t]
+    __device__ __forceinline__ void bounds(uint32_t dir, uint32_t dir16, uint32_t t, uint32_t &lo, uint32_t &hi,
+                                           bool dir8 = false) const {
         if (dir16 == 0u) {
             bounds32(*this, dir, t, lo, hi);
+            return;
+        }
+        if (dir8) {
+            const uint32_t g = t >> kDir8GroupShift;
+            const uint32_t b0 = lds_tab[dir + g], b1 = lds_tab[dir + g + 1];                    // ds_read2
+            const uint32_t w0 = lds_tab[dir16 + (t >> 2)], w1 = lds_tab[dir16 + (t >> 2) + 1];  // ds_read2
+            const uint32_t x = __builtin_amdgcn_alignbit(w1, w0, (t & 3u) * 8u);  // bytes t, t + 1
+            lo = b0 + (x & 0xFFu);
+            hi = (((t + 1u) & ((1u << kDir8GroupShift) - 1u)) == 0u ? b1 : b0) + ((x >> 8) & 0xFFu);
             return;
         }
         const uint32_t g = t >> kDir16GroupShift;
@@ -494,7 +507,7 @@ __device__ __forceinline__ uint32_t classify_indexed(const T &tab, const Indexed
         base[s] = v6 ? s6.off_ent : s4.off_ent;
         const uint32_t t = key[s] >> shift;  // < n_buckets for any key: both reads in range
         uint32_t lo, hi;
-        tab.bounds(dir, v6 ? s6.off_dir16 : s4.off_dir16, t, lo, hi);
+        tab.bounds(dir, v6 ? s6.off_dir16 : s4.off_dir16, t, lo, hi, a.dir8 != 0u);
         c[s] = lo;
         e[s] = mine ? hi : lo;
     }
@@ -690,7 +703,7 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
                            (pick(v6 ? s6.f2 : s4.f2) >> (v6 ? s6.shift2 : s4.shift2));
         if (LDS_DIRS) {
             uint32_t hi;
-            SplitTab{a.tab}.bounds(dir, v6 ? s6.off_dir16 : s4.off_dir16, t, st[s], hi);
+            SplitTab{a.tab}.bounds(dir, v6 ? s6.off_dir16 : s4.off_dir16, t, st[s], hi, a.dir8 != 0u);
             ln[s] = mine ? hi - st[s] : 0u;
         } else {
             // generalized slots: a family's unused slots (f1 == kFZero) read nothing
@@ -712,18 +725,21 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
     const uint32_t proto_fam = f.proto | (v6 ? 0x100u : 0u);
     const uint32_t *__restrict__ E4 = a.tab + a.f4.off_ent_base;
     const uint32_t *__restrict__ E6 = a.tab + a.f6.off_ent_base;
-    for (uint32_t win = 0; win < T; win += 64 * R) {
-        // (every round runs, empty or not: straight-line rounds let the
-        // compiler interleave their loads; skipping the empty rounds of a
-        // partial window behind wave-uniform branches measured 4 % slower on
-        // C5, profiles/r2_exact/skip/)
+    // One window of RR rounds (64 RR candidates) starting at candidate `win`,
+    // straight-line so the compiler interleaves its RR rounds of loads.  A
+    // window of R rounds runs while at least 64 (R - 1) + 1 candidates
+    // remain; the last window runs only the rounds its candidates fill (one
+    // wave-uniform dispatch on the remainder, not a branch per round: per-round
+    // branches broke the load interleave, profiles/r2_exact/skip/).
+    auto window = [&](uint32_t win, auto rr) {
+        constexpr int RR = decltype(rr)::value;
 #pragma unroll
-        for (int j = 0; j < R; ++j) W.mark[64 * j + lane] = 0u;
+        for (int j = 0; j < RR; ++j) W.mark[64 * j + lane] = 0u;
         wave_lds_sync();
         uint32_t so = off;  // candidate number of list s's first entry
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
-            if (ln[s] != 0u && so < win + 64u * R && so + ln[s] > win) {
+            if (ln[s] != 0u && so < win + 64u * RR && so + ln[s] > win) {
                 const uint32_t pos = so > win ? so - win : 0u;
                 W.mark[pos] = (((lane * NS + s) << 8) | pos) + 1u;
                 W.delta[pos] = ((st[s] - so) << 1) | (v6 ? 1u : 0u);
@@ -731,41 +747,45 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
             so += ln[s];
         }
         wave_lds_sync();
-        // R rounds: locate every candidate's list, then issue every round's
-        // entry loads (IPv6 candidates: all four pieces) before testing any
-        uint32_t owner[R], idx[R];
-        bool valid[R], six[R];
-        u32x3 A[R], B[R], C[R], D[R];
+        // RR rounds: locate every candidate's list, then issue every round's
+        // entry loads (IPv6 candidates: all four pieces) before testing any.
+        // Rounds 0..RR-2 are full (the dispatch below), only round RR-1 can
+        // hold lanes past the wave's candidates (the per-round k < T test
+        // stays: with it compiled out the scheduler hoists more loads, and
+        // the frames kernels spill at 128 VGPRs).
+        uint32_t owner[RR], idx[RR];
+        bool valid[RR], six[RR];
+        u32x3 A[RR], B[RR], C[RR], D[RR];
         uint32_t carry = 0;
 #pragma unroll
-        for (int j = 0; j < R; ++j) {
+        for (int j = 0; j < RR; ++j) {
             const uint32_t m = max(wave_incl_max(W.mark[64 * j + lane]), carry);
-            carry = __builtin_amdgcn_readlane(m, 63);
+            if (j + 1 < RR) carry = __builtin_amdgcn_readlane(m, 63);
             const uint32_t k = win + 64u * j + lane;
             valid[j] = k < T;
             owner[j] = ((m - 1u) >> 8) / NS;
             const uint32_t dp = W.delta[(m - 1u) & 0xFFu];
             six[j] = (dp & 1u) != 0u;
             // UNCOND: lanes past the wave's candidates load entry 0 of the
-            // IPv4 list (untested) instead of branching around the load —
-            // C5 0.750 vs 0.782 ms, but C3, whose last rounds are mostly
-            // empty, 0.59 vs 0.54 ms (profiles/r2_exact/uncond/)
+            // IPv4 list (untested) instead of branching around the load
+            // (profiles/r2_exact/uncond/)
             const uint32_t ent = !UNCOND || valid[j] ? k + static_cast<uint32_t>(static_cast<int32_t>(dp) >> 1) : 0u;
             const uint32_t *e = six[j] && (!UNCOND || valid[j]) ? E6 + ent * kHybEnt6Dwords : E4 + ent * kHybEnt4Dwords;
-            A[j] = B[j] = C[j] = D[j] = u32x3{0, 0, 0};
             if (UNCOND || valid[j]) {
                 A[j] = ld3(e);
                 B[j] = ld3(e + 3);
+            } else {
+                A[j] = B[j] = u32x3{0, 0, 0};
             }
-            if (valid[j] && six[j]) {
+            if (valid[j] && six[j]) {  // (C, D are read only for valid IPv6 candidates)
                 C[j] = ld3(e + 6);
                 D[j] = ld3(e + 9);
             }
         }
-        bool pass[R];
+        bool pass[RR];
         bool any6 = false;
 #pragma unroll
-        for (int j = 0; j < R; ++j) {
+        for (int j = 0; j < RR; ++j) {
             // the owner packet's fields
             const uint32_t o = owner[j];
             const uint32_t oks = bperm(ks, o), okd = bperm(kd, o);
@@ -782,7 +802,7 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
                 tb[q] = __builtin_bswap32(f.t[q]);
             }
 #pragma unroll
-            for (int j = 0; j < R; ++j) {
+            for (int j = 0; j < RR; ++j) {
                 if (ballot(pass[j] && six[j])) {  // whole wave: bpermute reads every lane
                     uint32_t os[4] = {0, 0, 0, 0}, ot[4] = {0, 0, 0, 0};
 #pragma unroll
@@ -797,10 +817,21 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
         // (posting from every lane, ~0 to its own word when nothing passed,
         // instead of the branch: C5 0.757 vs 0.750 ms, profiles/r2_exact/uncond/am_*)
 #pragma unroll
-        for (int j = 0; j < R; ++j)  // rule index << 32 | output code: the minimum carries the winner's output
+        for (int j = 0; j < RR; ++j)  // rule index << 32 | output code: the minimum carries the winner's output
             if (pass[j]) atomicMin(reinterpret_cast<unsigned long long *>(&W.best[owner[j]]),
                                    static_cast<unsigned long long>(idx[j]) << 32 | (B[j].z >> kHybOutShift));
         wave_lds_sync();
+    };
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, (R >= 3 ? 3 : R)>;
+    using IR = std::integral_constant<int, R>;
+    for (uint32_t win = 0; win < T; win += 64 * R) {
+        const uint32_t rem = T - win;  // wave-uniform
+        if (rem > 64u * (R - 1)) window(win, IR{});
+        else if (R >= 3 && rem > 128u) window(win, I3{});
+        else if (rem > 64u) window(win, I2{});
+        else window(win, I1{});
     }
     uint64_t best = W.best[lane];  // ~0 or rule index << 32 | output code
     // rules with no selective key: wave-uniform scan in rule order per family
@@ -1096,6 +1127,7 @@ static dev::IndexedArgs indexed_args(const DevTable *t) {
     a.tab = t->d_blob;
     const bool hyb = t->meta.algo == NFFACL_ALGO_HYBRID;
     a.stage_dwords = hyb ? t->meta.lds_dwords : static_cast<uint32_t>(t->meta.blob.size());
+    a.dir8 = hyb ? t->meta.dir8 : 0u;
     auto fam = [&](const FamilyIndex &fi, uint32_t off_cold, dev::FamArgs &fa) {
         for (uint32_t k = 0; k < kMaxSlots; ++k) {
             const DimInfo &d = fi.dims[k];

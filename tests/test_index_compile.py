@@ -20,7 +20,7 @@ class DimInfo(ctypes.Structure):
                 ("off_dir", ctypes.c_uint32), ("off_entries", ctypes.c_uint32), ("n_rules", ctypes.c_uint32),
                 ("max_list", ctypes.c_uint32), ("off_dir16", ctypes.c_uint32), ("n_entries", ctypes.c_uint64),
                 ("kind2", ctypes.c_uint32), ("shift2", ctypes.c_uint32), ("bits2", ctypes.c_uint32),
-                ("reserved", ctypes.c_uint32)]
+                ("dir8", ctypes.c_uint32)]
 
 
 MAX_SLOTS = 8
@@ -105,11 +105,15 @@ def bucket_of(di, F):
 
 def dir_values(blob, di):
     """dir[0..n_buckets] of a slot: plain u32, or two-level (table.hpp:
-    dir[t] = base[t >> 6] + u16 dir16[t])."""
+    dir[t] = base[t >> 6] + u16 dir16[t], or base[t >> 4] + u8 dir8[t])."""
     nb = di.n_buckets
     if di.off_dir16 == 0:
         return blob[di.off_dir:di.off_dir + nb + 1].astype(np.int64)
     t = np.arange(nb + 1)
+    if di.dir8:
+        base = blob[di.off_dir + (t >> 4)].astype(np.int64)
+        w = blob[di.off_dir16 + (t >> 2)].astype(np.int64)
+        return base + ((w >> (8 * (t & 3))) & 0xFF)
     base = blob[di.off_dir + (t >> 6)].astype(np.int64)
     w = blob[di.off_dir16 + (t >> 1)].astype(np.int64)
     rel = np.where(t & 1, w >> 16, w & 0xFFFF)
