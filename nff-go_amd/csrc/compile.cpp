@@ -115,6 +115,7 @@ struct DimBuild {
     std::vector<KeyRange> ranges; // parallel to rules
     // built
     uint32_t rb = 0, shift = 0, max_list = 0;
+    uint32_t max_rb = 32;             // radix cap (coarse address slots, see build_hybrid)
     std::vector<uint32_t> dir, ents;  // ents: record indices per bucket entry
     std::vector<uint64_t> span;       // per rule: buckets covered
 };
@@ -128,6 +129,13 @@ uint32_t pick_rb(size_t n, uint32_t key_bits) {
 }
 
 uint64_t budget_for(size_t n) { return 8ull * n + 65536ull; }
+
+// Coarse address slots (build_hybrid): rules kCoarseGap+ bits shorter than
+// their slot's radix move, when the slot holds >= kCoarseMinRules rules and
+// >= kCoarseMinMoved of them would move.
+constexpr uint32_t kCoarseGap = 3;
+constexpr size_t kCoarseMinRules = 4096;
+constexpr size_t kCoarseMinMoved = 256;
 
 // Fewest rules worth a source-port slot of their own (see assign_family).
 constexpr size_t kMinSportRules = 128;
@@ -425,7 +433,7 @@ void size_directories(DimBuild *const *all, const double *weight, int nd, size_t
     for (int i = 0; i < nd; ++i) {
         const DimBuild &d = *all[i];
         if (d.rules.empty()) { rb[i] = 1; continue; }
-        rb[i] = pick_rb(d.rules.size(), d.key_bits);
+        rb[i] = std::max(1u, std::min(pick_rb(d.rules.size(), d.key_bits), d.max_rb));
         mean[i].assign(rb[i] + 1, 0.0);
         for (uint32_t b = 1; b <= rb[i]; ++b) mean[i][b] = double(entries_at(d, b)) / double(1u << b);
     }
@@ -473,10 +481,10 @@ void fill_lists(DimBuild &d) {
 // Radix widths for `budget` bytes of directories, then the bucket lists;
 // returns the expected candidates per packet (mean list length summed over
 // the slots, families weighted by their share of the rules).
-double size_and_fill(DimBuild *const *all, const double *weight, size_t budget, int fmt = 0) {
-    size_directories(all, weight, 8, budget, fmt);
+double size_and_fill(DimBuild *const *all, const double *weight, size_t budget, int fmt = 0, int nd = 8) {
+    size_directories(all, weight, nd, budget, fmt);
     double expect = 0;
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < nd; ++i) {
         DimBuild &d = *all[i];
         if (d.rules.empty()) {
             d.rb = 1;
@@ -930,13 +938,61 @@ void build_hybrid(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vec
     // the directories (indexed_launch checks; exact entries, C3: 0.507 vs
     // 0.540 ms at 2 rounds, profiles/r2_exact/)
     if (flat && lds_dirs) out.flat_rounds = 4;
+    if (flat && lds_dirs && opt.uncond >= 0) out.flat_uncond = static_cast<uint32_t>(opt.uncond);
+    // Coarse address slots (flat-LDS): a rule whose prefix is shorter than
+    // its address slot's radix is replicated into 2^(radix - length) buckets
+    // (C5 at 15-bit radixes: 3.1-3.5 entries per rule, 6.4 MB of entries,
+    // L2 hit rate 0.55).  Rules at least kCoarseGap bits shorter than the
+    // radix move to a second slot on the same field whose radix is capped at
+    // that threshold: the same candidates per packet (a bucket no finer than
+    // the prefix), far fewer copies.  The slots are then compacted per family
+    // (generalized slots: each keyed on its field, CompiledTable::slots_g).
+    // Measured slower on C5 (table 7.7 -> 3.7 MB, L2 traffic down, but the
+    // two extra slots' lookups and marks cost more: 0.722 vs 0.649 ms), so
+    // it is a tuning option (NFFACL_TUNE_COARSE=1), off by default.
+    DimBuild coarse[2][2];
+    std::vector<DimBuild *> ext(all, all + 8);
+    std::vector<double> wext(weight, weight + 8);
+    bool compact = false;
+    if (flat && lds_dirs && opt.coarse) {
+        for (int f = 0; f < 2; ++f)
+            for (int k = 0; k < 2; ++k) {  // dst, src
+                DimBuild &d = plan[f].dims[k];
+                if (d.rules.size() < kCoarseMinRules || d.rb < kCoarseGap + 8) continue;
+                const uint32_t thr = d.rb - kCoarseGap;
+                DimBuild &c = coarse[f][k];
+                c.kind = d.kind;
+                c.key_bits = d.key_bits;
+                c.max_rb = thr;
+                const uint64_t wide = uint64_t(1) << (d.key_bits - thr);  // prefix shorter than thr bits
+                std::vector<uint32_t> keep;
+                std::vector<KeyRange> keep_r;
+                for (size_t i = 0; i < d.rules.size(); ++i) {
+                    const bool move = uint64_t(d.ranges[i].hi) - d.ranges[i].lo + 1 > wide;
+                    (move ? c.rules : keep).push_back(d.rules[i]);
+                    (move ? c.ranges : keep_r).push_back(d.ranges[i]);
+                }
+                if (c.rules.size() < kCoarseMinMoved) {  // not worth a slot: keep them
+                    c.rules.clear();
+                    c.ranges.clear();
+                    continue;
+                }
+                d.rules.swap(keep);
+                d.ranges.swap(keep_r);
+                ext.push_back(&c);
+                wext.push_back(weight[4 * f]);
+                compact = true;
+            }
+        if (compact) size_and_fill(ext.data(), wext.data(), budget, fmt, static_cast<int>(ext.size()));
+    }
+    const int nd = static_cast<int>(ext.size());
     // a group whose lists overflow its offsets: the next wider form, re-sized for the same budget
     auto form_fits = [&](int f) {
         if (f == 0) return true;
         const uint32_t gs = f == 8 ? kDir8GroupShift : kDir16GroupShift;
         const uint32_t lim = f == 8 ? 0xFFu : 0xFFFFu;
-        for (int i = 0; i < 8; ++i) {
-            const std::vector<uint32_t> &dir = all[i]->dir;
+        for (int i = 0; i < nd; ++i) {
+            const std::vector<uint32_t> &dir = ext[i]->dir;
             for (size_t t = 0; t < dir.size(); ++t)
                 if (dir[t] - dir[(t >> gs) << gs] > lim) return false;
         }
@@ -944,31 +1000,44 @@ void build_hybrid(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vec
     };
     while (!form_fits(fmt)) {
         fmt = fmt == 8 && want16 ? 16 : 0;
-        size_and_fill(all, weight, budget, fmt);
+        size_and_fill(ext.data(), wext.data(), budget, fmt, nd);
     }
     const bool dir16 = fmt != 0;
     out.dir8 = fmt == 8 ? 1u : 0u;
+    // slot order per family: positional [dst, src, dport, sport] (empty ones
+    // included), or compacted (non-empty slots only, coarse ones last)
+    std::vector<DimBuild *> order[2];
+    for (int f = 0; f < 2; ++f) {
+        for (int k = 0; k < 4; ++k)
+            if (!compact || !plan[f].dims[k].rules.empty()) order[f].push_back(&plan[f].dims[k]);
+        for (int k = 0; k < 2; ++k)
+            if (compact && !coarse[f][k].rules.empty()) order[f].push_back(&coarse[f][k]);
+    }
     std::vector<uint32_t> &blob = out.blob;
     FamilyIndex *fi[2] = {&out.idx4, &out.idx6};
     const std::vector<uint32_t> *recs[2] = {&rec4, &rec6};
     const uint32_t rw[2] = {kRec4Dwords, kRec6Dwords};
-    // the eight directories first: the LDS image of the lane and flat-LDS forms
-    uint32_t dir_words[8];  // directory words holding entry numbers (base words when two-level)
+    if (compact) {  // an empty directory {0, 0} for the kernels' unused slots (staged with the rest)
+        out.off_empty_dir = 0;
+        blob.insert(blob.end(), {0u, 0u});
+    }
+    // the directories first: the LDS image of the lane and flat-LDS forms
+    uint32_t dir_words[2][kMaxSlots];  // directory words holding entry numbers (base words when two-level)
     for (int f = 0; f < 2; ++f)
-        for (int k = 0; k < 4; ++k) {
-            const std::vector<uint32_t> &dir = all[4 * f + k]->dir;
+        for (size_t k = 0; k < order[f].size(); ++k) {
+            const std::vector<uint32_t> &dir = order[f][k]->dir;
             DimInfo &di = fi[f]->dims[k];
             di.off_dir = static_cast<uint32_t>(blob.size());
             if (!dir16) {
                 blob.insert(blob.end(), dir.begin(), dir.end());
-                dir_words[4 * f + k] = static_cast<uint32_t>(dir.size());
+                dir_words[f][k] = static_cast<uint32_t>(dir.size());
                 continue;
             }
             const size_t nb = dir.size() - 1;
             const uint32_t gs = out.dir8 ? kDir8GroupShift : kDir16GroupShift;
             const size_t groups = (nb >> gs) + 2;  // base[g + 1] stays readable
             for (size_t g = 0; g < groups; ++g) blob.push_back(dir[std::min(g << gs, nb)]);
-            dir_words[4 * f + k] = static_cast<uint32_t>(groups);
+            dir_words[f][k] = static_cast<uint32_t>(groups);
             di.off_dir16 = static_cast<uint32_t>(blob.size());
             di.dir8 = out.dir8;
             auto rel = [&](size_t t) -> uint32_t { return t <= nb ? dir[t] - dir[(t >> gs) << gs] : 0u; };
@@ -990,8 +1059,8 @@ void build_hybrid(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vec
         const uint32_t ew = flat ? (v6 ? kHybEnt6Dwords : kHybEnt4Dwords) : (v6 ? kEnt6Dwords : kEnt4Dwords);
         fi[f]->entry_dwords = ew;
         fi[f]->off_ent_base = static_cast<uint32_t>(blob.size());
-        for (int k = 0; k < 4; ++k) {
-            DimBuild &d = *all[4 * f + k];
+        for (size_t k = 0; k < order[f].size(); ++k) {
+            DimBuild &d = *order[f][k];
             DimInfo &di = fi[f]->dims[k];
             di.kind = d.kind;
             di.shift = d.shift;
@@ -1002,13 +1071,13 @@ void build_hybrid(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vec
             di.off_ent = static_cast<uint32_t>(blob.size());
             if (flat) {  // directory values: family-relative entry numbers
                 const uint32_t first = (di.off_ent - fi[f]->off_ent_base) / ew;
-                for (uint32_t t = 0; t < dir_words[4 * f + k]; ++t) blob[di.off_dir + t] += first;
+                for (uint32_t t = 0; t < dir_words[f][k]; ++t) blob[di.off_dir + t] += first;
                 for (uint32_t r : d.ents) emit_hyb_entry(recs[f]->data() + size_t(r) * rw[f], v6, r, blob);
             } else {     // relative to off_ent, as INDEXED
                 for (uint32_t r : d.ents) emit_entry(recs[f]->data() + size_t(r) * rw[f], v6, r, blob);
                 if (d.ents.empty()) blob.insert(blob.end(), ew, 0u);  // keep entry 0 addressable
             }
-            if (!d.rules.empty()) fi[f]->used_slots = k + 1;
+            if (!d.rules.empty()) fi[f]->used_slots = static_cast<uint32_t>(k + 1);
         }
         fi[f]->off_resid = static_cast<uint32_t>(blob.size());
         fi[f]->n_resid = static_cast<uint32_t>(plan[f].resid.size());
@@ -1018,6 +1087,7 @@ void build_hybrid(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vec
         }
         while (blob.size() % 4) blob.push_back(0);
     }
+    out.slots_g = compact;
     if (flat) {
         out.off_rec4 = static_cast<uint32_t>(blob.size());
         for (uint32_t r = 0; r < n4; ++r) emit_cold(rec4.data() + size_t(r) * kRec4Dwords, false, blob);
@@ -1064,6 +1134,10 @@ bool CompileOptions::from_env(CompileOptions &o, std::string &err) {
     if (set) o.dir16 = v != 0;
     if (!env_knob("NFFACL_TUNE_DIR8", 0, 1, v, set, err)) return false;
     if (set) o.dir8 = v != 0;
+    if (!env_knob("NFFACL_TUNE_COARSE", 0, 1, v, set, err)) return false;
+    if (set) o.coarse = v != 0;
+    if (!env_knob("NFFACL_TUNE_UNCOND", 0, 1, v, set, err)) return false;
+    if (set) o.uncond = static_cast<int>(v);
     if (!env_knob("NFFACL_TUNE_SLOTS2D", 0, 2, v, set, err)) return false;
     if (set) o.slots2d = static_cast<int>(v);
     if (!env_knob("NFFACL_TUNE_SLOT_COST", 0, 1000, v, set, err)) return false;

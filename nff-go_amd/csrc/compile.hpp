@@ -77,6 +77,9 @@ struct CompileOptions {
     double slot_cost = 0.1; // NFFACL_TUNE_SLOT_COST (1/100): expected candidates per packet a slot must save
     bool dir16 = true;      // NFFACL_TUNE_DIR16: two-level u16 LDS directories allowed
     bool dir8 = true;       // NFFACL_TUNE_DIR8: two-level u8 LDS directories allowed (HYBRID)
+    int uncond = -1;        // NFFACL_TUNE_UNCOND: flat-LDS branch-free entry loads (-1 = policy)
+    bool coarse = false;    // NFFACL_TUNE_COARSE: flat-LDS coarse address slots for short prefixes
+                            // (C5 table 7.7 -> 3.7 MB but 0.722 vs 0.649 ms: off; profiles/r2_dir8/coarse/)
     // false (+ `err`) if a set variable is out of range
     static bool from_env(CompileOptions &o, std::string &err);
 };

@@ -386,6 +386,32 @@ def test_full_size_c5_hybrid(torch_cuda, monkeypatch, flat):
     np.testing.assert_array_equal(outs[nffacl.ALGO_AUTO].cpu().numpy().view(np.uint32)[idx], want)
 
 
+@pytest.mark.parametrize("coarse,dir8", [("1", "1"), ("0", "0")])
+def test_c5_flat_lds_layout_options(torch_cuda, monkeypatch, coarse, dir8):
+    """The flat-LDS layout options besides the default (u8 directories, no
+    coarse slots): coarse address slots (five generalized slots: the NS = 5
+    kernels) and u16 directories, on 64-byte slots and IMIX frames, against
+    the oracle."""
+    torch = torch_cuda
+    monkeypatch.setenv("NFFACL_TUNE_COARSE", coarse)
+    monkeypatch.setenv("NFFACL_TUNE_DIR8", dir8)
+    g = synth.gen_rules(synth.SPECS["c5"], synth.RULE_SEEDS["c5"])
+    rules, (a4, a6) = _rules_and_arrays(g.text)
+    n = (1 << 16) + 3
+    slots = synth.gen_slots(g, n, 31)
+    with nffacl.Engine(rules, algo=nffacl.ALGO_HYBRID) as eng:
+        p, b = classify(torch, eng, slots, 64, n)
+        want = oracle.classify_slots(slots, 64, n, a4, a6, threads=THREADS)
+        np.testing.assert_array_equal(p, want)
+        np.testing.assert_array_equal(b, permit_bits(want))
+        frames, desc = synth.gen_imix(g, 1 << 14, 32)
+        port = torch.zeros(1 << 14, dtype=torch.int32, device="cuda")
+        eng.classify_frames_device(to_dev(torch, frames), to_dev(torch, desc.view(np.int64)), 1 << 14, port)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(port.cpu().numpy().view(np.uint32),
+                                      oracle.classify_frames(frames, desc, a4, a6, threads=THREADS))
+
+
 @pytest.mark.parametrize("flat", [0, 1, 2])
 @pytest.mark.parametrize("dir_kb", [1, 16, 1024])
 def test_hybrid_directory_budgets(torch_cuda, monkeypatch, dir_kb, flat):

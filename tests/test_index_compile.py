@@ -421,6 +421,7 @@ def test_hybrid_policy_c5_flat(monkeypatch):
     info = check_hybrid(g.text, slots, n)
     assert 0 < info.lds_dwords * 4 <= 135 * 1024 and info.fam[0].entry_dwords == 6
     assert info.fam[0].dims[3].n_rules == 0  # sparse source-port slot folded away
+    assert info.fam[0].dims[0].dir8 == 1  # u8 two-level directories
     monkeypatch.setenv("NFFACL_TUNE_FLAT", "1")
     info = check_hybrid(g.text, slots, n)
     assert info.lds_dwords == 0 and info.fam[0].entry_dwords == 6
@@ -473,3 +474,23 @@ def test_hybrid_large_output_numbers(flat, monkeypatch):
     text = "\n".join(lines) + "\n"
     n = 1 << 13
     check_hybrid(text, synth.gen_slots(synth.gen_rules(synth.SPECS["c3"], synth.RULE_SEEDS["c3"]), n, 71), n)
+
+
+@pytest.mark.parametrize("coarse,dir8", [("1", "1"), ("1", "0"), ("0", "0")])
+def test_hybrid_c5_coarse_slots_and_directory_forms(coarse, dir8, monkeypatch):
+    """The flat-LDS layout knobs: coarse address slots for short prefixes on
+    or off, u8 or u16 two-level directories; every combination gives the
+    oracle's first match (the default, u8 without coarse slots, runs in
+    test_hybrid_policy_c5_flat)."""
+    g = synth.gen_rules(synth.SPECS["c5"], synth.RULE_SEEDS["c5"])
+    n = 1 << 12
+    slots = synth.gen_slots(g, n, synth.PACKET_SEEDS["c5"])
+    monkeypatch.setenv("NFFACL_TUNE_COARSE", coarse)
+    monkeypatch.setenv("NFFACL_TUNE_DIR8", dir8)
+    info = check_hybrid(g.text, slots, n)
+    assert info.fam[0].dims[0].dir8 == int(dir8)
+    kinds = [info.fam[0].dims[k].kind for k in range(info.fam[0].n_slots)]
+    if coarse == "1":  # compacted slots: the sport slot dropped, src (0) and dst (1) twice
+        assert 4 not in kinds and kinds.count(0) == 2 and kinds.count(1) == 2
+    else:
+        assert info.fam[0].n_slots == 4
