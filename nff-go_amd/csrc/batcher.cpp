@@ -56,7 +56,7 @@ void gen_wait(std::atomic<uint32_t> &g, uint32_t seen) {
 // The batch's verdicts are in (or it failed): release its spinning and its
 // sleeping waiters.
 void publish_done(BatchBuf &x) {
-    x.done_seq.store(x.seq, std::memory_order_release);
+    x.done_seq.store(x.seq.load(std::memory_order_relaxed), std::memory_order_release);
     x.gen.fetch_add(1, std::memory_order_release);
     (void)syscall(SYS_futex, reinterpret_cast<uint32_t *>(&x.gen), FUTEX_WAKE_PRIVATE, INT32_MAX, nullptr, nullptr, 0);
 }
@@ -249,7 +249,7 @@ int nffacl_batcher_submit(nffacl_batcher *b, const uint8_t *const *frames, const
         if (cur.state == BatchBuf::FREE) {
             cur.state = BatchBuf::OPEN;
             ++b->busy;
-            cur.seq = b->next_seq++;
+            cur.seq.store(b->next_seq++, std::memory_order_relaxed);
             cur.count = 0;
             cur.readers.store(0, std::memory_order_relaxed);
             cur.written.store(0, std::memory_order_relaxed);
@@ -267,7 +267,7 @@ int nffacl_batcher_submit(nffacl_batcher *b, const uint8_t *const *frames, const
         cur.count += n;
         cur.readers.fetch_add(1, std::memory_order_relaxed);
         ++b->bursts;
-        *ticket = nffacl_ticket{cur.seq, b->open_idx, off, n, 0};
+        *ticket = nffacl_ticket{cur.seq.load(std::memory_order_relaxed), b->open_idx, off, n, 0};
         if (cur.count == b->max_batch) seal_open(b);
         else if (off == 0) b->cv_work.notify_one();  // a batch to ship
         break;
@@ -298,10 +298,10 @@ int nffacl_batcher_wait(nffacl_batcher *b, const nffacl_ticket *t, uint32_t *por
         b->spinners.fetch_sub(1, std::memory_order_acq_rel);
     }
     if (!done()) {
-        {
-            std::lock_guard<std::mutex> g(b->mu);
-            if (x.seq != t->seq || x.state == BatchBuf::FREE) return NFFACL_ERR_INVALID_ARG;  // stale ticket
-        }
+        // stale ticket (its buffer was recycled): no mutex on this path — at
+        // 64 waiters per batch the lock convoy cost more than the wait; a
+        // buffer freed but not reopened still has done_seq == seq (done above)
+        if (x.seq.load(std::memory_order_acquire) != t->seq) return NFFACL_ERR_INVALID_ARG;
         while (true) {
             const uint32_t g = x.gen.load(std::memory_order_acquire);
             if (done()) break;

@@ -36,7 +36,9 @@ namespace nffacl {
 struct BatchBuf {
     enum State { FREE, OPEN, SEALED, LAUNCHED, DONE };
     State state = FREE;
-    uint64_t seq = 0;       // batch sequence number while not FREE
+    // batch sequence number (written under the batcher mutex when the buffer
+    // opens; waiters read it without the lock to reject stale tickets)
+    std::atomic<uint64_t> seq{0};
     uint32_t count = 0;     // packets reserved
     std::atomic<uint32_t> readers{0};  // bursts that have not collected their verdicts yet
     std::atomic<uint32_t> written{0};  // packets whose bytes are in h_slots
