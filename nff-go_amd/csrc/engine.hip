@@ -372,6 +372,7 @@ struct IndexedArgs {
     uint32_t stage_dwords;  // leading dwords staged in LDS (multiple of 4)
     uint32_t flags;         // NFFACL_PARSE_*
     uint32_t dir8;          // HYBRID: two-level directories carry u8 offsets (SplitTab::bounds)
+    uint32_t generic;       // HYBRID flat forms: slots key on SlotArgs::f1/f2 (else slot s on field s)
     FamArgs f4, f6;
 };
 
@@ -610,12 +611,20 @@ __device__ __forceinline__ uint32_t hyb_miss(const u32x3 &A, const u32x3 &B, uin
 
 // IPv6 address words 1..3 of an exact entry (C = src1 src2 src3, D = dst1
 // dst2 dst3) against big-endian packet words s[1..3], t[1..3].
+// By first difference: the address matches its prefix of length L iff its
+// first bit differing from the rule's (counted from bit 32) lies at or past
+// L - 32 (v_ffbh per word instead of three prefix masks per address).
+__device__ __forceinline__ uint32_t first_diff96(uint32_t x1, uint32_t x2, uint32_t x3) {
+    const uint32_t p1 = __clz(x1), p2 = 32u + __clz(x2), p3 = 64u + __clz(x3);  // __clz(0) = 32
+    return x1 != 0u ? p1 : x2 != 0u ? p2 : p3;
+}
+
 __device__ __forceinline__ uint32_t hyb_miss6(const u32x3 &C, const u32x3 &D, uint32_t lens, const uint32_t (&s)[4],
                                               const uint32_t (&t)[4]) {
-    const int sl = static_cast<int>(lens & 0xFFu), dl = static_cast<int>((lens >> 8) & 0xFFu);
-    auto pm = [](int L, int k) { return prefix_mask(static_cast<uint32_t>(min(max(L - 32 * k, 0), 32))); };
-    return ((s[1] ^ C.x) & pm(sl, 1)) | ((s[2] ^ C.y) & pm(sl, 2)) | ((s[3] ^ C.z) & pm(sl, 3)) |
-           ((t[1] ^ D.x) & pm(dl, 1)) | ((t[2] ^ D.y) & pm(dl, 2)) | ((t[3] ^ D.z) & pm(dl, 3));
+    const uint32_t sl = lens & 0xFFu, dl = (lens >> 8) & 0xFFu;
+    const uint32_t ps = 32u + first_diff96(s[1] ^ C.x, s[2] ^ C.y, s[3] ^ C.z);
+    const uint32_t pd = 32u + first_diff96(t[1] ^ D.x, t[2] ^ D.y, t[3] ^ D.z);
+    return (ps < sl ? 1u : 0u) | (pd < dl ? 1u : 0u);
 }
 
 // ---- FLAT: a wave's candidates, 64 at a time --------------------------------
@@ -635,7 +644,7 @@ __device__ __forceinline__ uint32_t hyb_miss6(const u32x3 &C, const u32x3 &D, ui
 // the first match of the ordered lists, no early exit needed.
 template <int R>
 struct FlatScratch {
-    uint32_t mark[64 * R];   // window position -> (list id << 8 | position) + 1, 0 = none
+    uint32_t mark[64 * R];   // window position -> (owner lane << 11 | slot << 8 | position) + 1, 0 = none
     uint32_t delta[64 * R];  // window position -> (entry number - candidate number) << 1 | IPv6
     uint64_t best[64];       // per packet (lane): lowest passing rule index << 32 | output code
 };
@@ -694,6 +703,20 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
     };
     // list bounds of this packet in every slot (family-relative entry numbers)
     uint32_t st[NS], ln[NS];
+    // positional slots (a.generic == 0: slot s keys on field s, 1-D): the key
+    // is known at compile time, no per-lane field selects (wave-uniform branch)
+    if (LDS_DIRS && a.generic == 0u) {
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            const SlotArgs &s4 = a.f4.slot[s], &s6 = a.f6.slot[s];
+            const uint32_t key = s == kFDst ? kd : s == kFSrc ? ks : s == kFDport ? dport : s == kFSport ? sport : 0u;
+            const uint32_t t = key >> (v6 ? s6.shift : s4.shift);
+            uint32_t hi;
+            SplitTab{a.tab}.bounds(v6 ? s6.off_dir : s4.off_dir, v6 ? s6.off_dir16 : s4.off_dir16, t, st[s], hi,
+                                   a.dir8 != 0u);
+            ln[s] = mine ? hi - st[s] : 0u;
+        }
+    } else {
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
         const SlotArgs &s4 = a.f4.slot[s], &s6 = a.f6.slot[s];
@@ -714,6 +737,7 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
                 ln[s] = a.tab[dir + t + 1] - st[s];
             }
         }
+    }
     }
     uint32_t total = 0;
 #pragma unroll
@@ -741,7 +765,7 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
         for (int s = 0; s < NS; ++s) {
             if (ln[s] != 0u && so < win + 64u * RR && so + ln[s] > win) {
                 const uint32_t pos = so > win ? so - win : 0u;
-                W.mark[pos] = (((lane * NS + s) << 8) | pos) + 1u;
+                W.mark[pos] = ((lane << 11 | static_cast<uint32_t>(s) << 8) | pos) + 1u;
                 W.delta[pos] = ((st[s] - so) << 1) | (v6 ? 1u : 0u);
             }
             so += ln[s];
@@ -763,7 +787,7 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
             if (j + 1 < RR) carry = __builtin_amdgcn_readlane(m, 63);
             const uint32_t k = win + 64u * j + lane;
             valid[j] = k < T;
-            owner[j] = ((m - 1u) >> 8) / NS;
+            owner[j] = (m - 1u) >> 11;
             const uint32_t dp = W.delta[(m - 1u) & 0xFFu];
             six[j] = (dp & 1u) != 0u;
             // UNCOND: lanes past the wave's candidates load entry 0 of the
@@ -1128,6 +1152,7 @@ static dev::IndexedArgs indexed_args(const DevTable *t) {
     const bool hyb = t->meta.algo == NFFACL_ALGO_HYBRID;
     a.stage_dwords = hyb ? t->meta.lds_dwords : static_cast<uint32_t>(t->meta.blob.size());
     a.dir8 = hyb ? t->meta.dir8 : 0u;
+    a.generic = t->meta.slots_g ? 1u : 0u;
     auto fam = [&](const FamilyIndex &fi, uint32_t off_cold, dev::FamArgs &fa) {
         for (uint32_t k = 0; k < kMaxSlots; ++k) {
             const DimInfo &d = fi.dims[k];
