@@ -80,7 +80,11 @@ struct Fields {
 // frame whose EtherType is 0x8100 has its L3 header 4 bytes (one dword) later
 // and the tag's EtherType decides the family, so a tagged lane shifts d[3..14]
 // down by one dword and parses as usual (d[15] is never read afterwards).
-template <class FarDwords>
+// REG_OPTS (frames kernels): ports that lie inside the 64 bytes in registers
+// (IHL <= 11, untagged) come from them through a select chain, so only lanes
+// whose ports lie past byte 64 read memory — most waves of C3 have some lane
+// with options, and its dependent far read stalled the whole wave.
+template <bool REG_OPTS = false, class FarDwords>
 __device__ __forceinline__ void parse_fields(uint32_t (&d)[16], bool live, Fields &f, FarDwords far,
                                              uint32_t flags) {
     const bool vlan = (flags & NFFACL_PARSE_VLAN) != 0;
@@ -101,7 +105,25 @@ __device__ __forceinline__ void parse_fields(uint32_t (&d)[16], bool live, Field
     // IPv6: proto byte 20, src 22..37, dst 38..53, L4 at 54 (packet.go:283-285)
     const uint32_t ihl = (d[3] >> 16) & 0xFu;
     uint32_t pw = f.is6 ? funnel16(d[14], d[13]) : funnel16(d[9], d[8]);
-    if (f.is4 && ihl != 5u) {
+    if (REG_OPTS) {
+        const bool opt = f.is4 && ihl != 5u;
+        if (ballot(opt)) {
+            // in the (VLAN-shifted) registers the L4 dword is 3 + IHL; valid
+            // through d[15] untagged, d[14] tagged (d[15] is stale there)
+            const uint32_t k = 3u + ihl, lim = 15u - (l3dw - 3u);
+            uint32_t lo = 0, hi = 0;
+#pragma unroll
+            for (uint32_t j = 8; j <= 14; ++j) {
+                lo = k == j ? d[j] : lo;
+                hi = k == j ? d[j + 1] : hi;
+            }
+            if (opt) pw = funnel16(hi, lo);
+            if (opt && (k + 1u > lim || k < 8u)) {  // past the registers, or a malformed IHL < 5
+                far(l3dw + ihl, lo, hi);
+                pw = funnel16(hi, lo);
+            }
+        }
+    } else if (f.is4 && ihl != 5u) {
         // L4 bytes L3+4*IHL .. +3 = dword l3dw+IHL, byte 2.  (Taking IHL <= 11
         // from the registers instead, through a select chain, measured 2.6 %
         // slower on C2 and 1 % faster on C5 in one-process A/B: memory.)
@@ -1024,7 +1046,7 @@ k_indexed_frames(const uint8_t *__restrict__ frames, const uint64_t *__restrict_
         // the clip is skipped unless some lane of the wave holds a shorter one
         if (ballot(live && len < 64u)) clip16(d, len);
         Fields f;
-        parse_fields(d, live, f, [&](uint32_t k, uint32_t &lo, uint32_t &hi) {
+        parse_fields<true>(d, live, f, [&](uint32_t k, uint32_t &lo, uint32_t &hi) {
             far_dwords(pkt, len, k, lo, hi);
         }, a.flags);
         const uint32_t res = classify_any<NS, TM>(a, f);

@@ -215,6 +215,47 @@ def test_ip_options_and_wide_slots(torch_cuda, algo):
 
 
 @pytest.mark.parametrize("algo", ALGOS)
+def test_ip_options_frames_vlan(torch_cuda, algo):
+    """IHL 0..15 on packed frames (the frames kernels take ports inside the
+    first 64 bytes from registers and read memory only past them), untagged
+    and 802.1Q-tagged, frame lengths 128 / 80 / 64 / 61 / 40 (bytes past the
+    length read as 0), with and without NFFACL_PARSE_VLAN."""
+    torch = torch_cuda
+    rng = np.random.default_rng(13)
+    n = 4099
+    lens = [128, 80, 64, 61, 40]
+    buf, desc, off = [], [], 0
+    for i in range(n):
+        ihl = i % 16
+        f = bytearray(rng.integers(0, 256, 132, dtype=np.uint8).tobytes())
+        f[12:14] = b"\x08\x00"
+        f[14] = 0x40 | ihl
+        f[23] = [6, 17, 1][i % 3]
+        if (i // 16) % 2:  # tagged: TPID 0x8100 + TCI, the header 4 bytes later
+            f = f[:12] + bytearray(b"\x81\x00\x00\x05") + f[12:128]
+        ln = lens[(i // 32) % len(lens)]
+        room = (ln + 63) // 64 * 64
+        buf.append(bytes(f[:ln]) + bytes(room - ln))
+        desc.append(off << 16 | ln)
+        off += room
+    frames = np.frombuffer(b"".join(buf), np.uint8).copy()
+    desc = np.array(desc, np.uint64)
+    text = "\n".join(f"ANY ANY {p} {a}:{b} {c}:{d} {o}" for p, a, b, c, d, o in [
+        ("TCP", 0, 30000, 0, 65535, 2), ("UDP", 20000, 65535, 100, 40000, 3), ("ANY", 0, 0, 0, 65535, 4),
+        ("ANY", 0, 65535, 0, 0, 5), ("ANY", 1000, 50000, 1000, 50000, 6)]) + "\n"
+    rules, (a4, a6) = _rules_and_arrays(text)
+    d_frames, d_desc = to_dev(torch, frames), to_dev(torch, desc.view(np.int64))
+    with nffacl.Engine(rules, algo=algo) as eng:
+        for flags in (0, nffacl.PARSE_VLAN):
+            port = torch.zeros(n, dtype=torch.int32, device="cuda")
+            eng.classify_frames_device(d_frames, d_desc, n, port, None, None, flags)
+            torch.cuda.synchronize()
+            want = oracle.classify_frames(frames, desc, a4, a6, flags=flags)
+            np.testing.assert_array_equal(port.cpu().numpy().view(np.uint32), want)
+            assert len(set(want.tolist())) > 3
+
+
+@pytest.mark.parametrize("algo", ALGOS)
 @pytest.mark.parametrize("n", [1, 63, 64, 65, 1000])
 def test_ragged_sizes(torch_cuda, algo, n):
     g = synth.gen_rules(synth.RuleSpec(300), 11)
