@@ -934,10 +934,11 @@ void build_hybrid(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vec
         size_and_fill(all, weight, budget, fmt);
         out.flat_uncond = 1;
     }
-    // 4 rounds of candidate loads in flight whenever their scratch fits beside
-    // the directories (indexed_launch checks; exact entries, C3: 0.507 vs
-    // 0.540 ms at 2 rounds, profiles/r2_exact/)
-    if (flat && lds_dirs) out.flat_rounds = 4;
+    // 4 rounds of candidate loads in flight for tables with many candidates
+    // per packet, else 2: with the last window's rounds adaptive, C3 (1.45
+    // candidates) runs 0.469 vs 0.473 ms at 2 (profiles/r2_valu/pfab/; round 1
+    // measured 4 faster, 0.507 vs 0.540, before adaptive rounds)
+    if (flat && lds_dirs) out.flat_rounds = expect > kHybFlat4Candidates ? 4 : 2;
     if (flat && lds_dirs && opt.uncond >= 0) out.flat_uncond = static_cast<uint32_t>(opt.uncond);
     // Coarse address slots (flat-LDS): a rule whose prefix is shorter than
     // its address slot's radix is replicated into 2^(radix - length) buckets

@@ -1059,6 +1059,9 @@ k_indexed_frames(const uint8_t *__restrict__ frames, const uint64_t *__restrict_
     // other of two register buffers (ping-pong, no copies), and the
     // descriptors of the batch after.
     constexpr bool PF = TM == kTabSplit;  // (flat-LDS: +0.6 % on C3, profiles/r1_flat_lds/cold/)
+    // (flat-LDS, round 2: one prefetch buffer with copies, 2 rounds — 124
+    // VGPRs, no spill — ran 0.487 vs 0.469 ms on C3: the frame loads are not
+    // what the walk waits on; profiles/r2_valu/pfab/)
     // Frame lines load cooperatively (load_frames_rs) and are assembled per
     // lane just before their batch is classified.
     auto run_batch = [&](uint64_t b, uint64_t ds, const u32x4(&v)[4]) {
