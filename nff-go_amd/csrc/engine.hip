@@ -1009,7 +1009,11 @@ k_indexed_slots(const uint8_t *__restrict__ slots, uint32_t stride, uint64_t n, 
             if (nb < n) load16(slots + (nb + lane < n ? nb + lane : 0) * stride, d);  // prefetch
         }
         Fields f;
-        parse_fields(cur, live, f, [&](uint32_t k, uint32_t &lo, uint32_t &hi) {
+        // HYBRID walks: option ports from registers (as the frames kernels);
+        // the streaming INDEXED kernel (C2) keeps the divergent far read
+        // (the select chain cost it 2.6 %, round 1)
+        constexpr bool REG = TM == kTabFlatLds || TM == kTabFlatLds4 || TM == kTabFlatLds4U;
+        parse_fields<REG>(cur, live, f, [&](uint32_t k, uint32_t &lo, uint32_t &hi) {
             far_dwords(pkt, stride, k, lo, hi);
         }, a.flags);
         const uint32_t res = classify_any<NS, TM>(a, f);
