@@ -802,10 +802,16 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
         uint32_t owner[RR], idx[RR];
         bool valid[RR], six[RR];
         u32x3 A[RR], B[RR], C[RR], D[RR];
+        // the rounds' prefix-max scans are independent (only their carries
+        // chain): issued together, their DPP steps interleave instead of
+        // waiting out each other's data hazards
+        uint32_t scan[RR];
+#pragma unroll
+        for (int j = 0; j < RR; ++j) scan[j] = wave_incl_max(W.mark[64 * j + lane]);
         uint32_t carry = 0;
 #pragma unroll
         for (int j = 0; j < RR; ++j) {
-            const uint32_t m = max(wave_incl_max(W.mark[64 * j + lane]), carry);
+            const uint32_t m = max(scan[j], carry);
             if (j + 1 < RR) carry = __builtin_amdgcn_readlane(m, 63);
             const uint32_t k = win + 64u * j + lane;
             valid[j] = k < T;
