@@ -5,7 +5,7 @@
  * Every entry point is plain C: pointers, sizes and integer status codes; no
  * HIP, torch or C++ types cross this boundary (a HIP stream is passed as
  * `void*`).  A Go cgo package, a Python ctypes binding and the C++ host mirror
- * (nff-go_amd/csrc/host_api.hpp) all bind exactly these symbols.
+ * (nff-go_amd/host/nffgo.hpp) all bind exactly these symbols.
  *
  * Reference interfaces replaced (paths relative to aregm/nff-go):
  *   nffacl_rules_load_text      <- packet.GetL3ACLFromTextTable   packet/acl.go:148-178
@@ -62,7 +62,7 @@
 extern "C" {
 #endif
 
-#define NFFACL_ABI_VERSION 3
+#define NFFACL_ABI_VERSION 4
 
 /* Only the entry points below are exported from libnffacl.so (built with
  * -fvisibility=hidden). */
@@ -86,7 +86,8 @@ enum nffacl_status {
     NFFACL_ERR_NOMEM = -101,
     NFFACL_ERR_HIP = -102,
     NFFACL_ERR_NO_DEVICE = -103,
-    NFFACL_ERR_UNSUPPORTED = -104
+    NFFACL_ERR_UNSUPPORTED = -104,
+    NFFACL_ERR_TIMEOUT = -105    /* a bounded wait ran out (the work may still complete) */
 };
 
 /* ---- rule records (internal representation of acl.go:423-449) --------- */
@@ -150,6 +151,21 @@ NFFACL_API void nffacl_rules_free(nffacl_rules *rules);
 NFFACL_API int nffacl_rules_counts(const nffacl_rules *rules, size_t *n4, size_t *n6);
 NFFACL_API int nffacl_rules_get4(const nffacl_rules *rules, size_t i, nffacl_rule4 *out);
 NFFACL_API int nffacl_rules_get6(const nffacl_rules *rules, size_t i, nffacl_rule6 *out);
+
+/* Compile `rules` for HIP device `hip_device` and upload the table now; the
+ * calls that take a rule set per call (nffacl_service_classify,
+ * nffacl_batcher_submit_rules) otherwise do this on first use.  The table
+ * belongs to the rule set: nffacl_rules_free retires it (stream-ordered
+ * behind the work that used it).  This is what makes the reference's rule
+ * reload — build a new *L3Rules, swap the pointer (examples/tutorial/
+ * step08.go:38-44) — work unchanged: every call classifies against exactly
+ * the rule set it was given.  A rule set must outlive the calls using it. */
+NFFACL_API int nffacl_rules_prepare(const nffacl_rules *rules, int hip_device);
+
+/* The HIP device on the calling thread's NUMA node (the GPU a flow-function
+ * clone pinned to that node should use; device 0 when none matches), or
+ * NFFACL_ERR_NO_DEVICE.  Replaces the binding's former hard-wired GPU 0. */
+NFFACL_API int nffacl_local_device(void);
 
 /* ---- engine ------------------------------------------------------------ */
 
@@ -274,22 +290,25 @@ NFFACL_API int nffacl_classify_host_ex(nffacl_engine *eng, const uint8_t *h_slot
 /* ---- burst aggregator (host ingest) ----------------
  *
  * Many threads (the reference's flow-function clones, each with a burst of
- * <= 32 packets, or single packets from a SetSeparator-style scalar call)
- * submit bursts; the library copies each packet's first `stride` bytes into a
- * shared pinned slot ring and ships the open batch as soon as fewer than two
- * batches are on the GPU — so batches grow while the GPU is busy, up to
- * `max_batch` packets — and every submitter of that batch spins until its
- * verdicts are back.  `max_delay_us` bounds how long a batch waits behind a
- * full pipeline before it takes a further stream.  Thread-safe: any number of
- * concurrent submitters per batcher.  Every ticket must be waited for (its
- * batch buffer is reused only then); tickets not yet waited for may hold up
- * to (nbuf - 1) * max_batch packets before submit blocks for a buffer.
+ * <= 32 packets) submit bursts; the library copies each packet's first
+ * `stride` bytes into a shared pinned slot ring and ships the open batch as
+ * soon as fewer than two batches are on the GPU — so batches grow while the
+ * GPU is busy, up to `max_batch` packets — and every submitter of that batch
+ * sleeps until its verdicts are back.  A batch whose first burst has waited
+ * `max_delay_us` ships whatever else is in flight.  Thread-safe: any number of
+ * concurrent submitters per batcher.  Every ticket must be waited for exactly
+ * once (its batch buffer is reused only then); tickets not yet waited for may
+ * hold up to (nbuf - 1) * max_batch packets before submit blocks for a buffer.
+ * Each batch carries its own status: a failed launch fails the bursts of that
+ * batch only.  A batch classifies against one table — the engine's active
+ * table, or the rule set a burst was submitted with (nffacl_batcher_*_rules):
+ * bursts for different rule sets never share a batch.
  */
 typedef struct nffacl_batcher nffacl_batcher;
 
 typedef struct nffacl_ticket {
     uint64_t seq;
-    uint32_t buf, off, n, reserved;
+    uint32_t buf, off, n, reserved;  /* reserved: the burst's number in its batch */
 } nffacl_ticket;
 
 typedef struct nffacl_batcher_stats {
@@ -304,21 +323,80 @@ typedef struct nffacl_batcher_stats {
  * rotation (>= 2).  The engine must outlive the batcher. */
 NFFACL_API int nffacl_batcher_create(nffacl_engine *eng, uint32_t stride, uint32_t max_batch,
                                      uint32_t max_delay_us, uint32_t nbuf, nffacl_batcher **out);
+/* A batcher of HIP device `hip_device` with no engine: every burst names its
+ * rule set (nffacl_batcher_submit_rules / _classify_rules), the binding's
+ * shape for the reference's per-call *L3Rules (examples/tutorial/step08.go:
+ * 33-44: clones load the current pointer, a reload goroutine stores a new
+ * one). */
+NFFACL_API int nffacl_batcher_create_device(int hip_device, uint32_t stride, uint32_t max_batch,
+                                            uint32_t max_delay_us, uint32_t nbuf, nffacl_batcher **out);
 /* Queue a burst: frames[i] points at packet i's Ether header, lens[i] its
  * bytes (NULL lens: `stride` bytes each; bytes past a length read as 0).
- * n <= max_batch.  Returns without waiting; *ticket identifies the burst. */
+ * n <= max_batch.  Returns without waiting; *ticket identifies the burst.
+ * Engine batchers only (the engine's active table at launch). */
 NFFACL_API int nffacl_batcher_submit(nffacl_batcher *b, const uint8_t *const *frames, const uint32_t *lens,
                                      uint32_t n, nffacl_ticket *ticket);
-/* Block until the burst's batch is classified; ports[i] <- L3ACLPort of packet i. */
+/* The same against `rules` (its own table on the batcher's device, compiled
+ * on first use; nffacl_rules_prepare).  `rules` must outlive the wait. */
+NFFACL_API int nffacl_batcher_submit_rules(nffacl_batcher *b, const nffacl_rules *rules,
+                                           const uint8_t *const *frames, const uint32_t *lens, uint32_t n,
+                                           nffacl_ticket *ticket);
+/* Block until the burst's batch is classified; ports[i] <- L3ACLPort of packet
+ * i.  Returns the batch's status; a second wait on a ticket is rejected. */
 NFFACL_API int nffacl_batcher_wait(nffacl_batcher *b, const nffacl_ticket *ticket, uint32_t *ports);
+/* The same, giving up after timeout_us: NFFACL_ERR_TIMEOUT means the batch is
+ * not done yet (shipped or not) — no verdict, and the ticket stays valid: wait
+ * on it again. */
+NFFACL_API int nffacl_batcher_wait_timeout(nffacl_batcher *b, const nffacl_ticket *ticket, uint32_t *ports,
+                                           uint64_t timeout_us);
 /* submit + wait: the body of a VectorSeparateFunction. */
 NFFACL_API int nffacl_batcher_classify(nffacl_batcher *b, const uint8_t *const *frames, const uint32_t *lens,
                                        uint32_t n, uint32_t *ports);
+NFFACL_API int nffacl_batcher_classify_rules(nffacl_batcher *b, const nffacl_rules *rules,
+                                             const uint8_t *const *frames, const uint32_t *lens, uint32_t n,
+                                             uint32_t *ports);
 /* Ship the currently open batch now (do not wait for max_batch / max_delay_us). */
 NFFACL_API int nffacl_batcher_flush(nffacl_batcher *b);
 NFFACL_API int nffacl_batcher_get_stats(nffacl_batcher *b, nffacl_batcher_stats *out);
-/* Drains queued bursts, then frees; no submit/wait may be running. */
+/* Ships queued bursts, waits for the batches in flight, then frees; no
+ * submit/wait may be running. */
 NFFACL_API void nffacl_batcher_destroy(nffacl_batcher *b);
+
+/* ---- scalar calls: persistent GPU consumer ------------------------------
+ *
+ * (*Packet).L3ACLPort / L3ACLPermit (acl.go:495-506) called ONE packet at a
+ * time, the shape of every SetSeparator / SetSplitter user function
+ * (flow/flow.go:128, 1795-1797; examples/firewall/firewall.go:54-57;
+ * examples/tutorial/step08.go:33-35).  A service keeps one small kernel
+ * resident on its GPU that polls per-thread mailboxes in pinned host memory:
+ * a call writes its packet's first 80 bytes into the calling thread's
+ * mailbox and spins until the kernel has written the verdict back — no
+ * kernel launch, no driver call per packet.  The kernel exits after
+ * `idle_us` without calls (and every 100 ms) and is re-armed by the next
+ * call.  Thread-safe; one service per GPU serves every thread.
+ */
+typedef struct nffacl_service nffacl_service;
+
+typedef struct nffacl_service_stats {
+    uint64_t launches;  /* consumer kernel launches (re-arms) */
+    uint64_t requests;  /* calls answered */
+    uint64_t timeouts;  /* calls that returned NFFACL_ERR_TIMEOUT */
+    uint64_t running;   /* 1 while the consumer kernel is resident */
+} nffacl_service_stats;
+
+/* mailboxes: a multiple of 64 (one wave each 64; 0 = 128), one per calling
+ * thread (threads beyond that share mailboxes under a lock);
+ * idle_us: consumer lifetime without calls (0 = 2000). */
+NFFACL_API int nffacl_service_create(int hip_device, uint32_t mailboxes, uint32_t idle_us, nffacl_service **out);
+/* L3ACLPort of one packet: frame = its Ether header, len its bytes (bytes past
+ * len, and past 80, read as 0 — the batcher's 80-byte slot); flags:
+ * enum nffacl_parse_flags.  *port <- the verdict (permit = port > 0).  Blocks
+ * about one PCIe round trip; NFFACL_ERR_TIMEOUT after 1 s without an answer. */
+NFFACL_API int nffacl_service_classify(nffacl_service *svc, const nffacl_rules *rules, const uint8_t *frame,
+                                       uint32_t len, uint32_t flags, uint32_t *port);
+NFFACL_API int nffacl_service_get_stats(nffacl_service *svc, nffacl_service_stats *out);
+/* Stops the consumer and frees; no call may be running. */
+NFFACL_API void nffacl_service_destroy(nffacl_service *svc);
 
 /* ---- L2 ACL (packet/acl.go:68-117, 356-383, 413-421, 457-491) ----------- */
 

@@ -110,7 +110,7 @@ bool range_is_pinned(const void *p, size_t bytes) {
     size_t size = 0;
     if (hipMemGetAddressRange(&base, &size, a.devicePointer) != hipSuccess) {
         (void)hipGetLastError();
-        return true;  // the runtime does not track host ranges: the endpoint checks above stand
+        return false;  // the range cannot be confirmed as ONE allocation: stage it
     }
     const uintptr_t lo = reinterpret_cast<uintptr_t>(base);
     return da >= lo && db < lo + size;
@@ -139,6 +139,7 @@ const char *nffacl_strerror(int s) {
     case NFFACL_ERR_HIP: return "HIP runtime error";
     case NFFACL_ERR_NO_DEVICE: return "no HIP device";
     case NFFACL_ERR_UNSUPPORTED: return "unsupported";
+    case NFFACL_ERR_TIMEOUT: return "timed out";
     default: return "unknown status";
     }
 }
@@ -174,7 +175,11 @@ int nffacl_rules_from_arrays(const nffacl_rule4 *r4, size_t n4, const nffacl_rul
     return NFFACL_OK;
 }
 
-void nffacl_rules_free(nffacl_rules *rules) { delete rules; }
+void nffacl_rules_free(nffacl_rules *rules) {
+    if (!rules) return;
+    release_rules_tables(rules);  // its device tables retire behind the work that used them
+    delete rules;
+}
 
 int nffacl_rules_counts(const nffacl_rules *rules, size_t *n4, size_t *n6) {
     if (!rules) return NFFACL_ERR_INVALID_ARG;
@@ -241,8 +246,11 @@ int nffacl_table_compile(const nffacl_rules *rules, int algo, uint32_t *blob, ui
 
 // ---- engine ----------------------------------------------------------------
 
-int nffacl_engine_create_ex(int hip_device, const nffacl_rules *rules, int algo, nffacl_engine **out) {
-    if (!rules || !out) return NFFACL_ERR_INVALID_ARG;
+}  // extern "C"
+
+namespace nffacl {
+
+int engine_shell(int hip_device, nffacl_engine **out) {
     *out = nullptr;
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
@@ -257,7 +265,6 @@ int nffacl_engine_create_ex(int hip_device, const nffacl_rules *rules, int algo,
     nffacl_engine *eng = new (std::nothrow) nffacl_engine();
     if (!eng) return NFFACL_ERR_NOMEM;
     eng->device = hip_device;
-    eng->algo_req = algo;
     std::string terr;
     if (!Tune::from_env(eng->tune, terr)) {  // read once; never on the launch path
         set_last_error("tuning knob: " + terr);
@@ -273,9 +280,24 @@ int nffacl_engine_create_ex(int hip_device, const nffacl_rules *rules, int algo,
         delete eng;
         return NFFACL_ERR_HIP;
     }
-    int st = upload_table(eng, *rules, eng->active);
+    *out = eng;
+    return NFFACL_OK;
+}
+
+}  // namespace nffacl
+
+extern "C" {
+
+int nffacl_engine_create_ex(int hip_device, const nffacl_rules *rules, int algo, nffacl_engine **out) {
+    if (!rules || !out) return NFFACL_ERR_INVALID_ARG;
+    *out = nullptr;
+    nffacl_engine *eng = nullptr;
+    int st = engine_shell(hip_device, &eng);
+    if (st != NFFACL_OK) return st;
+    eng->algo_req = algo;
+    st = upload_table(eng, *rules, eng->active);
     if (st != NFFACL_OK) {
-        delete eng;
+        nffacl_engine_destroy(eng);
         return st;
     }
     *out = eng;

@@ -1,0 +1,865 @@
+// classify.hpp — device-side parse + match helpers of libnffacl (internal),
+// shared by the batch kernels (engine.hip) and the persistent scalar-call
+// consumer (service.hip).  See engine.hip for the execution model.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <type_traits>
+
+#include "devutil.hpp"
+#include "nffacl.h"
+#include "table.hpp"
+
+namespace nffacl {
+namespace dev {
+
+__device__ __forceinline__ uint32_t funnel16(uint32_t hi, uint32_t lo) {
+    // ({hi,lo} >> 16)[31:0] : wire bytes 4k+2 .. 4k+5 as a LE dword
+    return __builtin_amdgcn_alignbit(hi, lo, 16);
+}
+
+// Byte-swap each 16-bit half: LE dword of wire bytes [p0 p1 p2 p3] ->
+// (p0<<8|p1) | (p2<<8|p3) << 16 = sport | dport << 16 (SwapBytesUint16,
+// packet/packet.go:713-715, applied by l4ACL acl.go:511, 515).
+__device__ __forceinline__ uint32_t swap_halves(uint32_t w) {
+    return ((w & 0x00FF00FFu) << 8) | ((w >> 8) & 0x00FF00FFu);
+}
+
+// Non-zero iff some port of `ports` (sport | dport << 16) is outside
+// [lo, hi] per half (l4ACL, acl.go:512-518).
+__device__ __forceinline__ uint32_t port_miss(uint32_t ports, uint32_t lo, uint32_t hi) {
+    u16x2 p = __builtin_bit_cast(u16x2, ports);
+    u16x2 l = __builtin_bit_cast(u16x2, lo);
+    u16x2 h = __builtin_bit_cast(u16x2, hi);
+    u16x2 c = __builtin_elementwise_min(__builtin_elementwise_max(p, l), h);
+    return __builtin_bit_cast(uint32_t, c) ^ ports;
+}
+
+// Header fields of one packet (Appendix A of SURVEY.md).
+struct Fields {
+    bool is4, is6;
+    uint32_t proto;
+    uint32_t ports;     // sport | dport << 16 (host order)
+    uint32_t s[4], t[4];  // src / dst words (IPv4 uses [0])
+};
+
+// Parse the header fields from the first 64 bytes (d[0..15]) of a packet.
+// `far(k)` returns the little-endian dwords k and k+1 of the packet (bytes past
+// the slot/frame end as 0) for the rare IPv4 header whose IHL != 5 puts the L4
+// ports somewhere other than bytes 34..37; it runs in a divergent branch that
+// only lanes with IP options take.
+// `vlan` (wave-uniform launch flag NFFACL_PARSE_VLAN) selects
+// ParseAllKnownL3CheckVLAN (packet/vlan.go:104-117) over ParseAllKnownL3: a
+// frame whose EtherType is 0x8100 has its L3 header 4 bytes (one dword) later
+// and the tag's EtherType decides the family, so a tagged lane shifts d[3..14]
+// down by one dword and parses as usual (d[15] is never read afterwards).
+// REG_OPTS (frames kernels): ports that lie inside the 64 bytes in registers
+// (IHL <= 11, untagged) come from them through a select chain, so only lanes
+// whose ports lie past byte 64 read memory — most waves of C3 have some lane
+// with options, and its dependent far read stalled the whole wave.
+template <bool REG_OPTS = false, class FarDwords>
+__device__ __forceinline__ void parse_fields(uint32_t (&d)[16], bool live, Fields &f, FarDwords far,
+                                             uint32_t flags) {
+    const bool vlan = (flags & NFFACL_PARSE_VLAN) != 0;
+    uint32_t l3dw = 3u;  // dword holding the first L3 byte (at byte 2 of it)
+    if (vlan) {
+        const bool tagged = (d[3] & 0xFFFFu) == 0x0081u;  // 0x8100 on the wire
+        if (ballot(tagged)) {
+#pragma unroll
+            for (int k = 3; k < 15; ++k) d[k] = tagged ? d[k + 1] : d[k];
+            l3dw = tagged ? 4u : 3u;
+        }
+    }
+    // ParseAllKnownL3: EtherType at wire bytes 12-13 (packet.go:238-243, 264-269)
+    const uint32_t et = d[3] & 0xFFFFu;
+    f.is4 = live && et == 0x0008u;  // 0x0800 on the wire
+    f.is6 = live && et == 0xDD86u;  // 0x86DD on the wire
+    // IPv4: proto byte 23, src 26..29, dst 30..33, L4 at 14 + 4*IHL (packet.go:278-280)
+    // IPv6: proto byte 20, src 22..37, dst 38..53, L4 at 54 (packet.go:283-285)
+    const uint32_t ihl = (d[3] >> 16) & 0xFu;
+    uint32_t pw = f.is6 ? funnel16(d[14], d[13]) : funnel16(d[9], d[8]);
+    if (REG_OPTS) {
+        const bool opt = f.is4 && ihl != 5u;
+        if (ballot(opt)) {
+            // in the (VLAN-shifted) registers the L4 dword is 3 + IHL; valid
+            // through d[15] untagged, d[14] tagged (d[15] is stale there)
+            const uint32_t k = 3u + ihl, lim = 15u - (l3dw - 3u);
+            uint32_t lo = 0, hi = 0;
+#pragma unroll
+            for (uint32_t j = 8; j <= 14; ++j) {
+                lo = k == j ? d[j] : lo;
+                hi = k == j ? d[j + 1] : hi;
+            }
+            if (opt) pw = funnel16(hi, lo);
+            if (opt && (k + 1u > lim || k < 8u)) {  // past the registers, or a malformed IHL < 5
+                far(l3dw + ihl, lo, hi);
+                pw = funnel16(hi, lo);
+            }
+        }
+    } else if (f.is4 && ihl != 5u) {
+        // L4 bytes L3+4*IHL .. +3 = dword l3dw+IHL, byte 2.  (Taking IHL <= 11
+        // from the registers instead, through a select chain, measured 2.6 %
+        // slower on C2 and 1 % faster on C5 in one-process A/B: memory.)
+        uint32_t lo, hi;
+        far(l3dw + ihl, lo, hi);
+        pw = funnel16(hi, lo);
+    }
+    f.ports = swap_halves(pw);
+    f.proto = f.is6 ? (d[5] & 0xFFu) : (d[5] >> 24);
+    if (f.is6) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            f.s[k] = funnel16(d[6 + k], d[5 + k]);
+            f.t[k] = funnel16(d[10 + k], d[9 + k]);
+        }
+    } else {
+        f.s[0] = funnel16(d[7], d[6]);
+        f.t[0] = funnel16(d[8], d[7]);
+#pragma unroll
+        for (int k = 1; k < 4; ++k) { f.s[k] = 0; f.t[k] = 0; }
+    }
+}
+
+// Dwords k and k+1 of a packet whose readable, zero-padded extent is `lim`
+// bytes from `base` (4-byte aligned); bytes at or past `lim` read as 0.
+__device__ __forceinline__ void far_dwords(const uint8_t *base, uint32_t lim, uint32_t k,
+                                           uint32_t &lo, uint32_t &hi) {
+    const uint32_t *p = reinterpret_cast<const uint32_t *>(base);
+    auto masked = [&](uint32_t j) -> uint32_t {
+        const int rem = static_cast<int>(lim) - static_cast<int>(4 * j);
+        if (rem <= 0) return 0u;
+        const uint32_t v = p[j];
+        return rem >= 4 ? v : (v & ((1u << (8 * rem)) - 1u));
+    };
+    lo = masked(k);
+    hi = masked(k + 1);
+}
+
+// LINEAR: first-match scan in rule order, wave-uniform records.
+__device__ __forceinline__ uint32_t classify_linear(const Fields &f,
+                                                     const uint32_t *__restrict__ rec4, uint32_t n4,
+                                                     const uint32_t *__restrict__ rec6, uint32_t n6) {
+    uint32_t res = 0;
+    bool pend = f.is4;
+    if (ballot(pend)) {
+        for (uint32_t r = 0; r < n4; ++r) {
+            const uint32_t *R = rec4 + r * kRec4Dwords;
+            uint32_t m = ((f.s[0] ^ R[0]) & R[1]) | ((f.t[0] ^ R[2]) & R[3]);
+            const uint32_t meta = R[4];
+            const uint32_t idm = (meta >> 8) & 0xFFu;
+            if (idm) m |= (f.proto ^ meta) & idm;
+            if (meta & kMetaPortCheck) m |= port_miss(f.ports, R[5], R[6]);
+            const bool take = pend && m == 0u;
+            if (ballot(take)) {
+                if (take) { res = R[7]; pend = false; }
+                if (!ballot(pend)) break;
+            }
+        }
+    }
+    pend = f.is6;
+    if (ballot(pend)) {
+        for (uint32_t r = 0; r < n6; ++r) {
+            const uint32_t *R = rec6 + r * kRec6Dwords;
+            uint32_t m = ((f.s[0] ^ R[0]) & R[4]) | ((f.s[1] ^ R[1]) & R[5]) |
+                         ((f.s[2] ^ R[2]) & R[6]) | ((f.s[3] ^ R[3]) & R[7]) |
+                         ((f.t[0] ^ R[8]) & R[12]) | ((f.t[1] ^ R[9]) & R[13]) |
+                         ((f.t[2] ^ R[10]) & R[14]) | ((f.t[3] ^ R[11]) & R[15]);
+            const uint32_t meta = R[16];
+            const uint32_t idm = (meta >> 8) & 0xFFu;
+            if (idm) m |= (f.proto ^ meta) & idm;
+            if (meta & kMetaPortCheck) m |= port_miss(f.ports, R[17], R[18]);
+            const bool take = pend && m == 0u;
+            if (ballot(take)) {
+                if (take) { res = R[19]; pend = false; }
+                if (!ballot(pend)) break;
+            }
+        }
+    }
+    return res;
+}
+
+// Dense slots: packet i at slots + i*stride; the first 64 bytes are loaded
+// with four 16-byte loads.  Plain loads, not non-temporal: with one lane per
+// 64-byte row every cache line is consumed by four successive instructions,
+// and the nt policy cost 30% of stream bandwidth on this pattern
+// (profiles/r1_sol/sol.out: rows 5.26 TB/s vs rows_nt 3.66 TB/s).
+__device__ __forceinline__ void load16(const uint8_t *__restrict__ p, uint32_t (&d)[16]) {
+    const u32x4 *q = reinterpret_cast<const u32x4 *>(p);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const u32x4 v = q[j];
+        d[4 * j + 0] = v.x;
+        d[4 * j + 1] = v.y;
+        d[4 * j + 2] = v.z;
+        d[4 * j + 3] = v.w;
+    }
+}
+
+// ---- lane-contiguous ("coalesced") batch load for 64-byte slots ------------
+//
+// A wave's 64 packets are 4 KiB contiguous.  Instruction j loads KiB j with
+// lane l taking 16 bytes: packet 16j + l/4, chunk l%4 — every instruction
+// reads 1 KiB contiguous (the fastest HBM pattern measured: sol `coalesced`
+// 5.9 TB/s vs 5.3 TB/s for one 64-byte row per lane).  A 4x4 transpose inside
+// each lane quad (two DPP butterfly stages per dword plane) then gives lane
+// l = 4q + i all four chunks of packet 16i + q.
+
+template <bool NT>
+__device__ __forceinline__ void load_coal(const uint8_t *__restrict__ wave_base, uint32_t lane, u32x4 (&v)[4]) {
+    const u32x4 *q = reinterpret_cast<const u32x4 *>(wave_base) + lane;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = NT ? __builtin_nontemporal_load(q + 64 * j) : q[64 * j];
+}
+
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp(uint32_t x) {
+    return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), CTRL, 0xF, 0xF, false));
+}
+
+// v[k] = value of instruction k in this lane; returns f[c] = quad-mate c's
+// value of instruction (lane & 3).  Each butterfly stage sends one select per
+// pair and receives it with one unconditional DPP move whose result feeds both
+// arms of the following selects — a DPP result used in only one arm gets sunk
+// into a divergent branch, where it reads inactive lanes.
+__device__ __forceinline__ void quad_transpose(const uint32_t (&v)[4], uint32_t (&f)[4], bool b0, bool b1) {
+    constexpr int kSwap1 = 0xB1;  // quad_perm [1,0,3,2]
+    constexpr int kSwap2 = 0x4E;  // quad_perm [2,3,0,1]
+    const uint32_t r0 = dpp<kSwap1>(b0 ? v[0] : v[1]);
+    const uint32_t r1 = dpp<kSwap1>(b0 ? v[2] : v[3]);
+    uint32_t s[4];
+    s[0] = b0 ? r0 : v[0];
+    s[1] = b0 ? v[1] : r0;
+    s[2] = b0 ? r1 : v[2];
+    s[3] = b0 ? v[3] : r1;
+    const uint32_t q0 = dpp<kSwap2>(b1 ? s[0] : s[2]);
+    const uint32_t q1 = dpp<kSwap2>(b1 ? s[1] : s[3]);
+    f[0] = b1 ? q0 : s[0];
+    f[1] = b1 ? q1 : s[1];
+    f[2] = b1 ? s[2] : q0;
+    f[3] = b1 ? s[3] : q1;
+}
+
+// Rebuild this lane's packet (d[16] = its first 64 bytes) from the 4 loads.
+__device__ __forceinline__ void transpose_batch(const u32x4 (&v)[4], uint32_t lane, uint32_t (&d)[16]) {
+    const bool b0 = lane & 1u, b1 = lane & 2u;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {  // dword plane k of every chunk
+        const uint32_t in[4] = {v[0][k], v[1][k], v[2][k], v[3][k]};
+        uint32_t f[4];
+        quad_transpose(in, f, b0, b1);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) d[4 * c + k] = f[c];
+    }
+}
+
+// Row-swap variant (MODE 4): load_rowswap / rowswap_batch, devutil.hpp.
+
+// Packed frames, the same layout: for instruction j lane 16r + c loads chunk
+// r of frame 16j + c (that frame's descriptor fetched from lane 16j + c with
+// ds_bpermute), so every instruction consumes whole 64-byte frame lines and
+// non-temporal loads pay off; rowswap_batch then gives lane l the first 64
+// bytes of its own frame.  (sol `frames_rs_nt` 0.293 ms vs 0.340 ms for one
+// frame per lane, C3 IMIX, profiles/r1_frames_rs/.)  Every lane of the wave
+// must be active; `ds` is this lane's descriptor (offset << 16 | length; 0
+// for lanes past the batch end).  A chunk is read only if it starts inside
+// its frame: a 16-byte aligned load that starts at a frame byte stays in
+// that byte's page, so nothing past the last frame of the buffer is touched.
+__device__ __forceinline__ void load_frames_rs(const uint8_t *__restrict__ frames, uint64_t ds, uint32_t lane,
+                                               u32x4 (&v)[4]) {
+    const uint32_t lo = static_cast<uint32_t>(ds), hi = static_cast<uint32_t>(ds >> 32);
+    const uint32_t chunk = 16u * (lane >> 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int src = static_cast<int>((16u * j + (lane & 15u)) << 2);
+        const uint32_t l = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(lo)));
+        const uint32_t h = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(hi)));
+        const uint64_t o = (uint64_t(h) << 32 | l) >> 16;
+        v[j] = u32x4{0, 0, 0, 0};
+        if (chunk < (l & 0xFFFFu)) v[j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(frames + o) + (lane >> 4));
+    }
+}
+
+// One lane's frame: the first 64 bytes, chunks past `len` not read (see
+// load_frames_rs), then bytes past `len` zeroed.
+__device__ __forceinline__ void load16_frame(const uint8_t *__restrict__ p, uint32_t len, uint32_t (&d)[16]) {
+    const u32x4 *q = reinterpret_cast<const u32x4 *>(p);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        u32x4 v = u32x4{0, 0, 0, 0};
+        if (16u * j < len) v = q[j];
+        d[4 * j + 0] = v.x;
+        d[4 * j + 1] = v.y;
+        d[4 * j + 2] = v.z;
+        d[4 * j + 3] = v.w;
+    }
+    clip16(d, len);
+}
+
+// Packet index (within the wave's 64) held by lane l after transpose_batch.
+__device__ __forceinline__ uint32_t coal_packet(uint32_t lane) { return 16u * (lane & 3u) + (lane >> 2); }
+
+struct LinearArgs {
+    const uint32_t *rec4;
+    uint32_t n4;
+    const uint32_t *rec6;
+    uint32_t n6;
+    uint32_t flags;  // NFFACL_PARSE_*
+};
+
+// ---------------------------------------------------------------------------
+// INDEXED: per-lane interval search + ordered candidate lists (table.hpp).
+// ---------------------------------------------------------------------------
+
+struct SlotArgs {
+    uint32_t shift, off_dir, off_ent, off_dir16;  // off_dir16: 0 = plain u32 directory
+    // flat kernels (generalized slots, table.hpp SlotField): bucket =
+    // (key[f1] >> shift) << bits2 | key[f2] >> shift2, key[kFZero] = 0
+    uint32_t f1, f2, shift2, bits2;
+};
+struct FamArgs {
+    SlotArgs slot[kMaxSlots];  // INDEXED / LDS forms: [dst addr, src addr, dst port, src port]
+    uint32_t off_resid, n_resid;
+    uint32_t off_cold;      // HYBRID flat forms: output array (one u32 per rule)
+    uint32_t off_ent_base;  // HYBRID flat forms: the family's first entry
+};
+struct IndexedArgs {
+    const uint32_t *tab;    // device table (global memory)
+    uint32_t stage_dwords;  // leading dwords staged in LDS (multiple of 4)
+    uint32_t flags;         // NFFACL_PARSE_*
+    uint32_t dir8;          // HYBRID: two-level directories carry u8 offsets (SplitTab::bounds)
+    uint32_t generic;       // HYBRID flat forms: slots key on SlotArgs::f1/f2 (else slot s on field s)
+    FamArgs f4, f6;
+};
+
+// Table placement (kernel template argument).
+enum TableMode : int {
+    kTabGlobal = 0,  // INDEXED, read through L1/L2/MALL
+    kTabLds = 1,     // INDEXED, staged whole in LDS
+    kTabSplit = 2,   // HYBRID lane form: INDEXED entries in global memory,
+                     // directories staged in LDS, one workgroup per CU; the
+                     // spare VGPRs buy the frames kernel a two-batch software
+                     // pipeline.  (Two workgroups per CU with <= 78 KiB of
+                     // directories and 64 VGPRs ran 18 % slower on C3:
+                     // longer lists, spills; profiles/r1_hybrid/sw5.)
+    kTabFlat = 4,    // HYBRID table, directories read from global memory, the
+                     // candidates of a wave's 64 packets tested 64 at a time,
+                     // 2 rounds of loads in flight
+    kTabFlat4 = 5,   // the same, 4 rounds in flight
+    kTabFlatLds = 6, // HYBRID flat-LDS: the flat walk (2 rounds in flight)
+                     // over directories staged in LDS, one 1024-thread
+                     // workgroup per CU, candidate scratch after the image
+    kTabFlatLds4 = 7,  // the same, 4 rounds in flight (larger scratch)
+    kTabFlatLds4U = 8, // the same, entry loads of every non-empty round issued
+                       // without a per-lane branch (tables with many candidates
+                       // per packet: CompiledTable::flat_uncond)
+};
+
+extern __shared__ __attribute__((aligned(16))) uint32_t lds_tab[];
+
+// Table accessors: the whole table staged in LDS, or read through L1/L2.
+// ld4(i): i is a multiple of 4 (entries are 16-byte aligned, table.hpp) and is
+// indexed in vector units so the compiler can emit one ds_read_b128 /
+// global_load_dwordx4 (a byte-offset cast only gets split ds_read2_b32 pairs).
+// List bounds dir[t], dir[t + 1] of a plain u32 directory (one ds_read2 /
+// two dword loads).
+template <class T>
+__device__ __forceinline__ void bounds32(const T &tab, uint32_t dir, uint32_t t, uint32_t &lo, uint32_t &hi) {
+    lo = tab.ld(dir + t);
+    hi = tab.ld(dir + t + 1);
+}
+
+struct LdsTab {
+    __device__ __forceinline__ uint32_t ld(uint32_t i) const { return lds_tab[i]; }
+    __device__ __forceinline__ void bounds(uint32_t dir, uint32_t, uint32_t t, uint32_t &lo, uint32_t &hi,
+                                           bool = false) const {
+        bounds32(*this, dir, t, lo, hi);
+    }
+    __device__ __forceinline__ u32x4 ld4(uint32_t i) const {
+        return reinterpret_cast<const u32x4 *>(lds_tab)[i >> 2];
+    }
+};
+struct GlobalTab {
+    const uint32_t *__restrict__ p;
+    __device__ __forceinline__ uint32_t ld(uint32_t i) const { return p[i]; }
+    __device__ __forceinline__ void bounds(uint32_t dir, uint32_t, uint32_t t, uint32_t &lo, uint32_t &hi,
+                                           bool = false) const {
+        bounds32(*this, dir, t, lo, hi);
+    }
+    __device__ __forceinline__ u32x4 ld4(uint32_t i) const {
+        return reinterpret_cast<const u32x4 *>(p)[i >> 2];
+    }
+};
+// HYBRID lane form: directories (ld) staged in LDS, entries (ld4) global.
+// IN_LDS = false reads the same directory image from global memory (the
+// persistent scalar-call consumer, service.hip, which stages nothing).
+template <bool IN_LDS>
+struct DirTab {
+    const uint32_t *__restrict__ p;
+    __device__ __forceinline__ uint32_t ld(uint32_t i) const { return IN_LDS ? lds_tab[i] : p[i]; }
+    // two-level directory (table.hpp): dir[t] = base[t >> 6] + dir16[t], or
+    // with dir8 (wave-uniform) base[t >> 4] + dir8[t]
+    __device__ __forceinline__ void bounds(uint32_t dir, uint32_t dir16, uint32_t t, uint32_t &lo, uint32_t &hi,
+                                           bool dir8 = false) const {
+        if (dir16 == 0u) {
+            bounds32(*this, dir, t, lo, hi);
+            return;
+        }
+        if (dir8) {
+            const uint32_t g = t >> kDir8GroupShift;
+            const uint32_t b0 = ld(dir + g), b1 = ld(dir + g + 1);                    // ds_read2
+            const uint32_t w0 = ld(dir16 + (t >> 2)), w1 = ld(dir16 + (t >> 2) + 1);  // ds_read2
+            const uint32_t x = __builtin_amdgcn_alignbit(w1, w0, (t & 3u) * 8u);  // bytes t, t + 1
+            lo = b0 + (x & 0xFFu);
+            hi = (((t + 1u) & ((1u << kDir8GroupShift) - 1u)) == 0u ? b1 : b0) + ((x >> 8) & 0xFFu);
+            return;
+        }
+        const uint32_t g = t >> kDir16GroupShift;
+        const uint32_t b0 = ld(dir + g), b1 = ld(dir + g + 1);                         // ds_read2
+        const uint32_t w0 = ld(dir16 + (t >> 1)), w1 = ld(dir16 + (t >> 1) + 1);      // ds_read2
+        const bool odd = (t & 1u) != 0u;
+        lo = b0 + (odd ? w0 >> 16 : w0 & 0xFFFFu);
+        hi = (((t + 1u) >> kDir16GroupShift) != g ? b1 : b0) + (odd ? w1 & 0xFFFFu : w0 >> 16);
+    }
+    __device__ __forceinline__ u32x4 ld4(uint32_t i) const {
+        return reinterpret_cast<const u32x4 *>(p)[i >> 2];
+    }
+};
+using SplitTab = DirTab<true>;
+
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+
+// Mismatch bits of an entry's first 8 dwords (A = words 0..3, B = 4..7):
+// address words, protocol (exact flag) and ports — acl.go:526-539 / 546-557
+// with IPv6 restricted to the top 32 bits of each address.
+__device__ __forceinline__ uint32_t entry_miss(const u32x4 &A, const u32x4 &B, const Fields &f) {
+    const uint32_t proto = ((f.proto ^ B.x) & 0xFFu) & (0u - ((B.x >> 8) & 1u));
+    return ((f.s[0] ^ A.x) & A.y) | ((f.t[0] ^ A.z) & A.w) | proto | port_miss(f.ports, B.y, B.z);
+}
+
+// Mismatch bits of the IPv6 extension words 8..19 (address words 1..3).
+template <class T>
+__device__ __forceinline__ uint32_t entry_miss_ext(const T &tab, uint32_t off, const Fields &f) {
+    const u32x4 x = tab.ld4(off), y = tab.ld4(off + 4), z = tab.ld4(off + 8);
+    // x = s1 s2 s3 sm1 | y = sm2 sm3 t1 t2 | z = t3 tm1 tm2 tm3
+    return ((f.s[1] ^ x.x) & x.w) | ((f.s[2] ^ x.y) & y.x) | ((f.s[3] ^ x.z) & y.y) |
+           ((f.t[1] ^ y.z) & z.y) | ((f.t[2] ^ y.w) & z.z) | ((f.t[3] ^ z.x) & z.w);
+}
+
+// First match over the four key slots of the lane's family, walked together:
+// every iteration tests the next entry of every slot list, so the wave pays
+// max(list lengths) table round trips, not their sum.  Loops have
+// wave-uniform trip counts (ballots) and predicated bodies.
+// U = list entries per slot per loop trip: all NS x U entry loads of a trip
+// are issued before any is tested.
+template <int NS, int U, class T>
+__device__ __forceinline__ uint32_t classify_indexed(const T &tab, const IndexedArgs &a, const Fields &f) {
+    const bool v6 = f.is6;
+    const bool mine = f.is4 || f.is6;
+    const uint32_t ew = v6 ? kEnt6Dwords : kEnt4Dwords;
+    const uint32_t key[4] = {__builtin_bswap32(f.t[0]), __builtin_bswap32(f.s[0]), f.ports >> 16,
+                             f.ports & 0xFFFFu};
+    uint32_t c[NS], e[NS], base[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        const SlotArgs &s4 = a.f4.slot[s], &s6 = a.f6.slot[s];
+        const uint32_t shift = v6 ? s6.shift : s4.shift;
+        const uint32_t dir = v6 ? s6.off_dir : s4.off_dir;
+        base[s] = v6 ? s6.off_ent : s4.off_ent;
+        const uint32_t t = key[s] >> shift;  // < n_buckets for any key: both reads in range
+        uint32_t lo, hi;
+        tab.bounds(dir, v6 ? s6.off_dir16 : s4.off_dir16, t, lo, hi, a.dir8 != 0u);
+        c[s] = lo;
+        e[s] = mine ? hi : lo;
+    }
+    uint32_t best = kNone, out = 0;
+    while (true) {
+        bool any = false;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) any |= c[s] < e[s];
+        if (!ballot(any)) break;
+        u32x4 A[NS][U], B[NS][U];
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                // only lanes still walking this list load (a 16-byte load
+                // costs the TA 16 cycles per 64 active lanes; LDS: -1.3 % on
+                // C2, global: -4 % on C3, profiles/r1_masked)
+                A[s][u] = B[s][u] = u32x4{0, 0, 0, 0};
+                if (c[s] + u < e[s]) {
+                    const uint32_t off = base[s] + (c[s] + u) * ew;
+                    A[s][u] = tab.ld4(off);
+                    B[s][u] = tab.ld4(off + 4);
+                }
+            }
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            bool go = true;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const bool act = go && c[s] + u < e[s];
+                const uint32_t idx = B[s][u].x >> kEntIndexShift;
+                const bool earlier = act && idx < best;
+                bool pass = entry_miss(A[s][u], B[s][u], f) == 0u;
+                const bool ext = v6 && earlier && pass;
+                if (ballot(ext)) {
+                    if (ext) pass = entry_miss_ext(tab, base[s] + (c[s] + u) * ew + 8, f) == 0u;
+                }
+                const bool take = earlier && pass;
+                best = take ? idx : best;
+                out = take ? B[s][u].w : out;
+                // stop at a hit, or once the ascending list has passed `best`
+                go = earlier && !pass;
+            }
+            c[s] = go ? c[s] + U : e[s];
+        }
+    }
+    // rules with no selective key: wave-uniform scan in rule order per family
+#pragma unroll
+    for (int fam = 0; fam < 2; ++fam) {
+        const FamArgs &fa = fam ? a.f6 : a.f4;
+        const bool in_fam = fam ? f.is6 : f.is4;
+        const uint32_t w = fam ? kEnt6Dwords : kEnt4Dwords;
+        for (uint32_t i = 0; i < fa.n_resid; ++i) {
+            const uint32_t off = fa.off_resid + i * w;
+            const u32x4 A = tab.ld4(off), B = tab.ld4(off + 4);
+            const uint32_t idx = B.x >> kEntIndexShift;
+            const bool want = in_fam && idx < best;
+            if (!ballot(want)) break;  // residual list ascends too
+            bool pass = want && entry_miss(A, B, f) == 0u;
+            if (fam && ballot(pass)) {
+                if (pass) pass = entry_miss_ext(tab, off + 8, f) == 0u;
+            }
+            best = pass ? idx : best;
+            out = pass ? B.w : out;
+        }
+    }
+    return best != kNone ? out : 0u;
+}
+
+__device__ __forceinline__ void stage_table(const IndexedArgs &a) {
+    const u32x4 *src = reinterpret_cast<const u32x4 *>(a.tab);
+    u32x4 *dst = reinterpret_cast<u32x4 *>(lds_tab);
+    for (uint32_t i = threadIdx.x; i < a.stage_dwords / 4; i += blockDim.x) dst[i] = src[i];
+    __syncthreads();
+}
+
+// ---- HYBRID (table.hpp "hybrid table") --------------------------------------
+
+// Top-L-bits mask of a big-endian word, L in 0..32 (one 64-bit shift).
+__device__ __forceinline__ uint32_t prefix_mask(uint32_t L) {
+    return static_cast<uint32_t>(0xFFFFFFFF00000000ull >> L);
+}
+
+// 12-byte pieces of the exact flat-form entries (table.hpp): an IPv4 entry
+// is two (the compiler issues dwordx4 + dwordx2), an IPv6 entry four.
+typedef uint32_t u32x3 __attribute__((ext_vector_type(3), aligned(4)));
+
+__device__ __forceinline__ u32x3 ld3(const uint32_t *__restrict__ p) { return *reinterpret_cast<const u32x3 *>(p); }
+
+// Mismatch bits of an exact entry's first six words (both families): top
+// address words under their prefix lengths (IPv6: capped at 32), protocol,
+// ports — acl.go:526-539 / 546-557 for IPv4 completely, for IPv6 up to the
+// low address words.  ks/kd: big-endian src/dst (top) words.
+__device__ __forceinline__ uint32_t hyb_miss(const u32x3 &A, const u32x3 &B, uint32_t ks, uint32_t kd, uint32_t proto,
+                                             uint32_t ports) {
+    const uint32_t sl = min(B.z & 0xFFu, 32u), dl = min((B.z >> 8) & 0xFFu, 32u);
+    const uint32_t pm = ((proto ^ A.z) & 0xFFu) & (0u - ((A.z >> 8) & 1u));
+    return ((ks ^ A.x) & prefix_mask(sl)) | ((kd ^ A.y) & prefix_mask(dl)) | pm | port_miss(ports, B.x, B.y);
+}
+
+// IPv6 address words 1..3 of an exact entry (C = src1 src2 src3, D = dst1
+// dst2 dst3) against big-endian packet words s[1..3], t[1..3].
+// By first difference: the address matches its prefix of length L iff its
+// first bit differing from the rule's (counted from bit 32) lies at or past
+// L - 32 (v_ffbh per word instead of three prefix masks per address).
+__device__ __forceinline__ uint32_t first_diff96(uint32_t x1, uint32_t x2, uint32_t x3) {
+    const uint32_t p1 = __clz(x1), p2 = 32u + __clz(x2), p3 = 64u + __clz(x3);  // __clz(0) = 32
+    return x1 != 0u ? p1 : x2 != 0u ? p2 : p3;
+}
+
+__device__ __forceinline__ uint32_t hyb_miss6(const u32x3 &C, const u32x3 &D, uint32_t lens, const uint32_t (&s)[4],
+                                              const uint32_t (&t)[4]) {
+    const uint32_t sl = lens & 0xFFu, dl = (lens >> 8) & 0xFFu;
+    const uint32_t ps = 32u + first_diff96(s[1] ^ C.x, s[2] ^ C.y, s[3] ^ C.z);
+    const uint32_t pd = 32u + first_diff96(t[1] ^ D.x, t[2] ^ D.y, t[3] ^ D.z);
+    return (ps < sl ? 1u : 0u) | (pd < dl ? 1u : 0u);
+}
+
+// ---- FLAT: a wave's candidates, 64 at a time --------------------------------
+//
+// The list walks above cost one dependent table round trip per loop trip, and
+// a wave takes as many trips as its longest walk.  For tables that live in
+// L2/MALL that latency, not bandwidth, bounds the kernel (C5: 13 trips of
+// ~3 us per 64 packets).  Here every lane first looks up the list bounds of
+// its packet in each slot (one round trip), the wave lays all (packet, slot,
+// entry) candidates end to end (exclusive scan of the list lengths), and
+// round r gives lane l candidate 64 r + l: one table load per lane per round,
+// all 64 lanes busy, ceil(total / 64) rounds.  A lane finds its candidate's
+// list through an LDS window: every list overlapping the round's 64
+// positions marks its first position there, a prefix max over the window
+// carries the mark forward.  Each passing candidate posts its rule index to
+// the packet's LDS minimum (ds_min_u32): the minimum over every candidate is
+// the first match of the ordered lists, no early exit needed.
+template <int R>
+struct FlatScratch {
+    uint32_t mark[64 * R];   // window position -> (owner lane << 11 | slot << 8 | position) + 1, 0 = none
+    uint32_t delta[64 * R];  // window position -> (entry number - candidate number) << 1 | IPv6
+    uint64_t best[64];       // per packet (lane): lowest passing rule index << 32 | output code
+};
+
+// Order this wave's LDS writes before its following LDS reads of other lanes'
+// words (one wave: program order on the LDS queue; this keeps the compiler
+// from reordering across it).
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ uint32_t bperm(uint32_t v, uint32_t src_lane) {
+    return static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(static_cast<int>(src_lane << 2), static_cast<int>(v)));
+}
+
+// Wave-wide inclusive scans on DPP (GFX9 controls): row_shr 1, 2, 4, 8 build
+// the prefix inside each 16-lane row, row_bcast:15 (rows 1, 3) and
+// row_bcast:31 (rows 2, 3) carry the row totals.  Lanes without a source read
+// 0 (bound_ctrl), the identity of both + and max over unsigned values.
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ uint32_t dpp0(uint32_t x) {
+    return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), CTRL, ROW_MASK, 0xF, true));
+}
+
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
+    x += dpp0<0x111>(x);
+    x += dpp0<0x112>(x);
+    x += dpp0<0x114>(x);
+    x += dpp0<0x118>(x);
+    x += dpp0<0x142, 0xA>(x);
+    x += dpp0<0x143, 0xC>(x);
+    return x;
+}
+
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
+    x = max(x, dpp0<0x111>(x));
+    x = max(x, dpp0<0x112>(x));
+    x = max(x, dpp0<0x114>(x));
+    x = max(x, dpp0<0x118>(x));
+    x = max(x, dpp0<0x142, 0xA>(x));
+    x = max(x, dpp0<0x143, 0xC>(x));
+    return x;
+}
+
+template <int NS, int R, bool LDS_DIRS, bool UNCOND = false, bool DIRS_IN_LDS = true>
+__device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fields &f, FlatScratch<R> &W,
+                                                  uint32_t lane) {
+    const bool v6 = f.is6;
+    const bool mine = f.is4 || f.is6;
+    const uint32_t ks = __builtin_bswap32(f.s[0]), kd = __builtin_bswap32(f.t[0]);
+    const uint32_t sport = f.ports & 0xFFFFu, dport = f.ports >> 16;
+    // key[f] of a slot field f (SlotField; kFZero and unused slots: 0)
+    auto pick = [&](uint32_t fld) -> uint32_t {
+        return fld == kFDst ? kd : fld == kFSrc ? ks : fld == kFDport ? dport : fld == kFSport ? sport : 0u;
+    };
+    // list bounds of this packet in every slot (family-relative entry numbers)
+    uint32_t st[NS], ln[NS];
+    // positional slots (a.generic == 0: slot s keys on field s, 1-D): the key
+    // is known at compile time, no per-lane field selects (wave-uniform branch)
+    if (LDS_DIRS && a.generic == 0u) {
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            const SlotArgs &s4 = a.f4.slot[s], &s6 = a.f6.slot[s];
+            const uint32_t key = s == kFDst ? kd : s == kFSrc ? ks : s == kFDport ? dport : s == kFSport ? sport : 0u;
+            const uint32_t t = key >> (v6 ? s6.shift : s4.shift);
+            uint32_t hi;
+            DirTab<DIRS_IN_LDS>{a.tab}.bounds(v6 ? s6.off_dir : s4.off_dir, v6 ? s6.off_dir16 : s4.off_dir16, t, st[s], hi,
+                                   a.dir8 != 0u);
+            ln[s] = mine ? hi - st[s] : 0u;
+        }
+    } else {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        const SlotArgs &s4 = a.f4.slot[s], &s6 = a.f6.slot[s];
+        const uint32_t shift = v6 ? s6.shift : s4.shift;
+        const uint32_t dir = v6 ? s6.off_dir : s4.off_dir;
+        const uint32_t t = ((pick(v6 ? s6.f1 : s4.f1) >> shift) << (v6 ? s6.bits2 : s4.bits2)) |
+                           (pick(v6 ? s6.f2 : s4.f2) >> (v6 ? s6.shift2 : s4.shift2));
+        if (LDS_DIRS) {
+            uint32_t hi;
+            DirTab<DIRS_IN_LDS>{a.tab}.bounds(dir, v6 ? s6.off_dir16 : s4.off_dir16, t, st[s], hi, a.dir8 != 0u);
+            ln[s] = mine ? hi - st[s] : 0u;
+        } else {
+            // generalized slots: a family's unused slots (f1 == kFZero) read nothing
+            st[s] = 0u;
+            ln[s] = 0u;
+            if (mine && (v6 ? s6.f1 : s4.f1) != kFZero) {
+                st[s] = a.tab[dir + t];
+                ln[s] = a.tab[dir + t + 1] - st[s];
+            }
+        }
+    }
+    }
+    uint32_t total = 0;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) total += ln[s];
+    const uint32_t incl = wave_incl_sum(total);
+    const uint32_t off = incl - total;  // first candidate number of this packet
+    const uint32_t T = __builtin_amdgcn_readlane(incl, 63);
+    W.best[lane] = ~0ull;
+    const uint32_t proto_fam = f.proto | (v6 ? 0x100u : 0u);
+    const uint32_t *__restrict__ E4 = a.tab + a.f4.off_ent_base;
+    const uint32_t *__restrict__ E6 = a.tab + a.f6.off_ent_base;
+    // One window of RR rounds (64 RR candidates) starting at candidate `win`,
+    // straight-line so the compiler interleaves its RR rounds of loads.  A
+    // window of R rounds runs while at least 64 (R - 1) + 1 candidates
+    // remain; the last window runs only the rounds its candidates fill (one
+    // wave-uniform dispatch on the remainder, not a branch per round: per-round
+    // branches broke the load interleave, profiles/r2_exact/skip/).
+    auto window = [&](uint32_t win, auto rr) {
+        constexpr int RR = decltype(rr)::value;
+#pragma unroll
+        for (int j = 0; j < RR; ++j) W.mark[64 * j + lane] = 0u;
+        wave_lds_sync();
+        uint32_t so = off;  // candidate number of list s's first entry
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            if (ln[s] != 0u && so < win + 64u * RR && so + ln[s] > win) {
+                const uint32_t pos = so > win ? so - win : 0u;
+                W.mark[pos] = ((lane << 11 | static_cast<uint32_t>(s) << 8) | pos) + 1u;
+                W.delta[pos] = ((st[s] - so) << 1) | (v6 ? 1u : 0u);
+            }
+            so += ln[s];
+        }
+        wave_lds_sync();
+        // RR rounds: locate every candidate's list, then issue every round's
+        // entry loads (IPv6 candidates: all four pieces) before testing any.
+        // Rounds 0..RR-2 are full (the dispatch below), only round RR-1 can
+        // hold lanes past the wave's candidates (the per-round k < T test
+        // stays: with it compiled out the scheduler hoists more loads, and
+        // the frames kernels spill at 128 VGPRs).
+        uint32_t owner[RR], idx[RR];
+        bool valid[RR], six[RR];
+        u32x3 A[RR], B[RR], C[RR], D[RR];
+        // the rounds' prefix-max scans are independent (only their carries
+        // chain): issued together, their DPP steps interleave instead of
+        // waiting out each other's data hazards
+        uint32_t scan[RR];
+#pragma unroll
+        for (int j = 0; j < RR; ++j) scan[j] = wave_incl_max(W.mark[64 * j + lane]);
+        uint32_t carry = 0;
+#pragma unroll
+        for (int j = 0; j < RR; ++j) {
+            const uint32_t m = max(scan[j], carry);
+            if (j + 1 < RR) carry = __builtin_amdgcn_readlane(m, 63);
+            const uint32_t k = win + 64u * j + lane;
+            valid[j] = k < T;
+            owner[j] = (m - 1u) >> 11;
+            const uint32_t dp = W.delta[(m - 1u) & 0xFFu];
+            six[j] = (dp & 1u) != 0u;
+            // UNCOND: lanes past the wave's candidates load entry 0 of the
+            // IPv4 list (untested) instead of branching around the load
+            // (profiles/r2_exact/uncond/)
+            const uint32_t ent = !UNCOND || valid[j] ? k + static_cast<uint32_t>(static_cast<int32_t>(dp) >> 1) : 0u;
+            const uint32_t *e = six[j] && (!UNCOND || valid[j]) ? E6 + ent * kHybEnt6Dwords : E4 + ent * kHybEnt4Dwords;
+            if (UNCOND || valid[j]) {
+                A[j] = ld3(e);
+                B[j] = ld3(e + 3);
+            } else {
+                A[j] = B[j] = u32x3{0, 0, 0};
+            }
+            if (valid[j] && six[j]) {  // (C, D are read only for valid IPv6 candidates)
+                C[j] = ld3(e + 6);
+                D[j] = ld3(e + 9);
+            }
+        }
+        bool pass[RR];
+        bool any6 = false;
+#pragma unroll
+        for (int j = 0; j < RR; ++j) {
+            // the owner packet's fields
+            const uint32_t o = owner[j];
+            const uint32_t oks = bperm(ks, o), okd = bperm(kd, o);
+            const uint32_t opf = bperm(proto_fam, o), opt = bperm(f.ports, o);
+            pass[j] = valid[j] && hyb_miss(A[j], B[j], oks, okd, opf & 0xFFu, opt) == 0u;
+            idx[j] = A[j].z >> kEntIndexShift;
+            any6 |= pass[j] && six[j];
+        }
+        if (ballot(any6)) {  // IPv6 candidates: address words 1..3 of the owner
+            uint32_t sb[4], tb[4];
+#pragma unroll
+            for (int q = 1; q < 4; ++q) {
+                sb[q] = __builtin_bswap32(f.s[q]);
+                tb[q] = __builtin_bswap32(f.t[q]);
+            }
+#pragma unroll
+            for (int j = 0; j < RR; ++j) {
+                if (ballot(pass[j] && six[j])) {  // whole wave: bpermute reads every lane
+                    uint32_t os[4] = {0, 0, 0, 0}, ot[4] = {0, 0, 0, 0};
+#pragma unroll
+                    for (int q = 1; q < 4; ++q) {
+                        os[q] = bperm(sb[q], owner[j]);
+                        ot[q] = bperm(tb[q], owner[j]);
+                    }
+                    if (pass[j] && six[j]) pass[j] = hyb_miss6(C[j], D[j], B[j].z, os, ot) == 0u;
+                }
+            }
+        }
+        // (posting from every lane, ~0 to its own word when nothing passed,
+        // instead of the branch: C5 0.757 vs 0.750 ms, profiles/r2_exact/uncond/am_*)
+#pragma unroll
+        for (int j = 0; j < RR; ++j)  // rule index << 32 | output code: the minimum carries the winner's output
+            if (pass[j]) atomicMin(reinterpret_cast<unsigned long long *>(&W.best[owner[j]]),
+                                   static_cast<unsigned long long>(idx[j]) << 32 | (B[j].z >> kHybOutShift));
+        wave_lds_sync();
+    };
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, (R >= 3 ? 3 : R)>;
+    using IR = std::integral_constant<int, R>;
+    for (uint32_t win = 0; win < T; win += 64 * R) {
+        const uint32_t rem = T - win;  // wave-uniform
+        if (rem > 64u * (R - 1)) window(win, IR{});
+        else if (R >= 3 && rem > 128u) window(win, I3{});
+        else if (rem > 64u) window(win, I2{});
+        else window(win, I1{});
+    }
+    uint64_t best = W.best[lane];  // ~0 or rule index << 32 | output code
+    // rules with no selective key: wave-uniform scan in rule order per family
+#pragma unroll
+    for (int fam = 0; fam < 2; ++fam) {
+        const FamArgs &fa = fam ? a.f6 : a.f4;
+        const bool in_fam = fam ? f.is6 : f.is4;
+        const uint32_t ew = fam ? kHybEnt6Dwords : kHybEnt4Dwords;
+        for (uint32_t i = 0; i < fa.n_resid; ++i) {
+            const uint32_t *e = a.tab + fa.off_resid + i * ew;
+            const u32x3 RA = ld3(e), RB = ld3(e + 3);
+            const uint32_t ri = RA.z >> kEntIndexShift;
+            const bool want = in_fam && ri < uint32_t(best >> 32);
+            if (!ballot(want)) break;  // residual list ascends too
+            bool ok = want && hyb_miss(RA, RB, ks, kd, f.proto, f.ports) == 0u;
+            if (fam && ballot(ok)) {
+                uint32_t sb[4] = {0, 0, 0, 0}, tb[4] = {0, 0, 0, 0};
+#pragma unroll
+                for (int q = 1; q < 4; ++q) {
+                    sb[q] = __builtin_bswap32(f.s[q]);
+                    tb[q] = __builtin_bswap32(f.t[q]);
+                }
+                if (ok) ok = hyb_miss6(ld3(e + 6), ld3(e + 9), RB.z, sb, tb) == 0u;
+            }
+            best = ok ? (uint64_t(ri) << 32 | (RB.z >> kHybOutShift)) : best;
+        }
+    }
+    // output numbers below kHybOutEscape travel in the entry; others come from the output array
+    const bool hit = best != ~0ull;
+    uint32_t out = hit ? static_cast<uint32_t>(best) : 0u;
+    const bool rd = hit && out == kHybOutEscape;
+    if (ballot(rd)) {
+        const uint32_t r = static_cast<uint32_t>(best >> 32);
+        if (rd) out = a.tab[(v6 ? a.f6.off_cold : a.f4.off_cold) + r];
+    }
+    return out;
+}
+
+}  // namespace dev
+}  // namespace nffacl

@@ -17,9 +17,13 @@ namespace nffacl {
 void set_last_error(const std::string &s);
 const char *last_error();
 
-// One compiled table resident in HBM (lifetime: tables.hpp).
+// One compiled table resident in HBM (lifetime: tables.hpp).  The blob is
+// followed by the scalar-call consumer's descriptor (service.hpp SvcDesc).
 struct DevTable : DeviceBlob {
     CompiledTable meta;
+    uint32_t gen = 0;                  // process-unique table generation (service.hip)
+    uint32_t svc_kind = 0;             // SvcKind of the layout
+    const uint32_t *d_desc = nullptr;  // device address of the SvcDesc
 };
 using TablePtr = std::shared_ptr<DevTable>;
 
@@ -38,6 +42,12 @@ struct Tune {
 };
 
 int upload_table(nffacl_engine *eng, const nffacl_rules &rules, TablePtr &out);
+// An engine without a table (launch shape of `hip_device` only): the device
+// batcher's, whose batches take their rule sets' own tables (capi.cpp).
+int engine_shell(int hip_device, nffacl_engine **out);
+// Compile `rules` with `algo` / `copt`, upload blob + service descriptor
+// through `home` (whose device is current), fill `t`.
+int compile_upload(const nffacl_rules &rules, int algo, const CompileOptions &copt, TableHome &home, DevTable &t);
 
 }  // namespace nffacl
 

@@ -7,15 +7,31 @@
 // own layouts from them.
 #pragma once
 
+#include <atomic>
 #include <cstdint>
+#include <mutex>
 #include <string>
 #include <vector>
 
 #include "nffacl.h"
 
+namespace nffacl {
+struct DevTable;                  // engine.hpp
+constexpr int kMaxDevices = 16;   // HIP devices a rule set can be compiled for
+}  // namespace nffacl
+
 struct nffacl_rules {
     std::vector<nffacl_rule4> ip4;
     std::vector<nffacl_rule6> ip6;
+    // The compiled device table of this rule set, one per HIP device, built
+    // on first use by the calls that take the rule set itself (the scalar
+    // service, per-burst batcher submits, nffacl_rules_prepare) and retired
+    // with it in nffacl_rules_free: the Go binding's *L3Rules owns its table,
+    // so a rule reload (examples/tutorial/step08.go:38-44) is "load the new
+    // rules, store the pointer" exactly as in the reference.  Published once
+    // (release) and immutable afterwards; readers load without a lock.
+    mutable std::atomic<nffacl::DevTable *> dev[nffacl::kMaxDevices] = {};
+    mutable std::mutex dev_mu;  // serialises the first compile per device
 };
 
 struct nffacl_l2rules {
@@ -23,6 +39,12 @@ struct nffacl_l2rules {
 };
 
 namespace nffacl {
+
+// Compiled table of `rules` on HIP device `dev` (built + uploaded on first
+// use; service.hip).  nullptr + status on failure.
+DevTable *rules_table(const nffacl_rules *rules, int dev, int &status);
+// Retire every device table of `rules` (nffacl_rules_free).
+void release_rules_tables(const nffacl_rules *rules);
 
 // One line of a rule file after field splitting: acl.go:55-62 rawL3Rule.
 struct RawL3Rule {

@@ -1,0 +1,633 @@
+// service.hip — the persistent scalar-call consumer (nffacl_service_*) and the
+// per-rule-set device tables (nffacl_rules_prepare) of libnffacl.
+//
+// Call shape replaced: one packet per call from every flow-function clone —
+// pkt.L3ACLPermit(rules) / pkt.L3ACLPort(rules) inside a SetSeparator /
+// SetSplitter user function (flow/flow.go:128, 1795-1797;
+// examples/firewall/firewall.go:54-57; examples/tutorial/step08.go:33-35),
+// with the *L3Rules passed per call and swapped by the user at any time
+// (step08.go:38-44).  Layout and protocol: service.hpp.
+//
+// Device side: one wave64 per 64 mailboxes (lane = mailbox), polling with
+// 16-byte sc0 sc1 loads (they bypass L1/L2 and read host memory over PCIe),
+// mailboxes that were busy in the last `hot` window read whole each pass,
+// idle ones read only their tag chunk.  Complete requests are grouped by
+// table generation (wave-uniform descriptor), parsed and classified by the
+// same device functions as the batch kernels (classify.hpp), and answered
+// with ONE 8-byte system-scope store {tag, port} per request.  The kernel
+// leaves after `idle` without requests, after `life` in total, or when the
+// host sets the stop word, so every wave reaches its exit on its own.
+//
+// Host side: a caller owns a mailbox (thread-local assignment), writes the
+// eight chunks with aligned 16-byte stores (tag chunk last), and spins on its
+// response word.  An armer thread launches the kernel when a caller finds it
+// not running (a Dekker pair: the caller stores its request and then reads
+// `running`; the armer clears `running` after the kernel has exited and then
+// re-scans the mailboxes — one of the two always sees the other).
+#include <hip/hip_runtime.h>
+#include <immintrin.h>
+#include <sched.h>
+#include <sys/prctl.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cctype>
+#include <chrono>
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <new>
+#include <set>
+#include <string>
+#include <thread>
+
+#include "classify.hpp"
+#include "compile.hpp"
+#include "devutil.hpp"
+#include "engine.hpp"
+#include "rules.hpp"
+#include "service.hpp"
+
+namespace nffacl {
+namespace dev {
+
+struct SvcArgs {
+    const uint8_t *box;     // device alias of the mailboxes (kSvcBoxBytes each)
+    uint64_t *resp;         // device alias of the responses (kSvcRespStride words each)
+    const uint32_t *ctrl;   // ctrl[0] != 0: stop
+    uint32_t box_bytes;     // bytes of the mailbox array (buffer range)
+    uint64_t idle_ticks;    // leave after this long without a request (wall clock ticks)
+    uint64_t hot_ticks;     // a mailbox answered within this window is read whole every pass
+    uint64_t life_ticks;    // leave after this long in any case
+};
+
+// One 16-byte chunk of host memory, sc0 sc1 (past L1 and L2: host memory
+// written by the CPU is never served stale from a cache).
+__device__ __forceinline__ u32x4 ld16_host(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
+    return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>(off), 0, 17));
+}
+
+// Classify one group (wave-uniform descriptor `w`, table `tab`).
+__device__ __forceinline__ uint32_t svc_classify(const uint32_t (&w)[kSvcDescDwords], const uint32_t *tab,
+                                                 const Fields &f, FlatScratch<2> &W, uint32_t lane) {
+    const uint32_t kind = w[0], ns = w[1];
+    if (kind == kSvcLinear) return classify_linear(f, tab + w[4], w[5], tab + w[6], w[7]);
+    IndexedArgs a{};
+    a.tab = tab;
+    a.dir8 = w[3];
+    a.generic = 0;
+#pragma unroll
+    for (int fam = 0; fam < 2; ++fam) {
+        FamArgs &fa = fam ? a.f6 : a.f4;
+        const uint32_t b = 8 + 20 * fam;
+        fa.off_resid = w[b + 0];
+        fa.n_resid = w[b + 1];
+        fa.off_cold = w[b + 2];
+        fa.off_ent_base = w[b + 3];
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+            fa.slot[s] = SlotArgs{w[b + 4 + 4 * s], w[b + 5 + 4 * s], w[b + 6 + 4 * s], w[b + 7 + 4 * s],
+                                  static_cast<uint32_t>(s), kFZero, 0, 0};
+    }
+    if (kind == kSvcIndexed) {
+        if (ns == 2) return classify_indexed<2, 1>(GlobalTab{tab}, a, f);
+        if (ns == 3) return classify_indexed<3, 1>(GlobalTab{tab}, a, f);
+        return classify_indexed<4, 1>(GlobalTab{tab}, a, f);
+    }
+    if (kind == kSvcFlat) {
+        if (ns == 2) return classify_flat<2, 2, true, false, false>(a, f, W, lane);
+        if (ns == 3) return classify_flat<3, 2, true, false, false>(a, f, W, lane);
+        return classify_flat<4, 2, true, false, false>(a, f, W, lane);
+    }
+    return 0u;
+}
+
+__global__ void __launch_bounds__(64) k_service(SvcArgs a) {
+    __shared__ FlatScratch<2> W;
+    const uint32_t lane = lane_id();
+    const uint32_t mb = blockIdx.x * 64u + lane;  // mailboxes come in whole waves
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(a.box), 0,
+                                                                        static_cast<int>(a.box_bytes), 0x00020000);
+    const uint32_t box = mb * kSvcBoxBytes;
+    uint64_t *resp = a.resp + size_t(mb) * kSvcRespStride;
+    uint32_t done = static_cast<uint32_t>(__hip_atomic_load(resp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >> 32);
+    const uint64_t t0 = wall_clock64();
+    uint64_t last = t0, lane_last = t0;  // hot at start: the call that armed us is read whole
+    uint32_t cur_key = 0xFFFFFFFFu;  // generation << 1 | vlan of the descriptor in `w`
+    uint32_t w[kSvcDescDwords];
+#pragma unroll
+    for (uint32_t i = 0; i < kSvcDescDwords; ++i) w[i] = 0;
+    const uint32_t *tab = nullptr;
+    while (true) {
+        const uint64_t now = wall_clock64();
+        if (now - t0 > a.life_ticks) break;
+        const bool hot = now - lane_last <= a.hot_ticks;
+        u32x4 c[kSvcChunks];
+#pragma unroll
+        for (uint32_t j = 0; j < kSvcChunks; ++j) c[j] = u32x4{0, 0, 0, 0};
+        if (hot) {
+#pragma unroll
+            for (uint32_t j = 0; j < kSvcChunks; ++j) c[j] = ld16_host(rs, box + 16u * j);
+        } else {
+            c[kSvcChunks - 1] = ld16_host(rs, box + 16u * (kSvcChunks - 1));
+        }
+        uint32_t stop = 0;
+        if (lane == 0) stop = __hip_atomic_load(a.ctrl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (__builtin_amdgcn_readlane(stop, 0) != 0u) break;
+        const uint32_t tag = c[kSvcChunks - 1].w;
+        const bool fresh = tag != done;
+        // a cold mailbox with a new tag turns hot: read whole on the next pass
+        if (!hot && fresh) lane_last = now;
+        bool pend = hot && fresh;
+#pragma unroll
+        for (uint32_t j = 0; j + 1 < kSvcChunks; ++j) pend = pend && c[j].w == tag;  // untorn
+        uint64_t m = ballot(pend);
+        if (!ballot(fresh)) {
+            if (now - last > a.idle_ticks) break;
+            continue;
+        }
+        last = now;
+        while (m) {
+            const uint32_t first = static_cast<uint32_t>(__builtin_ctzll(m));
+            const uint32_t key = __builtin_amdgcn_readlane(c[kSvcChunks - 1].z, first);
+            const bool mine = pend && c[kSvcChunks - 1].z == key;
+            if (key != cur_key) {
+                // a table this wave has not walked yet (or a reused address):
+                // system-scope acquire (L1 and L2 invalidated), then its
+                // descriptor through plain vector loads, never the scalar cache
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+                const uint64_t lo = __builtin_amdgcn_readlane(c[kSvcChunks - 1].x, first);
+                const uint64_t hi = __builtin_amdgcn_readlane(c[kSvcChunks - 1].y, first);
+                const volatile uint32_t *dp = reinterpret_cast<const volatile uint32_t *>(hi << 32 | lo);
+#pragma unroll
+                for (uint32_t i = 0; i < kSvcDescDwords; ++i) w[i] = __builtin_amdgcn_readfirstlane(dp[i]);
+                tab = reinterpret_cast<const uint32_t *>(hi << 32 | lo) - w[2];
+                cur_key = key;
+            }
+            uint32_t full[3 * kSvcPktChunks], d[16];
+#pragma unroll
+            for (uint32_t j = 0; j < kSvcPktChunks; ++j) {
+                full[3 * j + 0] = c[j].x;
+                full[3 * j + 1] = c[j].y;
+                full[3 * j + 2] = c[j].z;
+            }
+#pragma unroll
+            for (int k = 0; k < 16; ++k) d[k] = full[k];
+            Fields f;
+            parse_fields<true>(d, mine, f, [&](uint32_t k, uint32_t &lo, uint32_t &hi) {
+                lo = 0;
+                hi = 0;
+#pragma unroll
+                for (uint32_t j = 0; j < 3 * kSvcPktChunks; ++j) {
+                    lo = k == j ? full[j] : lo;
+                    hi = k + 1 == j ? full[j] : hi;
+                }
+            }, key & 1u ? uint32_t(NFFACL_PARSE_VLAN) : 0u);
+            const uint32_t port = svc_classify(w, tab, f, W, lane);
+            if (mine) {
+                __hip_atomic_store(resp, uint64_t(tag) << 32 | port, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                done = tag;
+                lane_last = now;
+            }
+            pend = pend && !mine;
+            m = ballot(pend);
+        }
+    }
+}
+
+}  // namespace dev
+
+// ---- per-rule-set device tables -----------------------------------------------
+
+namespace {
+
+// One table home per device for the rule-set tables (uploads + stream-ordered
+// retirement), created on first use and kept for the life of the process.
+TableHome *rules_home(int dev) {
+    static std::once_flag once[kMaxDevices];
+    static TableHome *homes[kMaxDevices];
+    std::call_once(once[dev], [dev] {
+        auto *h = new TableHome();
+        if (h->init(dev) != hipSuccess) {
+            (void)hipGetLastError();
+            delete h;
+            h = nullptr;
+        }
+        homes[dev] = h;
+    });
+    return homes[dev];
+}
+
+struct DeviceRestore {
+    int old = -1;
+    explicit DeviceRestore(int dev) {
+        if (hipGetDevice(&old) != hipSuccess) old = -1;
+        if (old != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceRestore() {
+        if (old >= 0) (void)hipSetDevice(old);
+    }
+};
+
+}  // namespace
+
+DevTable *rules_table(const nffacl_rules *r, int dev, int &st) {
+    st = NFFACL_OK;
+    if (!r || dev < 0 || dev >= kMaxDevices) {
+        st = NFFACL_ERR_INVALID_ARG;
+        return nullptr;
+    }
+    DevTable *t = r->dev[dev].load(std::memory_order_acquire);
+    if (t) return t;
+    std::lock_guard<std::mutex> g(r->dev_mu);
+    t = r->dev[dev].load(std::memory_order_relaxed);
+    if (t) return t;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
+        (void)hipGetLastError();
+        set_last_error("no HIP device visible");
+        st = NFFACL_ERR_NO_DEVICE;
+        return nullptr;
+    }
+    if (dev >= count) {
+        st = NFFACL_ERR_INVALID_ARG;
+        return nullptr;
+    }
+    DeviceRestore ds(dev);
+    if ((st = prepare_kernels()) != NFFACL_OK) return nullptr;
+    TableHome *home = rules_home(dev);
+    if (!home) {
+        set_last_error("rules table home: stream creation failed");
+        st = NFFACL_ERR_HIP;
+        return nullptr;
+    }
+    home->reap(false);
+    // default layout (no tuning knobs): the forms the scalar consumer walks
+    auto *nt = new (std::nothrow) DevTable();
+    if (!nt) {
+        st = NFFACL_ERR_NOMEM;
+        return nullptr;
+    }
+    st = compile_upload(*r, NFFACL_ALGO_AUTO, CompileOptions{}, *home, *nt);
+    if (st != NFFACL_OK) {
+        delete nt;
+        return nullptr;
+    }
+    r->dev[dev].store(nt, std::memory_order_release);
+    return nt;
+}
+
+void release_rules_tables(const nffacl_rules *r) {
+    for (int dev = 0; dev < kMaxDevices; ++dev) {
+        DevTable *t = r->dev[dev].exchange(nullptr, std::memory_order_acq_rel);
+        if (!t) continue;
+        delete t;  // retires stream-ordered behind the batch launches that used it (tables.hpp)
+        if (TableHome *h = rules_home(dev)) h->reap(false);
+    }
+}
+
+}  // namespace nffacl
+
+// ---- the service object ---------------------------------------------------------
+
+using namespace nffacl;
+using Clock = std::chrono::steady_clock;
+
+namespace {
+
+struct alignas(64) MailboxState {
+    std::atomic<uint32_t> lock{0};  // owner (threads beyond the mailbox count share)
+    uint32_t seq = 0;               // last tag posted
+};
+
+}  // namespace
+
+struct nffacl_service {
+    int device = 0;
+    uint32_t id = 0;  // process-unique: keys the callers' thread-local mailbox choice
+    uint32_t n_mb = 0;
+    uint64_t timeout_us = 1000000;
+    uint8_t *h_mem = nullptr;  // mapped, coherent pinned host memory: boxes | responses | ctrl
+    uint8_t *h_box = nullptr;
+    uint64_t *h_resp = nullptr;
+    uint32_t *h_ctrl = nullptr;
+    dev::SvcArgs args{};
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;
+    std::unique_ptr<MailboxState[]> mbx;
+    std::atomic<uint32_t> next_mb{0};
+    std::atomic<bool> running{false};
+    std::atomic<int> error{NFFACL_OK};
+    std::mutex mu;
+    std::condition_variable cv;
+    bool kick = false, stop = false;
+    std::thread armer;
+    std::atomic<uint64_t> launches{0}, requests{0}, timeouts{0};
+};
+
+namespace {
+
+// Live services, stopped at process exit (a kernel still polling host memory
+// that the exiting process unmaps would fault).
+std::mutex g_live_mu;
+std::set<nffacl_service *> *g_live = nullptr;
+std::atomic<uint32_t> g_next_id{1};
+
+void stop_kernel(nffacl_service *s) {
+    __atomic_store_n(s->h_ctrl, 1u, __ATOMIC_RELEASE);
+    {
+        std::lock_guard<std::mutex> g(s->mu);
+        s->stop = true;
+    }
+    s->cv.notify_all();
+    if (s->armer.joinable()) s->armer.join();
+}
+
+void stop_all_at_exit() {
+    std::lock_guard<std::mutex> g(g_live_mu);
+    if (!g_live) return;
+    for (nffacl_service *s : *g_live) stop_kernel(s);
+}
+
+uint32_t box_tag(const nffacl_service *s, uint32_t i) {
+    return __atomic_load_n(reinterpret_cast<const uint32_t *>(s->h_box + size_t(i) * kSvcBoxBytes + kSvcBoxBytes - 4),
+                           __ATOMIC_ACQUIRE);
+}
+
+uint32_t resp_tag(const nffacl_service *s, uint32_t i) {
+    return static_cast<uint32_t>(__atomic_load_n(s->h_resp + size_t(i) * kSvcRespStride, __ATOMIC_ACQUIRE) >> 32);
+}
+
+bool any_pending(const nffacl_service *s) {
+    for (uint32_t i = 0; i < s->n_mb; ++i)
+        if (box_tag(s, i) != resp_tag(s, i)) return true;
+    return false;
+}
+
+void armer_main(nffacl_service *s) {
+    (void)hipSetDevice(s->device);
+    std::unique_lock<std::mutex> lk(s->mu);
+    while (true) {
+        s->cv.wait(lk, [&] { return s->kick || s->stop; });
+        if (s->stop) break;
+        s->kick = false;
+        lk.unlock();
+        s->running.store(true, std::memory_order_seq_cst);
+        hipLaunchKernelGGL(dev::k_service, dim3(s->n_mb / 64), dim3(64), 0, s->stream, s->args);
+        hipError_t e = hipGetLastError();
+        if (e == hipSuccess) e = hipEventRecord(s->done, s->stream);
+        if (e == hipSuccess) {
+            s->launches.fetch_add(1, std::memory_order_relaxed);
+            e = hipEventSynchronize(s->done);  // blocking-sync event: the armer sleeps
+        }
+        if (e != hipSuccess) s->error.store(NFFACL_ERR_HIP, std::memory_order_release);
+        s->running.store(false, std::memory_order_seq_cst);
+        lk.lock();
+        // a request posted after the kernel's last poll: launch again at once
+        if (e == hipSuccess && any_pending(s)) s->kick = true;
+    }
+}
+
+void kick(nffacl_service *s) {
+    {
+        std::lock_guard<std::mutex> g(s->mu);
+        s->kick = true;
+    }
+    s->cv.notify_one();
+}
+
+// This thread's mailbox of service `s` (assigned on first use, round robin).
+uint32_t my_mailbox(nffacl_service *s) {
+    struct Slot {
+        uint32_t id = 0, mb = 0;
+    };
+    thread_local Slot cache[4];
+    thread_local uint32_t victim = 0;
+    for (Slot &c : cache)
+        if (c.id == s->id) return c.mb;
+    Slot &c = cache[victim++ % 4];
+    c.id = s->id;
+    c.mb = s->next_mb.fetch_add(1, std::memory_order_relaxed) % s->n_mb;
+    return c.mb;
+}
+
+void release_service(nffacl_service *s) {
+    if (s->done) (void)hipEventDestroy(s->done);
+    if (s->stream) (void)hipStreamDestroy(s->stream);
+    if (s->h_mem) (void)hipHostFree(s->h_mem);
+    delete s;
+}
+
+}  // namespace
+
+namespace {
+
+// NUMA node of every HIP device (from its PCI function's sysfs entry), read once.
+struct DeviceNodes {
+    int count = 0;
+    int node[kMaxDevices];
+};
+
+const DeviceNodes &device_nodes() {
+    static DeviceNodes dn;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        int count = 0;
+        if (hipGetDeviceCount(&count) != hipSuccess) {
+            (void)hipGetLastError();
+            count = 0;
+        }
+        dn.count = std::min(count, kMaxDevices);
+        for (int d = 0; d < dn.count; ++d) {
+            dn.node[d] = -1;
+            char bus[64] = {0};
+            if (hipDeviceGetPCIBusId(bus, sizeof bus, d) != hipSuccess) {
+                (void)hipGetLastError();
+                continue;
+            }
+            for (char *c = bus; *c; ++c) *c = static_cast<char>(std::tolower(static_cast<unsigned char>(*c)));
+            const std::string path = std::string("/sys/bus/pci/devices/") + bus + "/numa_node";
+            if (FILE *f = std::fopen(path.c_str(), "r")) {
+                int n = -1;
+                if (std::fscanf(f, "%d", &n) == 1) dn.node[d] = n;
+                std::fclose(f);
+            }
+        }
+    });
+    return dn;
+}
+
+}  // namespace
+
+extern "C" {
+
+int nffacl_local_device(void) {
+    const DeviceNodes &dn = device_nodes();
+    if (dn.count <= 0) return NFFACL_ERR_NO_DEVICE;
+    unsigned cpu = 0, node = 0;
+    if (getcpu(&cpu, &node) != 0) return 0;
+    for (int d = 0; d < dn.count; ++d)
+        if (dn.node[d] == static_cast<int>(node)) return d;
+    return 0;
+}
+
+int nffacl_rules_prepare(const nffacl_rules *rules, int hip_device) {
+    int st = NFFACL_OK;
+    (void)rules_table(rules, hip_device, st);
+    return st;
+}
+
+int nffacl_service_create(int hip_device, uint32_t mailboxes, uint32_t idle_us, nffacl_service **out) {
+    if (!out) return NFFACL_ERR_INVALID_ARG;
+    *out = nullptr;
+    if (mailboxes == 0) mailboxes = 128;
+    if (mailboxes % 64 != 0 || mailboxes > 4096 || idle_us > 10000000u) return NFFACL_ERR_INVALID_ARG;
+    if (idle_us == 0) idle_us = 2000;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
+        (void)hipGetLastError();
+        set_last_error("no HIP device visible");
+        return NFFACL_ERR_NO_DEVICE;
+    }
+    if (hip_device < 0 || hip_device >= count || hip_device >= kMaxDevices) return NFFACL_ERR_INVALID_ARG;
+    HIP_TRY(hipSetDevice(hip_device));
+    int khz = 0;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, hip_device) != hipSuccess || khz <= 0) {
+        (void)hipGetLastError();
+        khz = 100000;  // gfx9 s_memrealtime: 100 MHz
+    }
+    nffacl_service *s = new (std::nothrow) nffacl_service();
+    if (!s) return NFFACL_ERR_NOMEM;
+    s->device = hip_device;
+    s->id = g_next_id.fetch_add(1, std::memory_order_relaxed);
+    s->n_mb = mailboxes;
+    s->mbx.reset(new (std::nothrow) MailboxState[mailboxes]);
+    const size_t box_bytes = size_t(mailboxes) * kSvcBoxBytes;
+    const size_t resp_bytes = size_t(mailboxes) * kSvcRespStride * 8;
+    const size_t bytes = box_bytes + resp_bytes + 64;
+    hipError_t e = s->mbx ? hipSuccess : hipErrorOutOfMemory;
+    if (e == hipSuccess)
+        e = hipHostMalloc(reinterpret_cast<void **>(&s->h_mem), bytes, hipHostMallocMapped | hipHostMallocCoherent);
+    uint8_t *d_mem = nullptr;
+    if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void **>(&d_mem), s->h_mem, 0);
+    int lo = 0, hi = 0;
+    if (e == hipSuccess) e = hipDeviceGetStreamPriorityRange(&lo, &hi);
+    // its own (highest-priority) stream: kept off the queues of batch work
+    if (e == hipSuccess) e = hipStreamCreateWithPriority(&s->stream, hipStreamNonBlocking, hi);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&s->done, hipEventBlockingSync | hipEventDisableTiming);
+    if (e != hipSuccess) {
+        set_last_error(std::string("service: ") + hipGetErrorString(e));
+        release_service(s);
+        return e == hipErrorOutOfMemory ? NFFACL_ERR_NOMEM : NFFACL_ERR_HIP;
+    }
+    std::memset(s->h_mem, 0, bytes);
+    s->h_box = s->h_mem;
+    s->h_resp = reinterpret_cast<uint64_t *>(s->h_mem + box_bytes);
+    s->h_ctrl = reinterpret_cast<uint32_t *>(s->h_mem + box_bytes + resp_bytes);
+    const uint64_t tpu = uint64_t(khz) / 1000;  // ticks per µs
+    s->args.box = d_mem;
+    s->args.resp = reinterpret_cast<uint64_t *>(d_mem + box_bytes);
+    s->args.ctrl = reinterpret_cast<const uint32_t *>(d_mem + box_bytes + resp_bytes);
+    s->args.box_bytes = static_cast<uint32_t>(box_bytes);
+    s->args.idle_ticks = uint64_t(idle_us) * tpu;
+    s->args.hot_ticks = 200 * tpu;
+    s->args.life_ticks = 100000 * tpu;  // 100 ms, then the armer re-launches if calls keep coming
+    {
+        std::lock_guard<std::mutex> g(g_live_mu);
+        if (!g_live) {
+            g_live = new std::set<nffacl_service *>();
+            std::atexit(stop_all_at_exit);
+        }
+        g_live->insert(s);
+    }
+    s->armer = std::thread(armer_main, s);
+    *out = s;
+    return NFFACL_OK;
+}
+
+int nffacl_service_classify(nffacl_service *s, const nffacl_rules *rules, const uint8_t *frame, uint32_t len,
+                            uint32_t flags, uint32_t *port) {
+    if (!s || !rules || (!frame && len) || (flags & ~uint32_t(NFFACL_PARSE_VLAN)) != 0) return NFFACL_ERR_INVALID_ARG;
+    int st = s->error.load(std::memory_order_acquire);
+    if (st != NFFACL_OK) return st;
+    DevTable *t = rules_table(rules, s->device, st);
+    if (!t) return st;
+    if (t->svc_kind == kSvcNone) return NFFACL_ERR_UNSUPPORTED;
+    const uint32_t mb = my_mailbox(s);
+    MailboxState &m = s->mbx[mb];
+    while (m.lock.exchange(1, std::memory_order_acquire) != 0) _mm_pause();
+    const uint32_t tag = ++m.seq;
+    // the eight chunks (service.hpp): packet bytes, 12 per chunk, + tag
+    alignas(16) uint8_t bytes[kSvcPktChunks * 12] = {0};
+    const uint32_t n = std::min(len, kSvcSlot);
+    if (n) std::memcpy(bytes, frame, n);
+    alignas(16) uint32_t c[kSvcChunks * 4];
+    for (uint32_t j = 0; j < kSvcPktChunks; ++j) {
+        std::memcpy(&c[4 * j], bytes + 12 * j, 12);
+        c[4 * j + 3] = tag;
+    }
+    const uint64_t desc = reinterpret_cast<uint64_t>(t->d_desc);
+    c[28] = static_cast<uint32_t>(desc);
+    c[29] = static_cast<uint32_t>(desc >> 32);
+    c[30] = t->gen << 1 | (flags & NFFACL_PARSE_VLAN ? 1u : 0u);
+    c[31] = tag;
+    __m128i *dst = reinterpret_cast<__m128i *>(s->h_box + size_t(mb) * kSvcBoxBytes);
+    for (uint32_t j = 0; j < kSvcChunks; ++j)  // ascending: the tag chunk last (x86 stores stay in order)
+        _mm_store_si128(dst + j, _mm_load_si128(reinterpret_cast<const __m128i *>(&c[4 * j])));
+    std::atomic_thread_fence(std::memory_order_seq_cst);  // request visible before `running` is read
+    if (!s->running.load(std::memory_order_seq_cst)) kick(s);
+    const uint64_t *r = s->h_resp + size_t(mb) * kSvcRespStride;
+    uint64_t v = 0;
+    uint32_t spins = 0;
+    Clock::time_point t0{};
+    st = NFFACL_OK;
+    while (true) {
+        v = __atomic_load_n(r, __ATOMIC_ACQUIRE);
+        if (static_cast<uint32_t>(v >> 32) == tag) break;
+        _mm_pause();
+        if ((++spins & 1023u) == 0) {
+            const Clock::time_point now = Clock::now();
+            if (spins == 1024) t0 = now;
+            if ((st = s->error.load(std::memory_order_acquire)) != NFFACL_OK) break;
+            if (!s->running.load(std::memory_order_seq_cst)) kick(s);
+            if (now - t0 > std::chrono::microseconds(s->timeout_us)) {
+                s->timeouts.fetch_add(1, std::memory_order_relaxed);
+                set_last_error("service: no answer within the timeout");
+                st = NFFACL_ERR_TIMEOUT;
+                break;
+            }
+        }
+    }
+    m.lock.store(0, std::memory_order_release);
+    if (st != NFFACL_OK) return st;
+    s->requests.fetch_add(1, std::memory_order_relaxed);
+    if (port) *port = static_cast<uint32_t>(v);
+    return NFFACL_OK;
+}
+
+int nffacl_service_get_stats(nffacl_service *s, nffacl_service_stats *out) {
+    if (!s || !out) return NFFACL_ERR_INVALID_ARG;
+    out->launches = s->launches.load(std::memory_order_relaxed);
+    out->requests = s->requests.load(std::memory_order_relaxed);
+    out->timeouts = s->timeouts.load(std::memory_order_relaxed);
+    out->running = s->running.load(std::memory_order_relaxed) ? 1u : 0u;
+    return NFFACL_OK;
+}
+
+void nffacl_service_destroy(nffacl_service *s) {
+    if (!s) return;
+    {
+        std::lock_guard<std::mutex> g(g_live_mu);
+        if (g_live) g_live->erase(s);
+    }
+    stop_kernel(s);
+    (void)hipSetDevice(s->device);
+    (void)hipStreamSynchronize(s->stream);
+    release_service(s);
+}
+
+}  // extern "C"

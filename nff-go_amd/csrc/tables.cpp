@@ -95,10 +95,11 @@ hipError_t DeviceBlob::upload(TableHome *h, const uint32_t *words, size_t n_word
     home = h;
     bytes = n_words * sizeof(uint32_t);
     void *p = nullptr;
-    hipError_t e = h->pools ? hipMallocAsync(&p, bytes, h->stream) : hipMalloc(&p, bytes);
-    if (e != hipSuccess && h->pools) {  // pool refused: plain allocation, freed after its fence
+    const bool pools = h->pools.load(std::memory_order_acquire);
+    hipError_t e = pools ? hipMallocAsync(&p, bytes, h->stream) : hipMalloc(&p, bytes);
+    if (e != hipSuccess && pools) {  // pool refused: plain allocation, freed after its fence
         (void)hipGetLastError();
-        h->pools = false;
+        h->pools.store(false, std::memory_order_release);
         e = hipMalloc(&p, bytes);
     }
     if (e != hipSuccess) return e;
@@ -121,7 +122,7 @@ DeviceBlob::~DeviceBlob() {
         gr.evs.push_back(u.second);
     }
     if (d_blob) {
-        if (!home->pools || hipFreeAsync(d_blob, home->stream) != hipSuccess) {
+        if (!home->pools.load(std::memory_order_acquire) || hipFreeAsync(d_blob, home->stream) != hipSuccess) {
             (void)hipGetLastError();
             gr.blob = d_blob;  // hipFree once the fence has fired
         }

@@ -17,6 +17,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdint>
 #include <mutex>
 #include <string>
@@ -32,7 +33,9 @@ void set_last_error(const std::string &s);
 struct TableHome {
     int device = 0;
     hipStream_t stream = nullptr;  // non-blocking: never orders against user streams
-    bool pools = false;            // stream-ordered allocator available (hipMallocAsync)
+    // stream-ordered allocator available (hipMallocAsync); cleared by the
+    // first upload it refuses, read by whichever thread retires a table
+    std::atomic<bool> pools{false};
     std::mutex mu;
     struct Grave {
         std::vector<hipEvent_t> evs;  // the retired table's per-stream completion events

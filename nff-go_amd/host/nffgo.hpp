@@ -13,20 +13,27 @@
 //   nffgo::flow::SeparateFunction / SplitFunction flow/flow.go:128, 134
 //   nffgo::flow::ACLSeparator / ACLSplitter      the scalar separator of
 //                                                examples/firewall/firewall.go:54-57
+//   nffgo::flow::RulesPointer                    the atomic *L3Rules of
+//                                                examples/tutorial/step08.go:9, 33-44
 //   nffgo::flow::VectorSeparateFunction          flow/flow.go:131
 //   nffgo::flow::ACLVectorSeparator              the vector separator body of
 //                                                testSingleWorkingFF.go:538-546
 //   nffgo::flow::Aggregator                      burst aggregation for GPU-size batches
 //
 // Every verdict is computed by the HIP kernels of libnffacl; there is no CPU
-// path.  The scalar separator ACLSeparator sends each packet through a
-// shared batcher, so the calls of concurrent clones ride in common GPU
-// batches; one call alone costs a GPU round trip.  Batch
-// through ACLVectorSeparator / Aggregator for throughput.
+// path.  Packet::L3ACLPort / L3ACLPermit — one packet per call, the rule set
+// passed per call, as in the reference — go through the per-GPU persistent
+// consumer (nffacl_service_*: one PCIe round trip, no kernel launch), against
+// the table the rule set itself owns (nffacl_rules_prepare), so a rule reload
+// is the reference's "load new rules, swap the pointer" and nothing else.
+// Bursts go through a shared batcher (ACLVectorSeparator) or an Aggregator.
+// The GPU is the one nearest the calling thread (nffacl_local_device), or the
+// one SetACLDevice chose.
 #pragma once
 
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <cstdint>
 #include <cstring>
 #include <functional>
@@ -81,6 +88,19 @@ using IPv6Address = std::array<uint8_t, 16>;   // types/ipv6.go:13
 
 namespace packet {
 
+// GPU the mirror's calls use: -1 = the one nearest the calling thread
+// (nffacl_local_device), else the device set here (once, at start-up, as a
+// Go program would pass it to flow.SystemInit).
+inline std::atomic<int> &acl_device_setting() {
+    static std::atomic<int> dev{-1};
+    return dev;
+}
+inline void SetACLDevice(int dev) { acl_device_setting().store(dev); }
+inline int ACLDevice() {
+    const int d = acl_device_setting().load(std::memory_order_relaxed);
+    return d >= 0 ? d : nffacl_local_device();
+}
+
 // Owner of an nffacl_rules handle plus, lazily, its compiled device table.
 class L3Rules {
 public:
@@ -109,10 +129,20 @@ public:
         return v;
     }
 
-    // Compiled table on HIP device 0 (first use compiles + uploads).
+    // Compile + upload the rule set's own table on the ACL device now (the
+    // first per-packet call does it otherwise): call it where the rules are
+    // loaded, as step08's reload goroutine would.
+    void Prepare() const {
+        const int st = nffacl_rules_prepare(h_, ACLDevice());
+        if (st != NFFACL_OK)
+            throw std::runtime_error(std::string("nffacl_rules_prepare: ") + nffacl_strerror(st) + " " +
+                                     nffacl_last_error());
+    }
+
+    // Engine (bulk host pipeline) on the ACL device (first use compiles + uploads).
     nffacl_engine *engine(int algo = NFFACL_ALGO_AUTO) const {
         std::call_once(once_, [&] {
-            st_ = nffacl_engine_create_ex(0, h_, algo, &eng_);
+            st_ = nffacl_engine_create_ex(ACLDevice(), h_, algo, &eng_);
             if (st_ != NFFACL_OK) err_ = nffacl_last_error();
         });
         if (st_ != NFFACL_OK)
@@ -193,13 +223,36 @@ inline void L3ACLPortBatch(const Packet *const *pkts, size_t n, uint32_t *ports,
                                  nffacl_last_error());
 }
 
-// acl.go:504 for one packet: a synchronous one-packet GPU call (latency
-// bound).  Clones classifying concurrently should share a
-// flow::SharedBatcher (flow::ACLSeparator) so their packets coalesce.
+namespace detail {
+// One persistent consumer per GPU for the whole process (nffacl_service_*).
+inline nffacl_service *service(int dev) {
+    struct Holder {
+        std::once_flag once;
+        nffacl_service *svc = nullptr;
+        int st = NFFACL_OK;
+        ~Holder() {
+            if (svc) nffacl_service_destroy(svc);
+        }
+    };
+    static Holder holders[16];
+    if (dev < 0 || dev >= 16) throw std::runtime_error("ACL device out of range");
+    Holder &h = holders[dev];
+    std::call_once(h.once, [&] { h.st = nffacl_service_create(dev, 256, 2000, &h.svc); });
+    if (h.st != NFFACL_OK)
+        throw std::runtime_error(std::string("nffacl_service_create: ") + nffacl_strerror(h.st) + " " +
+                                 nffacl_last_error());
+    return h.svc;
+}
+}  // namespace detail
+
+// acl.go:504 for one packet: the calling thread's mailbox of the GPU's
+// persistent consumer, against the rule set's own table.
 inline uint32_t Packet::L3ACLPort(const L3Rules &rules) const {
-    const Packet *p = this;
     uint32_t port = 0;
-    L3ACLPortBatch(&p, 1, &port, rules);
+    const int st = nffacl_service_classify(detail::service(ACLDevice()), rules.handle(), Ether, Len, 0, &port);
+    if (st != NFFACL_OK)
+        throw std::runtime_error(std::string("nffacl_service_classify: ") + nffacl_strerror(st) + " " +
+                                 nffacl_last_error());
     return port;
 }
 
@@ -228,7 +281,7 @@ public:
 
     nffacl_l2engine *engine() const {
         std::call_once(once_, [&] {
-            st_ = nffacl_l2_engine_create(0, h_, &eng_);
+            st_ = nffacl_l2_engine_create(ACLDevice(), h_, &eng_);
             if (st_ != NFFACL_OK) err_ = nffacl_last_error();
         });
         if (st_ != NFFACL_OK)
@@ -345,9 +398,18 @@ inline VectorSplitFunction ACLVectorSplitter(std::shared_ptr<const packet::L3Rul
 }
 
 // One nffacl_batcher per GPU, shared by every flow-function clone: the
-// clones' bursts ride in common GPU batches (INTEGRATION.md, DESIGN.md §4.5).
+// clones' bursts ride in common GPU batches (INTEGRATION.md, DESIGN.md §4.6).
+// The device form takes the rule set per burst (the reference's per-call
+// *L3Rules); the engine form classifies against one engine's active table.
 class SharedBatcher {
 public:
+    explicit SharedBatcher(int device = -1, uint32_t max_batch = 1 << 16, uint32_t max_delay_us = 100,
+                           uint32_t nbuf = 4) {
+        const int st = nffacl_batcher_create_device(device >= 0 ? device : packet::ACLDevice(), packet::kSlot,
+                                                    max_batch, max_delay_us, nbuf, &b_);
+        if (st != NFFACL_OK)
+            throw std::runtime_error(std::string("nffacl_batcher_create_device: ") + nffacl_strerror(st));
+    }
     SharedBatcher(std::shared_ptr<const packet::L3Rules> rules, uint32_t max_batch = 1 << 16,
                   uint32_t max_delay_us = 100, uint32_t nbuf = 4)
         : rules_(std::move(rules)) {
@@ -359,8 +421,9 @@ public:
     SharedBatcher &operator=(const SharedBatcher &) = delete;
     ~SharedBatcher() { nffacl_batcher_destroy(b_); }
 
-    // L3ACLPort of n packets (blocks until their batch is back).
-    void Classify(const packet::Packet *const *pkts, size_t n, uint32_t *ports) {
+    // L3ACLPort of n packets against `rules` (device form), or the engine's
+    // table (rules == nullptr, engine form); blocks until their batch is back.
+    void Classify(const packet::L3Rules *rules, const packet::Packet *const *pkts, size_t n, uint32_t *ports) {
         const uint8_t *frames[vBurstSize];
         uint32_t lens[vBurstSize];
         for (size_t off = 0; off < n; off += vBurstSize) {
@@ -369,12 +432,15 @@ public:
                 frames[i] = pkts[off + i]->Ether;
                 lens[i] = pkts[off + i]->Len;
             }
-            const int st = nffacl_batcher_classify(b_, frames, lens, static_cast<uint32_t>(m), ports + off);
+            const int st = rules ? nffacl_batcher_classify_rules(b_, rules->handle(), frames, lens,
+                                                                 static_cast<uint32_t>(m), ports + off)
+                                 : nffacl_batcher_classify(b_, frames, lens, static_cast<uint32_t>(m), ports + off);
             if (st != NFFACL_OK)
                 throw std::runtime_error(std::string("nffacl_batcher_classify: ") + nffacl_strerror(st) + " " +
                                          nffacl_last_error());
         }
     }
+    void Classify(const packet::Packet *const *pkts, size_t n, uint32_t *ports) { Classify(nullptr, pkts, n, ports); }
     nffacl_batcher_stats Stats() const {
         nffacl_batcher_stats s{};
         nffacl_batcher_get_stats(b_, &s);
@@ -382,32 +448,49 @@ public:
     }
 
 private:
-    std::shared_ptr<const packet::L3Rules> rules_;  // keeps the engine alive
+    std::shared_ptr<const packet::L3Rules> rules_;  // engine form: keeps the engine alive
     nffacl_batcher *b_ = nullptr;
 };
 
-// firewall.go:54-57's l3Separator (pkt.L3ACLPermit(rules)) for SetSeparator:
-// each call is a one-packet burst on the shared batcher, so the calls of all
-// clones running the separator coalesce into common GPU batches.
-inline SeparateFunction ACLSeparator(std::shared_ptr<SharedBatcher> batcher) {
-    return [batcher](packet::Packet *pkt) {
-        uint32_t port = 0;
-        const packet::Packet *p = pkt;
-        batcher->Classify(&p, 1, &port);
-        return port > 0;
-    };
+// firewall.go:54-57's l3Separator for SetSeparator: pkt.L3ACLPermit(rules)
+// per call, answered by the GPU's persistent consumer.
+inline SeparateFunction ACLSeparator(std::shared_ptr<const packet::L3Rules> rules) {
+    return [rules](packet::Packet *pkt) { return pkt->L3ACLPermit(*rules); };
 }
 // SetSplitter's per-packet L3ACLPort (examples/forwarding/forwarding.go:49-67).
-inline SplitFunction ACLSplitter(std::shared_ptr<SharedBatcher> batcher) {
-    return [batcher](packet::Packet *pkt) {
-        uint32_t port = 0;
-        const packet::Packet *p = pkt;
-        batcher->Classify(&p, 1, &port);
-        return port;
+inline SplitFunction ACLSplitter(std::shared_ptr<const packet::L3Rules> rules) {
+    return [rules](packet::Packet *pkt) { return pkt->L3ACLPort(*rules); };
+}
+
+// step08.go's `rulesp unsafe.Pointer`: the rule set user code swaps while
+// clones classify (atomic.StorePointer / LoadPointer, step08.go:33-44).  A
+// clone loads the pointer once per call and classifies against exactly that
+// rule set; the old one is freed when its last user drops it (Go's GC).
+class RulesPointer {
+public:
+    explicit RulesPointer(std::shared_ptr<const packet::L3Rules> r) : p_(std::move(r)) {}
+    std::shared_ptr<const packet::L3Rules> Load() const { return std::atomic_load(&p_); }
+    void Store(std::shared_ptr<const packet::L3Rules> r) { std::atomic_store(&p_, std::move(r)); }
+
+private:
+    std::shared_ptr<const packet::L3Rules> p_;
+};
+
+// step08.go:33-35's mySplitter: L3ACLPort against the current rule set.
+inline SplitFunction ACLSplitter(std::shared_ptr<RulesPointer> rulesp) {
+    return [rulesp](packet::Packet *pkt) {
+        const auto local = rulesp->Load();
+        return pkt->L3ACLPort(*local);
+    };
+}
+inline SeparateFunction ACLSeparator(std::shared_ptr<RulesPointer> rulesp) {
+    return [rulesp](packet::Packet *pkt) {
+        const auto local = rulesp->Load();
+        return pkt->L3ACLPermit(*local);
     };
 }
 
-// The vector separator of every clone, backed by one shared batcher.
+// The vector separator of every clone, backed by one shared batcher (engine form).
 inline VectorSeparateFunction ACLVectorSeparator(std::shared_ptr<SharedBatcher> batcher) {
     return [batcher](packet::Packet *const *pkts, const bool *mask, bool *answers) {
         const packet::Packet *sel[vBurstSize];
@@ -420,6 +503,25 @@ inline VectorSeparateFunction ACLVectorSeparator(std::shared_ptr<SharedBatcher> 
         uint32_t ports[vBurstSize] = {0};
         batcher->Classify(sel, n, ports);
         for (size_t k = 0; k < n; ++k) answers[idx[k]] = ports[k] > 0;
+    };
+}
+
+// The same over a device batcher against the current rule set of `rulesp`
+// (step08's pattern in vector form: the pointer is loaded once per burst).
+inline VectorSplitFunction ACLVectorSplitter(std::shared_ptr<SharedBatcher> batcher,
+                                             std::shared_ptr<RulesPointer> rulesp) {
+    return [batcher, rulesp](packet::Packet *const *pkts, const bool *mask, uint8_t *answers) {
+        const auto local = rulesp->Load();
+        const packet::Packet *sel[vBurstSize];
+        int idx[vBurstSize];
+        size_t n = 0;
+        for (int i = 0; i < vBurstSize; ++i) {
+            answers[i] = 0;
+            if (mask[i] && pkts[i]) { sel[n] = pkts[i]; idx[n++] = i; }
+        }
+        uint32_t ports[vBurstSize] = {0};
+        batcher->Classify(local.get(), sel, n, ports);
+        for (size_t k = 0; k < n; ++k) answers[idx[k]] = static_cast<uint8_t>(ports[k]);
     };
 }
 

@@ -53,6 +53,7 @@ ERR_NOMEM = -101
 ERR_HIP = -102
 ERR_NO_DEVICE = -103
 ERR_UNSUPPORTED = -104
+ERR_TIMEOUT = -105
 
 ALGO_AUTO, ALGO_LINEAR, ALGO_INDEXED, ALGO_HYBRID = 0, 1, 2, 3
 PARSE_VLAN = 1  # ParseAllKnownL3CheckVLAN (packet/vlan.go:104-117) instead of ParseAllKnownL3
@@ -126,12 +127,27 @@ class BatcherStats(ctypes.Structure):
 
 
 _batcher_create = _sig("nffacl_batcher_create", _i, _vp, _u32, _u32, _u32, _u32, _pp)
+_batcher_create_device = _sig("nffacl_batcher_create_device", _i, _i, _u32, _u32, _u32, _u32, _pp)
+_batcher_submit_rules = _sig("nffacl_batcher_submit_rules", _i, _vp, _vp, _vp, _vp, _u32, ctypes.POINTER(Ticket))
+_batcher_classify_rules = _sig("nffacl_batcher_classify_rules", _i, _vp, _vp, _vp, _vp, _u32, _vp)
+_batcher_wait_timeout = _sig("nffacl_batcher_wait_timeout", _i, _vp, ctypes.POINTER(Ticket), _vp, _u64)
 _batcher_submit = _sig("nffacl_batcher_submit", _i, _vp, _vp, _vp, _u32, ctypes.POINTER(Ticket))
 _batcher_wait = _sig("nffacl_batcher_wait", _i, _vp, ctypes.POINTER(Ticket), _vp)
 _batcher_classify = _sig("nffacl_batcher_classify", _i, _vp, _vp, _vp, _u32, _vp)
 _batcher_flush = _sig("nffacl_batcher_flush", _i, _vp)
 _batcher_stats = _sig("nffacl_batcher_get_stats", _i, _vp, ctypes.POINTER(BatcherStats))
 _batcher_destroy = _sig("nffacl_batcher_destroy", None, _vp)
+class ServiceStats(ctypes.Structure):
+    _fields_ = [("launches", ctypes.c_uint64), ("requests", ctypes.c_uint64), ("timeouts", ctypes.c_uint64),
+                ("running", ctypes.c_uint64)]
+
+
+_rules_prepare = _sig("nffacl_rules_prepare", _i, _vp, _i)
+_local_device = _sig("nffacl_local_device", _i)
+_service_create = _sig("nffacl_service_create", _i, _i, _u32, _u32, _pp)
+_service_classify = _sig("nffacl_service_classify", _i, _vp, _vp, _vp, _u32, _u32, ctypes.POINTER(_u32))
+_service_stats = _sig("nffacl_service_get_stats", _i, _vp, ctypes.POINTER(ServiceStats))
+_service_destroy = _sig("nffacl_service_destroy", None, _vp)
 _strerror = _sig("nffacl_strerror", ctypes.c_char_p, _i)
 _last_error = _sig("nffacl_last_error", ctypes.c_char_p)
 _abi_version = _sig("nffacl_abi_version", _i)
@@ -153,11 +169,20 @@ EXPORTED_SYMBOLS = [
     "nffacl_l2_classify_frames_device", "nffacl_l2_classify_host",
     "nffacl_batcher_create", "nffacl_batcher_submit", "nffacl_batcher_wait", "nffacl_batcher_classify",
     "nffacl_batcher_flush", "nffacl_batcher_get_stats", "nffacl_batcher_destroy",
+    "nffacl_batcher_create_device", "nffacl_batcher_submit_rules", "nffacl_batcher_classify_rules",
+    "nffacl_batcher_wait_timeout", "nffacl_local_device",
+    "nffacl_rules_prepare", "nffacl_service_create", "nffacl_service_classify", "nffacl_service_get_stats",
+    "nffacl_service_destroy",
 ]
 
 
 def abi_version() -> int:
     return _abi_version()
+
+
+def local_device() -> int:
+    """nffacl_local_device: the HIP device on the calling thread's NUMA node."""
+    return _local_device()
 
 
 class NFError(Exception):
@@ -267,6 +292,12 @@ class L3Rules:
             _rules_get6(self._h, i, a[i:i + 1].ctypes.data)
         return a
 
+    def prepare(self, device: int = 0):
+        """Compile + upload this rule set's own device table now (else on first use)."""
+        st = _rules_prepare(self._h, device)
+        if st != OK:
+            _raise(st, "nffacl_rules_prepare")
+
 
 def GetL3ACLFromTextTable(filename):
     """(rules, err) like the Go API; rules is None on error."""
@@ -369,10 +400,16 @@ class Batcher:
     reference's VectorSeparateFunction (flow.go:131) shared by many threads.
     ctypes drops the GIL during the calls, so Python threads really overlap."""
 
-    def __init__(self, engine: "Engine", stride: int = 80, max_batch: int = 1 << 16,
-                 max_delay_us: int = 100, nbuf: int = 4):
+    def __init__(self, engine: "Engine | None", stride: int = 80, max_batch: int = 1 << 16,
+                 max_delay_us: int = 100, nbuf: int = 4, device: int | None = None):
+        """An engine batcher (`engine`), or with engine=None and `device` a
+        device batcher whose bursts name their rule set (classify(..., rules=))."""
         out = ctypes.c_void_p()
-        st = _batcher_create(engine._h, stride, max_batch, max_delay_us, nbuf, ctypes.byref(out))
+        if engine is None and device is not None:
+            st = _batcher_create_device(device, stride, max_batch, max_delay_us, nbuf, ctypes.byref(out))
+        else:
+            st = _batcher_create(engine._h if engine is not None else None, stride, max_batch, max_delay_us, nbuf,
+                                 ctypes.byref(out))
         if st != OK:
             _raise(st, "nffacl_batcher_create")
         self._h = out.value
@@ -403,26 +440,37 @@ class Batcher:
         ptrs = (base + np.asarray(offsets, np.uint64)).astype(np.uint64)
         return ptrs, np.ascontiguousarray(lens, np.uint32)
 
-    def classify(self, ptrs: np.ndarray, lens: np.ndarray | None) -> np.ndarray:
+    def classify(self, ptrs: np.ndarray, lens: np.ndarray | None, rules: "L3Rules | None" = None) -> np.ndarray:
         n = len(ptrs)
         ports = np.zeros(n, np.uint32)
-        st = _batcher_classify(self._h, ptrs.ctypes.data, None if lens is None else lens.ctypes.data, n,
-                               ports.ctypes.data)
+        lp = None if lens is None else lens.ctypes.data
+        if rules is None:
+            st = _batcher_classify(self._h, ptrs.ctypes.data, lp, n, ports.ctypes.data)
+        else:
+            st = _batcher_classify_rules(self._h, rules.handle, ptrs.ctypes.data, lp, n, ports.ctypes.data)
         if st != OK:
             _raise(st, "nffacl_batcher_classify")
         return ports
 
-    def submit(self, ptrs: np.ndarray, lens: np.ndarray | None) -> Ticket:
+    def submit(self, ptrs: np.ndarray, lens: np.ndarray | None, rules: "L3Rules | None" = None) -> Ticket:
         t = Ticket()
-        st = _batcher_submit(self._h, ptrs.ctypes.data, None if lens is None else lens.ctypes.data, len(ptrs),
-                             ctypes.byref(t))
+        lp = None if lens is None else lens.ctypes.data
+        if rules is None:
+            st = _batcher_submit(self._h, ptrs.ctypes.data, lp, len(ptrs), ctypes.byref(t))
+        else:
+            st = _batcher_submit_rules(self._h, rules.handle, ptrs.ctypes.data, lp, len(ptrs), ctypes.byref(t))
         if st != OK:
             _raise(st, "nffacl_batcher_submit")
         return t
 
-    def wait(self, t: Ticket) -> np.ndarray:
+    def wait(self, t: Ticket, timeout_us: int | None = None) -> np.ndarray:
+        """Verdicts of a submitted burst; with timeout_us, NFError(ERR_TIMEOUT)
+        if its batch is not done by then (the ticket stays valid)."""
         ports = np.zeros(t.n, np.uint32)
-        st = _batcher_wait(self._h, ctypes.byref(t), ports.ctypes.data)
+        if timeout_us is None:
+            st = _batcher_wait(self._h, ctypes.byref(t), ports.ctypes.data)
+        else:
+            st = _batcher_wait_timeout(self._h, ctypes.byref(t), ports.ctypes.data, timeout_us)
         if st != OK:
             _raise(st, "nffacl_batcher_wait")
         return ports
@@ -436,6 +484,60 @@ class Batcher:
         s = BatcherStats()
         _batcher_stats(self._h, ctypes.byref(s))
         return {k: getattr(s, k) for k, _ in BatcherStats._fields_}
+
+
+class Service:
+    """Persistent GPU consumer for one-packet calls (nffacl_service_*): the
+    reference's (*Packet).L3ACLPort / L3ACLPermit called per packet from a
+    SetSeparator / SetSplitter function (acl.go:495-506, flow.go:128), with
+    the rule set passed per call.  ctypes drops the GIL during the call."""
+
+    def __init__(self, device: int = 0, mailboxes: int = 128, idle_us: int = 2000):
+        out = ctypes.c_void_p()
+        st = _service_create(device, mailboxes, idle_us, ctypes.byref(out))
+        if st != OK:
+            _raise(st, "nffacl_service_create")
+        self._h = out.value
+        self.device = device
+
+    def close(self):
+        h, self._h = getattr(self, "_h", None), None
+        if h and _service_destroy is not None:
+            try:
+                _service_destroy(h)
+            except Exception:  # interpreter teardown
+                pass
+
+    def __del__(self):
+        self.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def classify(self, rules: L3Rules, frame, flags: int = 0) -> int:
+        """L3ACLPort of one frame (bytes / uint8 array starting at the Ether header)."""
+        buf = np.frombuffer(bytes(frame), np.uint8) if not isinstance(frame, np.ndarray) else \
+            np.ascontiguousarray(frame, np.uint8)
+        port = _u32()
+        st = _service_classify(self._h, rules.handle, buf.ctypes.data if len(buf) else None, len(buf), flags,
+                               ctypes.byref(port))
+        if st != OK:
+            _raise(st, "nffacl_service_classify")
+        return port.value
+
+    def L3ACLPort(self, rules: L3Rules, frame) -> int:
+        return self.classify(rules, frame)
+
+    def L3ACLPermit(self, rules: L3Rules, frame) -> bool:
+        return self.classify(rules, frame) > 0
+
+    def stats(self) -> dict:
+        s = ServiceStats()
+        _service_stats(self._h, ctypes.byref(s))
+        return {k: getattr(s, k) for k, _ in ServiceStats._fields_}
 
 
 # ---- L2 ACL (acl.go:68-117, 356-383, 457-491) ---------------------------------

@@ -593,10 +593,10 @@ static void TestVectorSeparatorSharedBatcher(T &t) {
                                           (unsigned long long)st.batches, (unsigned long long)st.bursts);
 }
 
-// SetSeparator's scalar call shape (firewall.go:54-57, flow.go:128) through the
-// shared batcher: clones classifying one packet per call coalesce into common
-// GPU batches; every answer must be the single-packet verdict.
-static void TestScalarSeparatorSharedBatcher(T &t) {
+// SetSeparator's scalar call shape (firewall.go:54-57, flow.go:128): clones
+// classifying one packet per call through the GPU's persistent consumer;
+// every answer must be the single-packet verdict.
+static void TestScalarSeparatorService(T &t) {
     const char *dir = std::getenv("NFFACL_GOLDEN");
     const std::string g = dir ? dir : "tests/golden";
     auto split = packet::GetL3ACLFromTextTable(g + "/rules/test-split.conf");
@@ -611,9 +611,8 @@ static void TestScalarSeparatorSharedBatcher(T &t) {
     }
     std::vector<packet::Packet> pk;
     for (auto &p : tp) pk.push_back(p.pkt());
-    auto batcher = std::make_shared<flow::SharedBatcher>(split.first, 4096, 50, 4);
-    auto sep = flow::ACLSeparator(batcher);
-    auto spl = flow::ACLSplitter(batcher);
+    auto sep = flow::ACLSeparator(split.first);
+    auto spl = flow::ACLSplitter(split.first);
     constexpr int kClones = 16, kCalls = 400;
     std::atomic<int> bad{0};
     std::vector<std::thread> clones;
@@ -626,11 +625,88 @@ static void TestScalarSeparatorSharedBatcher(T &t) {
             }
         });
     for (auto &th : clones) th.join();
-    const auto st = batcher->Stats();
     if (bad) t.Errorf("%d wrong answers", bad.load());
-    if (st.bursts != uint64_t(kClones) * kCalls * 2) t.Errorf("bursts %llu", (unsigned long long)st.bursts);
-    if (st.batches >= st.bursts) t.Errorf("no aggregation: %llu batches for %llu calls",
-                                          (unsigned long long)st.batches, (unsigned long long)st.bursts);
+}
+
+// examples/tutorial/step08.go replayed: a reload thread loads a new rule file
+// every few ms (GetL3ACLFromTextTable) and swaps the pointer atomically
+// (step08.go:38-44) while 16 clones classify — one 32-packet burst through
+// the shared device batcher and one scalar L3ACLPort per iteration — each
+// against the rule set it loaded (step08.go:33-35).  Generation k maps dst
+// ports 111/222/333 to outputs rotated by k and port 444 to 10 + k, so every
+// answer names the rule set that produced it.
+static void TestRuleReloadStep08(T &t) {
+    struct Gen {
+        std::shared_ptr<const packet::L3Rules> rules;
+        int k;
+    };
+    auto load_gen = [&](int k) -> std::shared_ptr<const Gen> {
+        std::string text;
+        const int dp[4] = {111, 222, 333, 444};
+        for (int i = 0; i < 4; ++i)
+            text += "ANY ANY ANY ANY " + std::to_string(dp[i]) + " " +
+                    std::to_string(i < 3 ? (i + k) % 3 + 1 : 10 + k) + "\n";
+        const std::string path = tmpfile_with(text, ".conf");
+        auto r = packet::GetL3ACLFromTextTable(path);
+        std::remove(path.c_str());
+        if (r.second) return nullptr;
+        r.first->Prepare();  // compile + upload in the reload thread, not in a clone's call
+        return std::make_shared<const Gen>(Gen{r.first, k});
+    };
+    auto expect = [](int k, int i) -> uint32_t { return i < 3 ? uint32_t((i + k) % 3 + 1) : uint32_t(10 + k); };
+    std::vector<TestPacket> tp;
+    for (int i = 0; i < 4; ++i) {
+        TestPacket p{ipv4Packet(types::UDPNumber, types::UDPLen, true)};
+        const uint16_t dport = i == 0 ? 111 : i == 1 ? 222 : i == 2 ? 333 : 444;
+        p.bytes[36] = uint8_t(dport >> 8);
+        p.bytes[37] = uint8_t(dport);
+        tp.push_back(p);
+    }
+    std::vector<packet::Packet> pk;
+    for (auto &p : tp) pk.push_back(p.pkt());
+    std::shared_ptr<const Gen> cur = load_gen(0);
+    if (!cur) { t.Errorf("cannot load generation 0"); return; }
+    auto batcher = std::make_shared<flow::SharedBatcher>(-1, 4096, 50, 4);
+    constexpr int kClones = 16, kReloads = 40;
+    std::atomic<bool> halt{false};
+    std::atomic<int> bad{0}, bursts{0};
+    std::vector<std::atomic<int>> seen(kReloads + 1);
+    std::vector<std::thread> clones;
+    for (int c = 0; c < kClones; ++c)
+        clones.emplace_back([&, c] {
+            const packet::Packet *burst[flow::vBurstSize];
+            int which[flow::vBurstSize];
+            uint32_t ports[flow::vBurstSize];
+            for (int it = 0; !halt.load(); ++it) {
+                const std::shared_ptr<const Gen> local = std::atomic_load(&cur);  // atomic.LoadPointer
+                for (int i = 0; i < flow::vBurstSize; ++i) {
+                    which[i] = (i + it + c) % 4;
+                    burst[i] = &pk[which[i]];
+                }
+                batcher->Classify(local->rules.get(), burst, flow::vBurstSize, ports);
+                for (int i = 0; i < flow::vBurstSize; ++i)
+                    if (ports[i] != expect(local->k, which[i])) ++bad;
+                const int i = (it + c) % 4;
+                if (pk[i].L3ACLPort(*local->rules) != expect(local->k, i)) ++bad;
+                ++seen[local->k];
+                ++bursts;
+            }
+        });
+    for (int k = 1; k <= kReloads; ++k) {  // updateSeparateRules, time.Sleep shortened
+        std::this_thread::sleep_for(std::chrono::milliseconds(3));
+        auto next = load_gen(k);
+        if (!next) { t.Errorf("cannot load generation %d", k); break; }
+        std::atomic_store(&cur, next);  // atomic.StorePointer; the old set frees with its last user
+    }
+    std::this_thread::sleep_for(std::chrono::milliseconds(3));
+    halt = true;
+    for (auto &th : clones) th.join();
+    int gens = 0;
+    for (auto &s : seen) gens += s.load() > 0;
+    if (bad) t.Errorf("%d answers from the wrong rule set", bad.load());
+    if (gens < kReloads / 2) t.Errorf("only %d of %d generations were classified against", gens, kReloads + 1);
+    const auto st = batcher->Stats();
+    if (st.bursts < uint64_t(bursts.load())) t.Errorf("batcher saw %llu bursts", (unsigned long long)st.bursts);
 }
 
 int main(int argc, char **argv) {
@@ -654,7 +730,8 @@ int main(int argc, char **argv) {
         run("TestInternal_l2ACL_packetIPv4", TestInternal_l2ACL_packetIPv4);
         run("TestInternal_l2ACL_packetARP", TestInternal_l2ACL_packetARP);
         run("TestVectorSeparatorSharedBatcher", TestVectorSeparatorSharedBatcher);
-        run("TestScalarSeparatorSharedBatcher", TestScalarSeparatorSharedBatcher);
+        run("TestScalarSeparatorService", TestScalarSeparatorService);
+        run("TestRuleReloadStep08", TestRuleReloadStep08);
     }
     std::printf(g_failed ? "FAIL\n" : "ok\n");
     return g_failed ? 1 : 0;
