@@ -382,6 +382,8 @@ typedef struct nffacl_service_stats {
     uint64_t requests;  /* calls answered */
     uint64_t timeouts;  /* calls that returned NFFACL_ERR_TIMEOUT */
     uint64_t running;   /* 1 while the consumer kernel is resident */
+    uint64_t table_oob; /* 1 if a table walk ever indexed outside its table (read as 0 instead
+                           of faulting; a compiler/upload bug — the tests require 0) */
 } nffacl_service_stats;
 
 /* mailboxes: a multiple of 64 (one wave each 64; 0 = 128), one per calling

@@ -331,6 +331,10 @@ struct IndexedArgs {
     uint32_t dir8;          // HYBRID: two-level directories carry u8 offsets (SplitTab::bounds)
     uint32_t generic;       // HYBRID flat forms: slots key on SlotArgs::f1/f2 (else slot s on field s)
     FamArgs f4, f6;
+    // persistent consumer (service.hip) only: table size for the bounds
+    // checks of its global-memory walk, and the host word they flag
+    uint32_t tab_dwords;
+    uint32_t *oob;
 };
 
 // Table placement (kernel template argument).
@@ -397,7 +401,11 @@ struct GlobalTab {
 template <bool IN_LDS>
 struct DirTab {
     const uint32_t *__restrict__ p;
-    __device__ __forceinline__ uint32_t ld(uint32_t i) const { return IN_LDS ? lds_tab[i] : p[i]; }
+    uint32_t limit = 0;  // !IN_LDS: words past the table read as 0 (service.hip)
+    __device__ __forceinline__ uint32_t ld(uint32_t i) const {
+        if (IN_LDS) return lds_tab[i];
+        return i < limit ? p[i] : 0u;
+    }
     // two-level directory (table.hpp): dir[t] = base[t >> 6] + dir16[t], or
     // with dir8 (wave-uniform) base[t >> 4] + dir8[t]
     __device__ __forceinline__ void bounds(uint32_t dir, uint32_t dir16, uint32_t t, uint32_t &lo, uint32_t &hi,
@@ -656,6 +664,26 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
                                                   uint32_t lane) {
     const bool v6 = f.is6;
     const bool mine = f.is4 || f.is6;
+    // The persistent consumer (DIRS_IN_LDS == false) reads the table with
+    // bounds checks: a word outside it reads as 0 and raises the host flag
+    // a.oob (reported by nffacl_service_get_stats) instead of faulting.
+    auto g3 = [&](const uint32_t *p) -> u32x3 {
+        if (!DIRS_IN_LDS) {
+            const uint64_t off = static_cast<uint64_t>(p - a.tab);
+            if (off + 3u > a.tab_dwords) {
+                __hip_atomic_store(a.oob, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                return u32x3{0, 0, 0};
+            }
+        }
+        return ld3(p);
+    };
+    auto g1 = [&](uint32_t i) -> uint32_t {
+        if (!DIRS_IN_LDS && i >= a.tab_dwords) {
+            __hip_atomic_store(a.oob, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            return 0u;
+        }
+        return a.tab[i];
+    };
     const uint32_t ks = __builtin_bswap32(f.s[0]), kd = __builtin_bswap32(f.t[0]);
     const uint32_t sport = f.ports & 0xFFFFu, dport = f.ports >> 16;
     // key[f] of a slot field f (SlotField; kFZero and unused slots: 0)
@@ -673,7 +701,7 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
             const uint32_t key = s == kFDst ? kd : s == kFSrc ? ks : s == kFDport ? dport : s == kFSport ? sport : 0u;
             const uint32_t t = key >> (v6 ? s6.shift : s4.shift);
             uint32_t hi;
-            DirTab<DIRS_IN_LDS>{a.tab}.bounds(v6 ? s6.off_dir : s4.off_dir, v6 ? s6.off_dir16 : s4.off_dir16, t, st[s], hi,
+            DirTab<DIRS_IN_LDS>{a.tab, a.tab_dwords}.bounds(v6 ? s6.off_dir : s4.off_dir, v6 ? s6.off_dir16 : s4.off_dir16, t, st[s], hi,
                                    a.dir8 != 0u);
             ln[s] = mine ? hi - st[s] : 0u;
         }
@@ -687,15 +715,15 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
                            (pick(v6 ? s6.f2 : s4.f2) >> (v6 ? s6.shift2 : s4.shift2));
         if (LDS_DIRS) {
             uint32_t hi;
-            DirTab<DIRS_IN_LDS>{a.tab}.bounds(dir, v6 ? s6.off_dir16 : s4.off_dir16, t, st[s], hi, a.dir8 != 0u);
+            DirTab<DIRS_IN_LDS>{a.tab, a.tab_dwords}.bounds(dir, v6 ? s6.off_dir16 : s4.off_dir16, t, st[s], hi, a.dir8 != 0u);
             ln[s] = mine ? hi - st[s] : 0u;
         } else {
             // generalized slots: a family's unused slots (f1 == kFZero) read nothing
             st[s] = 0u;
             ln[s] = 0u;
             if (mine && (v6 ? s6.f1 : s4.f1) != kFZero) {
-                st[s] = a.tab[dir + t];
-                ln[s] = a.tab[dir + t + 1] - st[s];
+                st[s] = g1(dir + t);
+                ln[s] = g1(dir + t + 1) - st[s];
             }
         }
     }
@@ -763,14 +791,14 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
             const uint32_t ent = !UNCOND || valid[j] ? k + static_cast<uint32_t>(static_cast<int32_t>(dp) >> 1) : 0u;
             const uint32_t *e = six[j] && (!UNCOND || valid[j]) ? E6 + ent * kHybEnt6Dwords : E4 + ent * kHybEnt4Dwords;
             if (UNCOND || valid[j]) {
-                A[j] = ld3(e);
-                B[j] = ld3(e + 3);
+                A[j] = g3(e);
+                B[j] = g3(e + 3);
             } else {
                 A[j] = B[j] = u32x3{0, 0, 0};
             }
             if (valid[j] && six[j]) {  // (C, D are read only for valid IPv6 candidates)
-                C[j] = ld3(e + 6);
-                D[j] = ld3(e + 9);
+                C[j] = g3(e + 6);
+                D[j] = g3(e + 9);
             }
         }
         bool pass[RR];
@@ -833,7 +861,7 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
         const uint32_t ew = fam ? kHybEnt6Dwords : kHybEnt4Dwords;
         for (uint32_t i = 0; i < fa.n_resid; ++i) {
             const uint32_t *e = a.tab + fa.off_resid + i * ew;
-            const u32x3 RA = ld3(e), RB = ld3(e + 3);
+            const u32x3 RA = g3(e), RB = g3(e + 3);
             const uint32_t ri = RA.z >> kEntIndexShift;
             const bool want = in_fam && ri < uint32_t(best >> 32);
             if (!ballot(want)) break;  // residual list ascends too
@@ -845,7 +873,7 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
                     sb[q] = __builtin_bswap32(f.s[q]);
                     tb[q] = __builtin_bswap32(f.t[q]);
                 }
-                if (ok) ok = hyb_miss6(ld3(e + 6), ld3(e + 9), RB.z, sb, tb) == 0u;
+                if (ok) ok = hyb_miss6(g3(e + 6), g3(e + 9), RB.z, sb, tb) == 0u;
             }
             best = ok ? (uint64_t(ri) << 32 | (RB.z >> kHybOutShift)) : best;
         }
@@ -856,7 +884,7 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
     const bool rd = hit && out == kHybOutEscape;
     if (ballot(rd)) {
         const uint32_t r = static_cast<uint32_t>(best >> 32);
-        if (rd) out = a.tab[(v6 ? a.f6.off_cold : a.f4.off_cold) + r];
+        if (rd) out = g1((v6 ? a.f6.off_cold : a.f4.off_cold) + r);
     }
     return out;
 }

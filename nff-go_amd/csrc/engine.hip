@@ -345,14 +345,15 @@ static SvcDesc service_desc(const CompiledTable &m) {
     return d;
 }
 
+// Tables uploaded so far (DevTable::gen of the latest).
+static std::atomic<uint32_t> g_table_epoch{0};
+
 int compile_upload(const nffacl_rules &rules, int algo, const CompileOptions &copt, TableHome &home, DevTable &t) {
     std::string err;
     if (!compile_table(rules, algo, copt, t.meta, err)) {
         set_last_error("compile: " + err);
         return NFFACL_ERR_INVALID_ARG;
     }
-    static std::atomic<uint32_t> next_gen{1};
-    t.gen = next_gen.fetch_add(1, std::memory_order_relaxed) & 0x7FFFFFFFu;
     const SvcDesc d = service_desc(t.meta);
     t.svc_kind = d.kind;
     std::vector<uint32_t> words(t.meta.blob);
@@ -365,8 +366,13 @@ int compile_upload(const nffacl_rules &rules, int algo, const CompileOptions &co
     }
     t.bytes = t.meta.blob.size() * sizeof(uint32_t);  // reported size: the table itself
     t.d_desc = t.d_blob + t.meta.blob.size();
+    // the generation is drawn after the upload has completed (service.hip:
+    // a consumer launched after the counter passed it sees the table)
+    t.gen = g_table_epoch.fetch_add(1, std::memory_order_seq_cst) + 1;
     return NFFACL_OK;
 }
+
+uint32_t table_epoch() { return g_table_epoch.load(std::memory_order_seq_cst); }
 
 int upload_table(nffacl_engine *eng, const nffacl_rules &rules, TablePtr &out) {
     auto t = std::make_shared<DevTable>();

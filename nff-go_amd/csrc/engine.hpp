@@ -21,7 +21,7 @@ const char *last_error();
 // followed by the scalar-call consumer's descriptor (service.hpp SvcDesc).
 struct DevTable : DeviceBlob {
     CompiledTable meta;
-    uint32_t gen = 0;                  // process-unique table generation (service.hip)
+    uint32_t gen = 0;                  // upload epoch: process-unique, increasing (service.hip)
     uint32_t svc_kind = 0;             // SvcKind of the layout
     const uint32_t *d_desc = nullptr;  // device address of the SvcDesc
 };
@@ -48,6 +48,8 @@ int engine_shell(int hip_device, nffacl_engine **out);
 // Compile `rules` with `algo` / `copt`, upload blob + service descriptor
 // through `home` (whose device is current), fill `t`.
 int compile_upload(const nffacl_rules &rules, int algo, const CompileOptions &copt, TableHome &home, DevTable &t);
+// Generation of the latest completed table upload.
+uint32_t table_epoch();
 
 }  // namespace nffacl
 

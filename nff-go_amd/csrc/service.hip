@@ -17,6 +17,12 @@
 // with ONE 8-byte system-scope store {tag, port} per request.  The kernel
 // leaves after `idle` without requests, after `life` in total, or when the
 // host sets the stop word, so every wave reaches its exit on its own.
+// Table coherence: a long-lived kernel must not read a table uploaded after
+// it started (a DMA write does not reach a stale line of a reused address in
+// this XCD's L2; a dispatch invalidates the caches).  Table generations are
+// drawn after each upload completes and the armer passes the latest one to
+// every launch; a request for a newer table makes every wave leave (ctrl[1])
+// and the armer re-launches — once per new table, not per call.
 //
 // Host side: a caller owns a mailbox (thread-local assignment), writes the
 // eight chunks with aligned 16-byte stores (tag chunk last), and spins on its
@@ -58,8 +64,9 @@ namespace dev {
 struct SvcArgs {
     const uint8_t *box;     // device alias of the mailboxes (kSvcBoxBytes each)
     uint64_t *resp;         // device alias of the responses (kSvcRespStride words each)
-    const uint32_t *ctrl;   // ctrl[0] != 0: stop
+    uint32_t *ctrl;         // ctrl[0] != 0: stop (host); ctrl[1] != 0: restart (a wave saw a newer table)
     uint32_t box_bytes;     // bytes of the mailbox array (buffer range)
+    uint32_t epoch;         // table generations <= epoch were uploaded before this launch
     uint64_t idle_ticks;    // leave after this long without a request (wall clock ticks)
     uint64_t hot_ticks;     // a mailbox answered within this window is read whole every pass
     uint64_t life_ticks;    // leave after this long in any case
@@ -71,15 +78,43 @@ __device__ __forceinline__ u32x4 ld16_host(__amdgpu_buffer_rsrc_t rs, uint32_t o
     return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>(off), 0, 17));
 }
 
+// INDEXED inline entries read from global memory with bounds checks (a word
+// outside the table reads as 0 and raises the host flag instead of faulting).
+struct CheckedTab {
+    const uint32_t *__restrict__ p;
+    uint32_t limit;
+    uint32_t *oob;
+    __device__ __forceinline__ void flag() const {
+        __hip_atomic_store(oob, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    __device__ __forceinline__ uint32_t ld(uint32_t i) const {
+        if (i < limit) return p[i];
+        flag();
+        return 0u;
+    }
+    __device__ __forceinline__ void bounds(uint32_t dir, uint32_t, uint32_t t, uint32_t &lo, uint32_t &hi,
+                                           bool = false) const {
+        lo = ld(dir + t);
+        hi = ld(dir + t + 1);
+    }
+    __device__ __forceinline__ u32x4 ld4(uint32_t i) const {
+        if (i + 4u <= limit) return reinterpret_cast<const u32x4 *>(p)[i >> 2];
+        flag();
+        return u32x4{0, 0, 0, 0};
+    }
+};
+
 // Classify one group (wave-uniform descriptor `w`, table `tab`).
 __device__ __forceinline__ uint32_t svc_classify(const uint32_t (&w)[kSvcDescDwords], const uint32_t *tab,
-                                                 const Fields &f, FlatScratch<2> &W, uint32_t lane) {
+                                                 const Fields &f, FlatScratch<2> &W, uint32_t lane, uint32_t *oob) {
     const uint32_t kind = w[0], ns = w[1];
     if (kind == kSvcLinear) return classify_linear(f, tab + w[4], w[5], tab + w[6], w[7]);
     IndexedArgs a{};
     a.tab = tab;
     a.dir8 = w[3];
     a.generic = 0;
+    a.tab_dwords = w[2];
+    a.oob = oob;
 #pragma unroll
     for (int fam = 0; fam < 2; ++fam) {
         FamArgs &fa = fam ? a.f6 : a.f4;
@@ -94,9 +129,10 @@ __device__ __forceinline__ uint32_t svc_classify(const uint32_t (&w)[kSvcDescDwo
                                   static_cast<uint32_t>(s), kFZero, 0, 0};
     }
     if (kind == kSvcIndexed) {
-        if (ns == 2) return classify_indexed<2, 1>(GlobalTab{tab}, a, f);
-        if (ns == 3) return classify_indexed<3, 1>(GlobalTab{tab}, a, f);
-        return classify_indexed<4, 1>(GlobalTab{tab}, a, f);
+        const CheckedTab ct{tab, w[2], oob};
+        if (ns == 2) return classify_indexed<2, 1>(ct, a, f);
+        if (ns == 3) return classify_indexed<3, 1>(ct, a, f);
+        return classify_indexed<4, 1>(ct, a, f);
     }
     if (kind == kSvcFlat) {
         if (ns == 2) return classify_flat<2, 2, true, false, false>(a, f, W, lane);
@@ -135,9 +171,12 @@ __global__ void __launch_bounds__(64) k_service(SvcArgs a) {
         } else {
             c[kSvcChunks - 1] = ld16_host(rs, box + 16u * (kSvcChunks - 1));
         }
-        uint32_t stop = 0;
-        if (lane == 0) stop = __hip_atomic_load(a.ctrl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        if (__builtin_amdgcn_readlane(stop, 0) != 0u) break;
+        uint64_t cw = 0;  // stop | restart << 32
+        if (lane == 0) cw = __hip_atomic_load(reinterpret_cast<uint64_t *>(a.ctrl), __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_SYSTEM);
+        if ((__builtin_amdgcn_readlane(static_cast<uint32_t>(cw), 0) |
+             __builtin_amdgcn_readlane(static_cast<uint32_t>(cw >> 32), 0)) != 0u)
+            break;
         const uint32_t tag = c[kSvcChunks - 1].w;
         const bool fresh = tag != done;
         // a cold mailbox with a new tag turns hot: read whole on the next pass
@@ -151,15 +190,23 @@ __global__ void __launch_bounds__(64) k_service(SvcArgs a) {
             continue;
         }
         last = now;
+        bool restart = false;
         while (m) {
             const uint32_t first = static_cast<uint32_t>(__builtin_ctzll(m));
             const uint32_t key = __builtin_amdgcn_readlane(c[kSvcChunks - 1].z, first);
             const bool mine = pend && c[kSvcChunks - 1].z == key;
+            if ((key >> 1) > a.epoch) {
+                // a table uploaded after this launch: its bytes are visible to
+                // a NEW launch (the dispatch invalidates the caches), not
+                // necessarily to this one (a reused address can still sit in
+                // this XCD's L2).  Every wave leaves; the armer re-launches.
+                if (lane == 0) __hip_atomic_store(a.ctrl + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                restart = true;
+                break;
+            }
             if (key != cur_key) {
-                // a table this wave has not walked yet (or a reused address):
-                // system-scope acquire (L1 and L2 invalidated), then its
-                // descriptor through plain vector loads, never the scalar cache
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+                // the descriptor of a table this wave has not walked yet, by
+                // plain vector loads (never through the scalar cache)
                 const uint64_t lo = __builtin_amdgcn_readlane(c[kSvcChunks - 1].x, first);
                 const uint64_t hi = __builtin_amdgcn_readlane(c[kSvcChunks - 1].y, first);
                 const volatile uint32_t *dp = reinterpret_cast<const volatile uint32_t *>(hi << 32 | lo);
@@ -187,7 +234,7 @@ __global__ void __launch_bounds__(64) k_service(SvcArgs a) {
                     hi = k + 1 == j ? full[j] : hi;
                 }
             }, key & 1u ? uint32_t(NFFACL_PARSE_VLAN) : 0u);
-            const uint32_t port = svc_classify(w, tab, f, W, lane);
+            const uint32_t port = svc_classify(w, tab, f, W, lane, a.ctrl + 2);
             if (mine) {
                 __hip_atomic_store(resp, uint64_t(tag) << 32 | port, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 done = tag;
@@ -196,6 +243,7 @@ __global__ void __launch_bounds__(64) k_service(SvcArgs a) {
             pend = pend && !mine;
             m = ballot(pend);
         }
+        if (restart) break;
     }
 }
 
@@ -322,6 +370,7 @@ struct nffacl_service {
     std::atomic<uint32_t> next_mb{0};
     std::atomic<bool> running{false};
     std::atomic<int> error{NFFACL_OK};
+    std::string error_msg;  // under mu: what failed in the armer thread
     std::mutex mu;
     std::condition_variable cv;
     bool kick = false, stop = false;
@@ -377,6 +426,8 @@ void armer_main(nffacl_service *s) {
         s->kick = false;
         lk.unlock();
         s->running.store(true, std::memory_order_seq_cst);
+        __atomic_store_n(&s->h_ctrl[1], 0u, __ATOMIC_SEQ_CST);
+        s->args.epoch = table_epoch();  // every table of this generation or older is in HBM
         hipLaunchKernelGGL(dev::k_service, dim3(s->n_mb / 64), dim3(64), 0, s->stream, s->args);
         hipError_t e = hipGetLastError();
         if (e == hipSuccess) e = hipEventRecord(s->done, s->stream);
@@ -384,9 +435,12 @@ void armer_main(nffacl_service *s) {
             s->launches.fetch_add(1, std::memory_order_relaxed);
             e = hipEventSynchronize(s->done);  // blocking-sync event: the armer sleeps
         }
-        if (e != hipSuccess) s->error.store(NFFACL_ERR_HIP, std::memory_order_release);
         s->running.store(false, std::memory_order_seq_cst);
         lk.lock();
+        if (e != hipSuccess) {
+            s->error_msg = std::string("service consumer: ") + hipGetErrorName(e) + ": " + hipGetErrorString(e);
+            s->error.store(NFFACL_ERR_HIP, std::memory_order_release);
+        }
         // a request posted after the kernel's last poll: launch again at once
         if (e == hipSuccess && any_pending(s)) s->kick = true;
     }
@@ -531,7 +585,7 @@ int nffacl_service_create(int hip_device, uint32_t mailboxes, uint32_t idle_us, 
     const uint64_t tpu = uint64_t(khz) / 1000;  // ticks per µs
     s->args.box = d_mem;
     s->args.resp = reinterpret_cast<uint64_t *>(d_mem + box_bytes);
-    s->args.ctrl = reinterpret_cast<const uint32_t *>(d_mem + box_bytes + resp_bytes);
+    s->args.ctrl = reinterpret_cast<uint32_t *>(d_mem + box_bytes + resp_bytes);
     s->args.box_bytes = static_cast<uint32_t>(box_bytes);
     s->args.idle_ticks = uint64_t(idle_us) * tpu;
     s->args.hot_ticks = 200 * tpu;
@@ -552,8 +606,13 @@ int nffacl_service_create(int hip_device, uint32_t mailboxes, uint32_t idle_us, 
 int nffacl_service_classify(nffacl_service *s, const nffacl_rules *rules, const uint8_t *frame, uint32_t len,
                             uint32_t flags, uint32_t *port) {
     if (!s || !rules || (!frame && len) || (flags & ~uint32_t(NFFACL_PARSE_VLAN)) != 0) return NFFACL_ERR_INVALID_ARG;
+    auto failed = [s](int st) {
+        std::lock_guard<std::mutex> g(s->mu);
+        set_last_error(s->error_msg);
+        return st;
+    };
     int st = s->error.load(std::memory_order_acquire);
-    if (st != NFFACL_OK) return st;
+    if (st != NFFACL_OK) return failed(st);
     DevTable *t = rules_table(rules, s->device, st);
     if (!t) return st;
     if (t->svc_kind == kSvcNone) return NFFACL_ERR_UNSUPPORTED;
@@ -603,6 +662,7 @@ int nffacl_service_classify(nffacl_service *s, const nffacl_rules *rules, const 
         }
     }
     m.lock.store(0, std::memory_order_release);
+    if (st == NFFACL_ERR_HIP) return failed(st);
     if (st != NFFACL_OK) return st;
     s->requests.fetch_add(1, std::memory_order_relaxed);
     if (port) *port = static_cast<uint32_t>(v);
@@ -615,6 +675,7 @@ int nffacl_service_get_stats(nffacl_service *s, nffacl_service_stats *out) {
     out->requests = s->requests.load(std::memory_order_relaxed);
     out->timeouts = s->timeouts.load(std::memory_order_relaxed);
     out->running = s->running.load(std::memory_order_relaxed) ? 1u : 0u;
+    out->table_oob = __atomic_load_n(&s->h_ctrl[2], __ATOMIC_ACQUIRE);
     return NFFACL_OK;
 }
 

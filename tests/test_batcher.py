@@ -94,3 +94,122 @@ def test_submit_then_wait_and_flush(torch_cuda, workload):
         with pytest.raises(nffacl.NFError):
             b.classify(ptrs[:2048], lens[:2048])  # > max_batch
     eng.close()
+
+
+# ---- robustness (per-batch status, bounded waits, wait order) -------------------
+
+def _c2_ptrs(workload):
+    g, slots, want = workload
+    ptrs, lens = nffacl.Batcher.frame_pointers(slots, np.arange(len(want), dtype=np.uint64) * 80,
+                                                np.full(len(want), 80, np.uint32))
+    return g, ptrs, lens, want
+
+
+@pytest.mark.gpu
+def test_failed_launch_fails_only_its_batch(torch_cuda, workload, monkeypatch):
+    """One injected launch failure (NFFACL_TUNE_BATCH_FAIL_AT, read at
+    creation): that burst gets the error, every later burst is served and
+    bit-exact (no sticky error)."""
+    g, ptrs, lens, want = _c2_ptrs(workload)
+    eng = nffacl.Engine(nffacl.L3Rules.parse_text(g.text))
+    monkeypatch.setenv("NFFACL_TUNE_BATCH_FAIL_AT", "2")
+    b = nffacl.Batcher(eng, stride=80, max_batch=1024, max_delay_us=50, nbuf=3)
+    monkeypatch.delenv("NFFACL_TUNE_BATCH_FAIL_AT")
+    try:
+        np.testing.assert_array_equal(b.classify(ptrs[:32], lens[:32]), want[:32])
+        with pytest.raises(nffacl.NFError) as ei:
+            b.classify(ptrs[32:64], lens[32:64])
+        assert ei.value.status == nffacl.ERR_HIP
+        for k in range(2, 40):
+            s = slice(32 * k, 32 * (k + 1))
+            np.testing.assert_array_equal(b.classify(ptrs[s], lens[s]), want[s])
+    finally:
+        b.close()
+        eng.close()
+
+
+@pytest.mark.gpu
+def test_wait_timeout_then_wait_again(torch_cuda, workload, monkeypatch):
+    """A batch held back (NFFACL_TUNE_BATCH_HOLD: nothing ships before flush)
+    never completes on its own: the bounded wait returns ERR_TIMEOUT and the
+    ticket stays valid; after flush the same ticket yields the verdicts."""
+    g, ptrs, lens, want = _c2_ptrs(workload)
+    eng = nffacl.Engine(nffacl.L3Rules.parse_text(g.text))
+    monkeypatch.setenv("NFFACL_TUNE_BATCH_HOLD", "1")
+    b = nffacl.Batcher(eng, stride=80, max_batch=1024, max_delay_us=10, nbuf=3)
+    monkeypatch.delenv("NFFACL_TUNE_BATCH_HOLD")
+    try:
+        t = b.submit(ptrs[:32], lens[:32])
+        with pytest.raises(nffacl.NFError) as ei:
+            b.wait(t, timeout_us=3000)
+        assert ei.value.status == nffacl.ERR_TIMEOUT
+        b.flush()
+        np.testing.assert_array_equal(b.wait(t, timeout_us=2_000_000), want[:32])
+        with pytest.raises(nffacl.NFError) as ei:  # a second wait on the same ticket is rejected
+            b.wait(t, timeout_us=1000)
+        assert ei.value.status == nffacl.ERR_INVALID_ARG
+    finally:
+        b.close()
+        eng.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nbuf", [2, 3, 4])
+def test_partial_batches_ship_without_flush(torch_cuda, workload, nbuf):
+    """A lone partial batch ships by itself at any nbuf (no flush), and a
+    thread that queues bursts over several buffers may wait on its LAST
+    ticket first (bounded waits: a regression fails instead of hanging)."""
+    g, ptrs, lens, want = _c2_ptrs(workload)
+    eng = nffacl.Engine(nffacl.L3Rules.parse_text(g.text))
+    try:
+        with nffacl.Batcher(eng, stride=80, max_batch=64, max_delay_us=200, nbuf=nbuf) as b:
+            t = b.submit(ptrs[:5], lens[:5])
+            np.testing.assert_array_equal(b.wait(t, timeout_us=2_000_000), want[:5])
+            k = nbuf - 1  # bursts filling nbuf - 1 buffers (each 64 = max_batch)
+            ts = [b.submit(ptrs[64 * i:64 * (i + 1)], lens[64 * i:64 * (i + 1)]) for i in range(k)]
+            ts.append(b.submit(ptrs[64 * k:64 * k + 7], lens[64 * k:64 * k + 7]))
+            np.testing.assert_array_equal(b.wait(ts[-1], timeout_us=2_000_000), want[64 * k:64 * k + 7])
+            for i in range(k):
+                np.testing.assert_array_equal(b.wait(ts[i], timeout_us=2_000_000), want[64 * i:64 * (i + 1)])
+    finally:
+        eng.close()
+
+
+@pytest.mark.gpu
+def test_device_batcher_rules_per_burst(torch_cuda, workload):
+    """A device batcher (no engine): 8 threads' bursts name one of two rule
+    sets each; bursts of different rule sets never share a batch, and every
+    burst equals the oracle for its own rule set."""
+    g, slots, _ = workload
+    gb = synth.gen_rules(synth.SPECS["c2"], synth.RULE_SEEDS["c2"] + 7)
+    texts = [g.text, gb.text]
+    rs = [nffacl.L3Rules.parse_text(t) for t in texts]
+    n = len(slots) // 80
+    wants = []
+    for t in texts:
+        a4, a6 = ro.parse_text_table(t.encode()).arrays()
+        wants.append(oracle.classify_slots(slots, 80, n, a4, a6, threads=8))
+    assert (wants[0] != wants[1]).mean() > 0.2
+    ptrs, lens = nffacl.Batcher.frame_pointers(slots, np.arange(n, dtype=np.uint64) * 80, np.full(n, 80, np.uint32))
+    with pytest.raises(nffacl.NFError):  # a device batcher needs the rule set per burst
+        with nffacl.Batcher(None, stride=80, device=0) as b0:
+            b0.classify(ptrs[:4], lens[:4])
+    errors = []
+    with nffacl.Batcher(None, stride=80, max_batch=4096, max_delay_us=50, nbuf=4, device=0) as b:
+        def worker(t):
+            try:
+                for s in range(t * 32, 16384, 8 * 32):
+                    which = (s // 32 + t) % 2
+                    got = b.classify(ptrs[s:s + 32], lens[s:s + 32], rules=rs[which])
+                    if not np.array_equal(got, wants[which][s:s + 32]):
+                        errors.append((t, s, which))
+            except Exception as ex:
+                errors.append(ex)
+        ths = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        st = b.stats()
+    assert not errors, errors[:5]
+    assert st["bursts"] == 16384 // 32 and st["batches"] < st["bursts"]

@@ -186,3 +186,9 @@ def test_invalid_arguments(svc, golden):
     with pytest.raises(nffacl.NFError):
         nffacl.Service(0, mailboxes=100)
     assert svc.classify(rules, b"") == 0  # empty frame: not IP
+
+
+def test_no_table_walk_left_its_table(svc):
+    """The consumer's bounds checks never fired over this module's calls."""
+    st = svc.stats()
+    assert st["table_oob"] == 0 and st["timeouts"] == 0, st

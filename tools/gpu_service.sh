@@ -4,7 +4,7 @@
 # L3ACLPort calls through the C++ mirror (flow::ACLSplitter), every answer
 # checked against the oracle.   usage: gpu_service.sh TAG [CFG]
 R="$GRAFT_REPO_ROOT"; OUT="$R/gpurun_out/service_$1"; CFG=${2:-c2}; mkdir -p "$OUT"; cd "$R"
-timeout -k 10 400 python -u -m pytest tests/test_service.py tests/test_cpp_mirror.py -m gpu -x -v --timeout 200 \
+timeout -k 10 400 python -u -m pytest tests/test_service.py tests/test_reload.py tests/test_batcher.py tests/test_cpp_mirror.py -m gpu -x -v --timeout 200 \
     --timeout-method thread -p no:cacheprovider > "$OUT/pytest.out" 2>&1
 rc=$?; echo "pytest exit $rc" >> "$OUT/steps.log"; [ $rc -eq 0 ] || exit $rc
 python tools/service_bench.py "$OUT/in" "$CFG" || exit 1
