@@ -205,13 +205,23 @@ __global__ void __launch_bounds__(64) k_service(SvcArgs a) {
                 break;
             }
             if (key != cur_key) {
-                // the descriptor of a table this wave has not walked yet, by
-                // plain vector loads (never through the scalar cache)
-                const uint64_t lo = __builtin_amdgcn_readlane(c[kSvcChunks - 1].x, first);
-                const uint64_t hi = __builtin_amdgcn_readlane(c[kSvcChunks - 1].y, first);
-                const volatile uint32_t *dp = reinterpret_cast<const volatile uint32_t *>(hi << 32 | lo);
+                // the descriptor of a table this wave has not walked yet (all
+                // its loads in flight together; the table predates this
+                // launch, so no cache level can hold an older copy of it)
+                // (readlane returns int: through uint32_t, or the low word sign-extends)
+                const uint64_t lo = static_cast<uint32_t>(__builtin_amdgcn_readlane(c[kSvcChunks - 1].x, first));
+                const uint64_t hi = static_cast<uint32_t>(__builtin_amdgcn_readlane(c[kSvcChunks - 1].y, first));
+                const u32x4 *dq = reinterpret_cast<const u32x4 *>(hi << 32 | lo);
+                u32x4 q[kSvcDescDwords / 4];
 #pragma unroll
-                for (uint32_t i = 0; i < kSvcDescDwords; ++i) w[i] = __builtin_amdgcn_readfirstlane(dp[i]);
+                for (uint32_t i = 0; i < kSvcDescDwords / 4; ++i) q[i] = dq[i];
+#pragma unroll
+                for (uint32_t i = 0; i < kSvcDescDwords / 4; ++i) {
+                    w[4 * i + 0] = __builtin_amdgcn_readfirstlane(q[i].x);
+                    w[4 * i + 1] = __builtin_amdgcn_readfirstlane(q[i].y);
+                    w[4 * i + 2] = __builtin_amdgcn_readfirstlane(q[i].z);
+                    w[4 * i + 3] = __builtin_amdgcn_readfirstlane(q[i].w);
+                }
                 tab = reinterpret_cast<const uint32_t *>(hi << 32 | lo) - w[2];
                 cur_key = key;
             }

@@ -38,9 +38,9 @@ constexpr uint32_t kSvcRespStride = 8;     // u64 words per response (64 B: one 
 
 // ---- table descriptor (device memory, after each table's blob) ---------------
 //
-// What the consumer needs to walk a table, read once per table generation
-// with plain vector loads (never through the scalar cache: a long-lived
-// kernel must not trust cached words of a reallocated address).
+// What the consumer needs to walk a table, read once per table generation.
+// A consumer launch only walks tables uploaded before it started (service.hip:
+// table generations), so none of its caches can hold an older copy.
 enum SvcKind : uint32_t {
     kSvcNone = 0,     // layout the consumer does not walk (tuning-only forms)
     kSvcLinear = 1,   // LINEAR records
