@@ -79,6 +79,19 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def c3_bytes_per_packet(frames: np.ndarray, desc: np.ndarray) -> float:
+    """Algorithmic bytes per IMIX packet: its first 64-byte line + 8-byte
+    descriptor + 4-byte verdict, plus a second 64-byte line for IPv4 frames
+    whose ports lie past byte 63 (IHL >= 12: L4 at 14 + 4 IHL >= 62) and that
+    are longer than 64 bytes (bytes past a frame read as 0)."""
+    off = (desc >> np.uint64(16)).astype(np.int64)
+    ln = (desc & np.uint64(0xFFFF)).astype(np.int64)
+    et = frames[off + 12].astype(np.int64) << 8 | frames[off + 13]
+    ihl = frames[off + 14] & 0x0F
+    second = (et == 0x0800) & (ihl >= 12) & (ln > 64)
+    return round(64 + 8 + 4 + 64 * float(second.mean()), 3)
+
+
 def build_rules(cfg: str):
     from nffacl import synth
     if cfg == "l2":
@@ -293,6 +306,8 @@ def run_config(cfg: str, args, rank: int, world: int, local: int, dev, nd, headl
     value = total / elapsed / 1e6
     mean_k = float(kms.mean()) / 1e3
     bpp = BYTES_PER_PACKET.get(cfg, 68)
+    if frames_mode:  # exact per-config average: + the second line of IPv4 IHL >= 12 frames
+        bpp = c3_bytes_per_packet(frames, desc)
     achieved = bpp * n / mean_k / 1e9
     rec = {
         "metric": METRICS[cfg],
@@ -399,8 +414,10 @@ def main():
     # its shard, verdicts come back with one dist.gather; bit-exact vs rank
     # 0's own classify of the whole batch above.
     if world > 1:
-        out["rccl_ranks"] = dist.get_world_size()
+        out["ranks"] = dist.get_world_size()
         out["backend"] = dist.get_backend()
+        if out["backend"] == "nccl":  # RCCL on ROCm
+            out["rccl_ranks"] = out["ranks"]
     if world > 1 and not args.no_scatter and not st["frames_mode"] and not st["l2_mode"]:
         stream = st["stream"]
 

@@ -5,11 +5,11 @@
 //
 // Launch policy (adaptive batching): a batch ships as soon as it holds a burst,
 // fewer than kEagerInflight batches are on the GPU and a buffer stays free
-// behind it (or nothing is on the GPU at all), so an idle GPU costs a burst
-// one launch round trip, while a busy one lets the open batch grow (up to
-// max_batch) until a batch completes.  A batch whose first burst has waited
-// max_delay_us ships in any case: no wait order of the submitters' tickets
-// can hold it back (buffers whose tickets are not collected yet stay busy).
+// behind it, so an idle GPU costs a burst one launch round trip, while a busy
+// one lets the open batch grow (up to max_batch) until a batch completes.  A
+// batch whose first burst has waited max_delay_us ships in any case: no
+// number of buffers and no wait order of the submitters' tickets can hold it
+// back (buffers whose tickets are not collected yet stay busy).
 // The reference's clones submit synchronously (segmentProcess waits for its
 // separator's answers, flow/flow.go:1487-1520), so the open batch collects
 // exactly the bursts of the clones whose previous batch came back — no timer
@@ -148,12 +148,13 @@ void launcher_main(nffacl_batcher *b) {
         }
         if (x.state == BatchBuf::OPEN && x.count > 0 && !b->hold) {
             // open_idx == launch_idx here.  Eager: fewer than kEagerInflight
-            // batches on the GPU and a free buffer behind this one, or nothing
-            // on the GPU at all (buffers whose tickets are not collected yet
-            // must not hold a lone batch back).  Late: its first burst has
-            // waited max_delay — it ships whatever else is busy (producers
-            // then wait for a buffer: back-pressure).
-            const bool room = b->inflight_n < kEagerInflight && (b->busy + 2 <= b->nbuf || b->inflight_n == 0);
+            // batches on the GPU and a free buffer behind this one (so a
+            // thread's unwaited tickets fill whole batches: they may hold
+            // nbuf - 1 of them).  Late: its first burst has waited max_delay
+            // — it ships however busy the other buffers are (held by tickets
+            // nobody has collected yet, in any wait order); producers then
+            // wait for a buffer (back-pressure).
+            const bool room = b->inflight_n < kEagerInflight && b->busy + 2 <= b->nbuf;
             const auto deadline = x.opened + b->max_delay;
             if (b->stop || room || Clock::now() >= deadline) {
                 seal_open(b);

@@ -414,14 +414,15 @@ static int ensure_host_pipeline(nffacl_engine *eng, uint32_t stride, uint64_t n)
     for (int b = 0; b < 2; ++b) {
         if (eng->h_stage[b]) { (void)hipHostFree(eng->h_stage[b]); eng->h_stage[b] = nullptr; }
         if (eng->d_slots[b]) { (void)hipFree(eng->d_slots[b]); eng->d_slots[b] = nullptr; }
-        if (eng->h_port[b]) { (void)hipHostFree(eng->h_port[b]); eng->h_port[b] = nullptr; }
+        if (eng->h_port[b]) { (void)hipHostFree(eng->h_port[b]); eng->h_port[b] = nullptr; eng->d_hport[b] = nullptr; }
         if (eng->d_port[b]) { (void)hipFree(eng->d_port[b]); eng->d_port[b] = nullptr; }
     }
     eng->chunk = 0;
     for (int b = 0; b < 2; ++b) {
         HIP_CHECK(hipHostMalloc(reinterpret_cast<void **>(&eng->h_stage[b]), chunk * stride, hipHostMallocDefault));
         HIP_CHECK(hipMalloc(reinterpret_cast<void **>(&eng->d_slots[b]), chunk * stride));
-        HIP_CHECK(hipHostMalloc(reinterpret_cast<void **>(&eng->h_port[b]), chunk * 4, hipHostMallocDefault));
+        HIP_CHECK(hipHostMalloc(reinterpret_cast<void **>(&eng->h_port[b]), chunk * 4, hipHostMallocMapped));
+        HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void **>(&eng->d_hport[b]), eng->h_port[b], 0));
         HIP_CHECK(hipMalloc(reinterpret_cast<void **>(&eng->d_port[b]), chunk * 4));
         if (!eng->streams[b]) HIP_CHECK(hipStreamCreateWithFlags(&eng->streams[b], hipStreamNonBlocking));
         if (!eng->done[b]) HIP_CHECK(hipEventCreateWithFlags(&eng->done[b], hipEventDisableTiming));
@@ -436,6 +437,16 @@ int nffacl_classify_host(nffacl_engine *eng, const uint8_t *h_slots, uint32_t st
     return nffacl_classify_host_ex(eng, h_slots, stride, n, h_port, h_permit, 0);
 }
 
+// Device alias of pinned (mapped) host memory, or nullptr.
+static void *host_alias(const void *p) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    return a.type == hipMemoryTypeHost ? a.devicePointer : nullptr;
+}
+
 int nffacl_classify_host_ex(nffacl_engine *eng, const uint8_t *h_slots, uint32_t stride, uint64_t n,
                             uint32_t *h_port, uint8_t *h_permit, uint32_t flags) {
     if (!eng || !flags_ok(flags)) return NFFACL_ERR_INVALID_ARG;
@@ -446,7 +457,17 @@ int nffacl_classify_host_ex(nffacl_engine *eng, const uint8_t *h_slots, uint32_t
     int st = ensure_host_pipeline(eng, stride, n);
     if (st != NFFACL_OK) return st;
     const TablePtr t = acquire_table(eng);  // one table for every chunk of this call
-    const bool direct = range_is_pinned(h_slots, n * stride);
+    // Pinned input (one registered allocation, 16-byte aligned): no copy at
+    // all — the kernel reads the slots over PCIe itself (its lane-contiguous
+    // 1 KiB loads keep the link busy; one DMA direction less to schedule) and
+    // writes the verdicts into mapped pinned memory, the caller's when that is
+    // pinned too.  Otherwise: staged chunks, H2D -> kernel -> D2H.
+    const uint8_t *d_host_slots = nullptr;
+    if (range_is_pinned(h_slots, n * stride) && reinterpret_cast<uintptr_t>(h_slots) % 16 == 0)
+        d_host_slots = static_cast<const uint8_t *>(host_alias(h_slots));
+    uint32_t *d_host_port = nullptr;
+    if (d_host_slots && h_port && range_is_pinned(h_port, n * 4) && reinterpret_cast<uintptr_t>(h_port) % 4 == 0)
+        d_host_port = static_cast<uint32_t *>(host_alias(h_port));
     const uint64_t chunk = eng->chunk;
     const uint64_t nchunks = (n + chunk - 1) / chunk;
     uint64_t pending_chunk[2] = {~0ull, ~0ull};
@@ -456,9 +477,10 @@ int nffacl_classify_host_ex(nffacl_engine *eng, const uint8_t *h_slots, uint32_t
         const uint64_t c = pending_chunk[b];
         const uint64_t first = c * chunk;
         const uint64_t cnt = std::min<uint64_t>(chunk, n - first);
-        if (h_port) std::memcpy(h_port + first, eng->h_port[b], cnt * 4);
+        const uint32_t *res = d_host_port ? h_port + first : eng->h_port[b];
+        if (h_port && !d_host_port) std::memcpy(h_port + first, res, cnt * 4);
         if (h_permit)
-            for (uint64_t i = 0; i < cnt; ++i) h_permit[first + i] = eng->h_port[b][i] != 0;
+            for (uint64_t i = 0; i < cnt; ++i) h_permit[first + i] = res[i] != 0;
         pending_chunk[b] = ~0ull;
         return NFFACL_OK;
     };
@@ -467,15 +489,21 @@ int nffacl_classify_host_ex(nffacl_engine *eng, const uint8_t *h_slots, uint32_t
         if ((st = drain(b)) != NFFACL_OK) return st;
         const uint64_t first = c * chunk;
         const uint64_t cnt = std::min<uint64_t>(chunk, n - first);
-        const uint8_t *src = h_slots + first * stride;
-        if (!direct) {
+        if (d_host_slots) {
+            uint32_t *out = d_host_port ? d_host_port + first : eng->d_hport[b];
+            st = launch_slots(eng, t.get(), d_host_slots + first * stride, stride, cnt, out, nullptr, eng->streams[b],
+                              flags);
+            if (st != NFFACL_OK) return st;
+        } else {
+            const uint8_t *src = h_slots + first * stride;
             std::memcpy(eng->h_stage[b], src, cnt * stride);
-            src = eng->h_stage[b];
+            HIP_CHECK(hipMemcpyAsync(eng->d_slots[b], eng->h_stage[b], cnt * stride, hipMemcpyHostToDevice,
+                                     eng->streams[b]));
+            st = launch_slots(eng, t.get(), eng->d_slots[b], stride, cnt, eng->d_port[b], nullptr, eng->streams[b],
+                              flags);
+            if (st != NFFACL_OK) return st;
+            HIP_CHECK(hipMemcpyAsync(eng->h_port[b], eng->d_port[b], cnt * 4, hipMemcpyDeviceToHost, eng->streams[b]));
         }
-        HIP_CHECK(hipMemcpyAsync(eng->d_slots[b], src, cnt * stride, hipMemcpyHostToDevice, eng->streams[b]));
-        st = launch_slots(eng, t.get(), eng->d_slots[b], stride, cnt, eng->d_port[b], nullptr, eng->streams[b], flags);
-        if (st != NFFACL_OK) return st;
-        HIP_CHECK(hipMemcpyAsync(eng->h_port[b], eng->d_port[b], cnt * 4, hipMemcpyDeviceToHost, eng->streams[b]));
         HIP_CHECK(hipEventRecord(eng->done[b], eng->streams[b]));
         pending_chunk[b] = c;
     }

@@ -375,6 +375,7 @@ __device__ __forceinline__ void bounds32(const T &tab, uint32_t dir, uint32_t t,
 }
 
 struct LdsTab {
+    static constexpr bool kFreeLoads = true;  // out-of-range LDS reads return 0, never fault
     __device__ __forceinline__ uint32_t ld(uint32_t i) const { return lds_tab[i]; }
     __device__ __forceinline__ void bounds(uint32_t dir, uint32_t, uint32_t t, uint32_t &lo, uint32_t &hi,
                                            bool = false) const {
@@ -385,6 +386,7 @@ struct LdsTab {
     }
 };
 struct GlobalTab {
+    static constexpr bool kFreeLoads = false;
     const uint32_t *__restrict__ p;
     __device__ __forceinline__ uint32_t ld(uint32_t i) const { return p[i]; }
     __device__ __forceinline__ void bounds(uint32_t dir, uint32_t, uint32_t t, uint32_t &lo, uint32_t &hi,
@@ -400,6 +402,7 @@ struct GlobalTab {
 // persistent scalar-call consumer, service.hip, which stages nothing).
 template <bool IN_LDS>
 struct DirTab {
+    static constexpr bool kFreeLoads = false;  // entries (ld4) are global
     const uint32_t *__restrict__ p;
     uint32_t limit = 0;  // !IN_LDS: words past the table read as 0 (service.hip)
     __device__ __forceinline__ uint32_t ld(uint32_t i) const {
@@ -455,12 +458,21 @@ __device__ __forceinline__ uint32_t entry_miss_ext(const T &tab, uint32_t off, c
            ((f.t[1] ^ y.z) & z.y) | ((f.t[2] ^ y.w) & z.z) | ((f.t[3] ^ z.x) & z.w);
 }
 
+// x * entry dwords (IPv6 20 = 16 + 4, IPv4 8): shifts, not a quarter-rate multiply.
+__device__ __forceinline__ uint32_t times_ew(uint32_t x, bool v6) { return v6 ? (x << 4) + (x << 2) : x << 3; }
+
 // First match over the four key slots of the lane's family, walked together:
 // every iteration tests the next entry of every slot list, so the wave pays
 // max(list lengths) table round trips, not their sum.  Loops have
 // wave-uniform trip counts (ballots) and predicated bodies.
 // U = list entries per slot per loop trip: all NS x U entry loads of a trip
-// are issued before any is tested.
+// are issued before any is tested.  The walk keeps dword offsets (cursor,
+// end) per slot, advanced by adds.  Tables whose reads are free to issue for
+// every lane (T::kFreeLoads: LDS, where an inactive lane's read is harmless
+// and cheaper than the exec-mask juggling and register zeroing a predicated
+// load needs) load unconditionally; global tables load only for lanes still
+// walking (a 16-byte load costs the TA 16 cycles per 64 active lanes; global:
+// -4 % on C3, profiles/r1_masked).
 template <int NS, int U, class T>
 __device__ __forceinline__ uint32_t classify_indexed(const T &tab, const IndexedArgs &a, const Fields &f) {
     const bool v6 = f.is6;
@@ -468,18 +480,18 @@ __device__ __forceinline__ uint32_t classify_indexed(const T &tab, const Indexed
     const uint32_t ew = v6 ? kEnt6Dwords : kEnt4Dwords;
     const uint32_t key[4] = {__builtin_bswap32(f.t[0]), __builtin_bswap32(f.s[0]), f.ports >> 16,
                              f.ports & 0xFFFFu};
-    uint32_t c[NS], e[NS], base[NS];
+    uint32_t c[NS], e[NS];  // dword offsets: the slot list's next entry, its end
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
         const SlotArgs &s4 = a.f4.slot[s], &s6 = a.f6.slot[s];
         const uint32_t shift = v6 ? s6.shift : s4.shift;
         const uint32_t dir = v6 ? s6.off_dir : s4.off_dir;
-        base[s] = v6 ? s6.off_ent : s4.off_ent;
+        const uint32_t base = v6 ? s6.off_ent : s4.off_ent;
         const uint32_t t = key[s] >> shift;  // < n_buckets for any key: both reads in range
         uint32_t lo, hi;
         tab.bounds(dir, v6 ? s6.off_dir16 : s4.off_dir16, t, lo, hi, a.dir8 != 0u);
-        c[s] = lo;
-        e[s] = mine ? hi : lo;
+        c[s] = base + times_ew(lo, v6);
+        e[s] = mine ? base + times_ew(hi, v6) : c[s];
     }
     uint32_t best = kNone, out = 0;
     while (true) {
@@ -492,14 +504,16 @@ __device__ __forceinline__ uint32_t classify_indexed(const T &tab, const Indexed
         for (int s = 0; s < NS; ++s)
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                // only lanes still walking this list load (a 16-byte load
-                // costs the TA 16 cycles per 64 active lanes; LDS: -1.3 % on
-                // C2, global: -4 % on C3, profiles/r1_masked)
-                A[s][u] = B[s][u] = u32x4{0, 0, 0, 0};
-                if (c[s] + u < e[s]) {
-                    const uint32_t off = base[s] + (c[s] + u) * ew;
+                const uint32_t off = c[s] + u * ew;
+                if (T::kFreeLoads) {
                     A[s][u] = tab.ld4(off);
                     B[s][u] = tab.ld4(off + 4);
+                } else {
+                    A[s][u] = B[s][u] = u32x4{0, 0, 0, 0};
+                    if (off < e[s]) {
+                        A[s][u] = tab.ld4(off);
+                        B[s][u] = tab.ld4(off + 4);
+                    }
                 }
             }
 #pragma unroll
@@ -507,13 +521,14 @@ __device__ __forceinline__ uint32_t classify_indexed(const T &tab, const Indexed
             bool go = true;
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const bool act = go && c[s] + u < e[s];
+                const uint32_t off = c[s] + u * ew;
+                const bool act = go && off < e[s];
                 const uint32_t idx = B[s][u].x >> kEntIndexShift;
                 const bool earlier = act && idx < best;
                 bool pass = entry_miss(A[s][u], B[s][u], f) == 0u;
                 const bool ext = v6 && earlier && pass;
                 if (ballot(ext)) {
-                    if (ext) pass = entry_miss_ext(tab, base[s] + (c[s] + u) * ew + 8, f) == 0u;
+                    if (ext) pass = entry_miss_ext(tab, off + 8, f) == 0u;
                 }
                 const bool take = earlier && pass;
                 best = take ? idx : best;
@@ -521,7 +536,7 @@ __device__ __forceinline__ uint32_t classify_indexed(const T &tab, const Indexed
                 // stop at a hit, or once the ascending list has passed `best`
                 go = earlier && !pass;
             }
-            c[s] = go ? c[s] + U : e[s];
+            c[s] = go ? c[s] + U * ew : e[s];
         }
     }
     // rules with no selective key: wave-uniform scan in rule order per family

@@ -69,7 +69,8 @@ struct nffacl_engine {
     std::mutex host_mu;
     size_t chunk = 0;
     uint8_t *h_stage[2] = {nullptr, nullptr};
-    uint32_t *h_port[2] = {nullptr, nullptr};
+    uint32_t *h_port[2] = {nullptr, nullptr};   // mapped pinned verdict staging
+    uint32_t *d_hport[2] = {nullptr, nullptr};  // their device aliases (zero-copy path)
     uint8_t *d_slots[2] = {nullptr, nullptr};
     uint32_t *d_port[2] = {nullptr, nullptr};
     hipStream_t streams[2] = {nullptr, nullptr};

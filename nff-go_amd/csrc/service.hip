@@ -81,6 +81,7 @@ __device__ __forceinline__ u32x4 ld16_host(__amdgpu_buffer_rsrc_t rs, uint32_t o
 // INDEXED inline entries read from global memory with bounds checks (a word
 // outside the table reads as 0 and raises the host flag instead of faulting).
 struct CheckedTab {
+    static constexpr bool kFreeLoads = false;
     const uint32_t *__restrict__ p;
     uint32_t limit;
     uint32_t *oob;

@@ -62,7 +62,7 @@ def test_bench_two_ranks_one_gpu_scatter(gpu_available):
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     d = _json_line(r.stdout)
-    assert d["n_gpus"] == 2 and d["rccl_ranks"] == 2 and d["backend"] == "gloo"
+    assert d["n_gpus"] == 2 and d["ranks"] == 2 and d["backend"] == "gloo" and "rccl_ranks" not in d
     assert d["bit_exact_sample"]
     sc = d["scatter_inclusive"]
     assert sc["bit_exact_vs_local"] and sc["collectives"] == "dist.scatter + dist.gather"

@@ -327,6 +327,28 @@ def test_classify_host_matches_device(torch_cuda):
     np.testing.assert_array_equal(permit, (want != 0).astype(np.uint8))
 
 
+@pytest.mark.parametrize("stride", [64, 80])
+def test_classify_host_pinned_zero_copy(torch_cuda, stride):
+    """Pinned input: the kernel reads the host slots over PCIe itself (no
+    copies) and writes the verdicts into mapped memory; ragged n, > one chunk,
+    pinned and pageable verdict buffers."""
+    torch = torch_cuda
+    g = synth.gen_rules(synth.SPECS["c2"], synth.RULE_SEEDS["c2"])
+    rules, (a4, a6) = _rules_and_arrays(g.text)
+    n = (1 << 21) + 37
+    slots = synth.gen_slots(g, n, 123, stride=stride)
+    pinned = torch.from_numpy(slots).pin_memory()
+    want = oracle.classify_slots(slots, stride, n, a4, a6, threads=THREADS)
+    with nffacl.Engine(rules) as eng:
+        port, permit = eng.classify_host(pinned.numpy(), stride, n)
+        np.testing.assert_array_equal(port, want)
+        np.testing.assert_array_equal(permit, (want != 0).astype(np.uint8))
+        out = torch.zeros(n, dtype=torch.int32).pin_memory()  # pinned verdicts: written in place
+        st = nffacl._classify_host(eng._h, pinned.data_ptr(), stride, n, out.data_ptr(), None, 0)
+        assert st == nffacl.OK
+        np.testing.assert_array_equal(out.numpy().view(np.uint32), want)
+
+
 def test_stability_separate_split_proportions(torch_cuda, golden):
     """testSingleWorkingFF.go: separate -> exactly the dst-port-111 third is
     permitted; split -> outputs 1/2 by dst port (test-*.conf)."""
