@@ -384,6 +384,12 @@ typedef struct nffacl_service_stats {
     uint64_t running;   /* 1 while the consumer kernel is resident */
     uint64_t table_oob; /* 1 if a table walk ever indexed outside its table (read as 0 instead
                            of faulting; a compiler/upload bug — the tests require 0) */
+    /* where the time goes, summed over the consumer's completed launches: */
+    uint64_t polls;     /* mailbox polls (one PCIe read of every hot mailbox each) */
+    double poll_ns;     /* mean poll duration, load issue to data */
+    uint64_t groups;    /* request groups classified (one table per group) */
+    double group_ns;    /* mean time to classify + answer a group */
+    uint64_t answered;  /* requests answered by the consumer */
 } nffacl_service_stats;
 
 /* mailboxes: a multiple of 64 (one wave each 64; 0 = 128), one per calling

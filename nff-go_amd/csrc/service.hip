@@ -67,6 +67,8 @@ struct SvcArgs {
     uint32_t *ctrl;         // ctrl[0] != 0: stop (host); ctrl[1] != 0: restart (a wave saw a newer table)
     uint32_t box_bytes;     // bytes of the mailbox array (buffer range)
     uint32_t epoch;         // table generations <= epoch were uploaded before this launch
+    uint64_t *stats;        // per wave kSvcStatWords u64 (host memory), written at exit
+    uint32_t lds_dwords;    // INDEXED tables up to this size are staged in LDS (0: never)
     uint64_t idle_ticks;    // leave after this long without a request (wall clock ticks)
     uint64_t hot_ticks;     // a mailbox answered within this window is read whole every pass
     uint64_t life_ticks;    // leave after this long in any case
@@ -107,7 +109,8 @@ struct CheckedTab {
 
 // Classify one group (wave-uniform descriptor `w`, table `tab`).
 __device__ __forceinline__ uint32_t svc_classify(const uint32_t (&w)[kSvcDescDwords], const uint32_t *tab,
-                                                 const Fields &f, FlatScratch<2> &W, uint32_t lane, uint32_t *oob) {
+                                                 const Fields &f, FlatScratch<2> &W, uint32_t lane, uint32_t *oob,
+                                                 bool staged) {
     const uint32_t kind = w[0], ns = w[1];
     if (kind == kSvcLinear) return classify_linear(f, tab + w[4], w[5], tab + w[6], w[7]);
     IndexedArgs a{};
@@ -128,6 +131,11 @@ __device__ __forceinline__ uint32_t svc_classify(const uint32_t (&w)[kSvcDescDwo
         for (int s = 0; s < 4; ++s)
             fa.slot[s] = SlotArgs{w[b + 4 + 4 * s], w[b + 5 + 4 * s], w[b + 6 + 4 * s], w[b + 7 + 4 * s],
                                   static_cast<uint32_t>(s), kFZero, 0, 0};
+    }
+    if (kind == kSvcIndexed && staged) {  // the whole table in LDS (lds_tab[0, w[2]))
+        if (ns == 2) return classify_indexed<2, 1>(LdsTab{}, a, f);
+        if (ns == 3) return classify_indexed<3, 1>(LdsTab{}, a, f);
+        return classify_indexed<4, 1>(LdsTab{}, a, f);
     }
     if (kind == kSvcIndexed) {
         const CheckedTab ct{tab, w[2], oob};
@@ -155,32 +163,57 @@ __global__ void __launch_bounds__(64) k_service(SvcArgs a) {
     const uint64_t t0 = wall_clock64();
     uint64_t last = t0, lane_last = t0;  // hot at start: the call that armed us is read whole
     uint32_t cur_key = 0xFFFFFFFFu;  // generation << 1 | vlan of the descriptor in `w`
+    uint32_t staged_gen = 0xFFFFFFFFu;  // generation of the table staged in LDS
     uint32_t w[kSvcDescDwords];
 #pragma unroll
     for (uint32_t i = 0; i < kSvcDescDwords; ++i) w[i] = 0;
     const uint32_t *tab = nullptr;
+    // where the time goes (wall-clock ticks, written to host memory at exit):
+    // polls and their ticks (issue to data), groups classified and their
+    // ticks, requests answered
+    uint64_t n_polls = 0, poll_ticks = 0, n_groups = 0, group_ticks = 0, n_req = 0;
+    // One poll always in flight: the next pass's mailbox reads are issued as
+    // soon as this pass's data is in registers, before its requests are
+    // classified, so the PCIe round trip overlaps the classification
+    // (LDS-staged tables issue no vector memory reads that would wait behind
+    // it).  A poll reads the whole mailbox of lanes answered within `hot`,
+    // only the tag chunk of the others.
+    u32x4 nx[kSvcChunks];
+    uint64_t ncw = 0, nt = t0;
+    bool nhot = true;
+    auto issue = [&]() {
+        nt = wall_clock64();
+        nhot = nt - lane_last <= a.hot_ticks;
+#pragma unroll
+        for (uint32_t j = 0; j < kSvcChunks; ++j) nx[j] = u32x4{0, 0, 0, 0};
+        if (nhot) {
+#pragma unroll
+            for (uint32_t j = 0; j < kSvcChunks; ++j) nx[j] = ld16_host(rs, box + 16u * j);
+        } else {
+            nx[kSvcChunks - 1] = ld16_host(rs, box + 16u * (kSvcChunks - 1));
+        }
+        ncw = 0;  // stop | restart << 32
+        if (lane == 0) ncw = __hip_atomic_load(reinterpret_cast<uint64_t *>(a.ctrl), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_SYSTEM);
+    };
+    issue();
     while (true) {
-        const uint64_t now = wall_clock64();
-        if (now - t0 > a.life_ticks) break;
-        const bool hot = now - lane_last <= a.hot_ticks;
         u32x4 c[kSvcChunks];
 #pragma unroll
-        for (uint32_t j = 0; j < kSvcChunks; ++j) c[j] = u32x4{0, 0, 0, 0};
-        if (hot) {
-#pragma unroll
-            for (uint32_t j = 0; j < kSvcChunks; ++j) c[j] = ld16_host(rs, box + 16u * j);
-        } else {
-            c[kSvcChunks - 1] = ld16_host(rs, box + 16u * (kSvcChunks - 1));
-        }
-        uint64_t cw = 0;  // stop | restart << 32
-        if (lane == 0) cw = __hip_atomic_load(reinterpret_cast<uint64_t *>(a.ctrl), __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_SYSTEM);
+        for (uint32_t j = 0; j < kSvcChunks; ++j) c[j] = nx[j];  // waits for the poll issued a pass ago
+        const uint64_t cw = ncw, now = nt;
+        const bool hot = nhot;
+        if (now - t0 > a.life_ticks) break;
+        issue();  // the next pass's poll, in flight from here
         if ((__builtin_amdgcn_readlane(static_cast<uint32_t>(cw), 0) |
              __builtin_amdgcn_readlane(static_cast<uint32_t>(cw >> 32), 0)) != 0u)
             break;
         const uint32_t tag = c[kSvcChunks - 1].w;
         const bool fresh = tag != done;
-        // a cold mailbox with a new tag turns hot: read whole on the next pass
+        const uint64_t t_data = wall_clock64();
+        ++n_polls;
+        poll_ticks += t_data - now;
+        // a cold mailbox with a new tag turns hot: read whole from the poll after next
         if (!hot && fresh) lane_last = now;
         bool pend = hot && fresh;
 #pragma unroll
@@ -193,6 +226,7 @@ __global__ void __launch_bounds__(64) k_service(SvcArgs a) {
         last = now;
         bool restart = false;
         while (m) {
+            const uint64_t t_group = wall_clock64();
             const uint32_t first = static_cast<uint32_t>(__builtin_ctzll(m));
             const uint32_t key = __builtin_amdgcn_readlane(c[kSvcChunks - 1].z, first);
             const bool mine = pend && c[kSvcChunks - 1].z == key;
@@ -226,6 +260,16 @@ __global__ void __launch_bounds__(64) k_service(SvcArgs a) {
                 tab = reinterpret_cast<const uint32_t *>(hi << 32 | lo) - w[2];
                 cur_key = key;
             }
+            // small INDEXED tables are walked from LDS: staged once per table
+            // (per launch), and then no table read waits behind the PCIe polls
+            const bool staged = w[0] == kSvcIndexed && w[2] <= a.lds_dwords;
+            if (staged && staged_gen != (key >> 1)) {
+                const u32x4 *src = reinterpret_cast<const u32x4 *>(tab);
+                u32x4 *dst = reinterpret_cast<u32x4 *>(lds_tab);
+                for (uint32_t i = lane; i < (w[2] + 3u) / 4u; i += 64u) dst[i] = src[i];
+                wave_lds_sync();
+                staged_gen = key >> 1;
+            }
             uint32_t full[3 * kSvcPktChunks], d[16];
 #pragma unroll
             for (uint32_t j = 0; j < kSvcPktChunks; ++j) {
@@ -245,7 +289,7 @@ __global__ void __launch_bounds__(64) k_service(SvcArgs a) {
                     hi = k + 1 == j ? full[j] : hi;
                 }
             }, key & 1u ? uint32_t(NFFACL_PARSE_VLAN) : 0u);
-            const uint32_t port = svc_classify(w, tab, f, W, lane, a.ctrl + 2);
+            const uint32_t port = svc_classify(w, tab, f, W, lane, a.ctrl + 2, staged);
             if (mine) {
                 __hip_atomic_store(resp, uint64_t(tag) << 32 | port, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 done = tag;
@@ -253,8 +297,17 @@ __global__ void __launch_bounds__(64) k_service(SvcArgs a) {
             }
             pend = pend && !mine;
             m = ballot(pend);
+            ++n_groups;
+            n_req += __builtin_popcountll(ballot(mine));
+            group_ticks += wall_clock64() - t_group;
         }
         if (restart) break;
+    }
+    if (lane == 0) {
+        uint64_t *st = a.stats + size_t(blockIdx.x) * kSvcStatWords;
+        const uint64_t v[5] = {n_polls, poll_ticks, n_groups, group_ticks, n_req};
+#pragma unroll
+        for (int i = 0; i < 5; ++i) __hip_atomic_store(st + i, v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -374,6 +427,9 @@ struct nffacl_service {
     uint8_t *h_box = nullptr;
     uint64_t *h_resp = nullptr;
     uint32_t *h_ctrl = nullptr;
+    uint64_t *h_stats = nullptr;  // per wave: the consumer's counters of its last launch
+    uint64_t acc[kSvcStatWords] = {};  // under mu: summed over launches
+    uint64_t ticks_per_us = 100;
     dev::SvcArgs args{};
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
@@ -439,7 +495,8 @@ void armer_main(nffacl_service *s) {
         s->running.store(true, std::memory_order_seq_cst);
         __atomic_store_n(&s->h_ctrl[1], 0u, __ATOMIC_SEQ_CST);
         s->args.epoch = table_epoch();  // every table of this generation or older is in HBM
-        hipLaunchKernelGGL(dev::k_service, dim3(s->n_mb / 64), dim3(64), 0, s->stream, s->args);
+        hipLaunchKernelGGL(dev::k_service, dim3(s->n_mb / 64), dim3(64), size_t(s->args.lds_dwords) * 4, s->stream,
+                           s->args);
         hipError_t e = hipGetLastError();
         if (e == hipSuccess) e = hipEventRecord(s->done, s->stream);
         if (e == hipSuccess) {
@@ -448,6 +505,11 @@ void armer_main(nffacl_service *s) {
         }
         s->running.store(false, std::memory_order_seq_cst);
         lk.lock();
+        for (uint32_t wv = 0; wv < s->n_mb / 64; ++wv)
+            for (uint32_t i = 0; i < kSvcStatWords; ++i) {
+                s->acc[i] += __atomic_load_n(&s->h_stats[wv * kSvcStatWords + i], __ATOMIC_ACQUIRE);
+                __atomic_store_n(&s->h_stats[wv * kSvcStatWords + i], 0ull, __ATOMIC_RELAXED);
+            }
         if (e != hipSuccess) {
             s->error_msg = std::string("service consumer: ") + hipGetErrorName(e) + ": " + hipGetErrorString(e);
             s->error.store(NFFACL_ERR_HIP, std::memory_order_release);
@@ -573,7 +635,8 @@ int nffacl_service_create(int hip_device, uint32_t mailboxes, uint32_t idle_us, 
     s->mbx.reset(new (std::nothrow) MailboxState[mailboxes]);
     const size_t box_bytes = size_t(mailboxes) * kSvcBoxBytes;
     const size_t resp_bytes = size_t(mailboxes) * kSvcRespStride * 8;
-    const size_t bytes = box_bytes + resp_bytes + 64;
+    const size_t stat_bytes = size_t(mailboxes / 64) * kSvcStatWords * 8;
+    const size_t bytes = box_bytes + resp_bytes + 64 + stat_bytes;
     hipError_t e = s->mbx ? hipSuccess : hipErrorOutOfMemory;
     if (e == hipSuccess)
         e = hipHostMalloc(reinterpret_cast<void **>(&s->h_mem), bytes, hipHostMallocMapped | hipHostMallocCoherent);
@@ -594,13 +657,36 @@ int nffacl_service_create(int hip_device, uint32_t mailboxes, uint32_t idle_us, 
     s->h_resp = reinterpret_cast<uint64_t *>(s->h_mem + box_bytes);
     s->h_ctrl = reinterpret_cast<uint32_t *>(s->h_mem + box_bytes + resp_bytes);
     const uint64_t tpu = uint64_t(khz) / 1000;  // ticks per µs
+    s->ticks_per_us = tpu;
     s->args.box = d_mem;
     s->args.resp = reinterpret_cast<uint64_t *>(d_mem + box_bytes);
     s->args.ctrl = reinterpret_cast<uint32_t *>(d_mem + box_bytes + resp_bytes);
+    s->args.stats = reinterpret_cast<uint64_t *>(d_mem + box_bytes + resp_bytes + 64);
+    s->h_stats = reinterpret_cast<uint64_t *>(s->h_mem + box_bytes + resp_bytes + 64);
     s->args.box_bytes = static_cast<uint32_t>(box_bytes);
     s->args.idle_ticks = uint64_t(idle_us) * tpu;
     s->args.hot_ticks = 200 * tpu;
     s->args.life_ticks = 100000 * tpu;  // 100 ms, then the armer re-launches if calls keep coming
+    // INDEXED tables up to 64 KiB (C1/C2-class) are staged in the consumer's
+    // LDS (NFFACL_TUNE_SVC_LDS=0: walk every table from global memory)
+    s->args.lds_dwords = kSvcLdsDwords;
+    {
+        long v = 0;
+        bool set = false;
+        std::string err;
+        if (!env_knob("NFFACL_TUNE_SVC_LDS", 0, 1, v, set, err)) {
+            set_last_error(err);
+            release_service(s);
+            return NFFACL_ERR_INVALID_ARG;
+        }
+        if (set && v == 0) s->args.lds_dwords = 0;
+    }
+    if (s->args.lds_dwords &&
+        hipFuncSetAttribute(reinterpret_cast<const void *>(dev::k_service), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            static_cast<int>(s->args.lds_dwords * 4)) != hipSuccess) {
+        (void)hipGetLastError();
+        s->args.lds_dwords = 0;
+    }
     {
         std::lock_guard<std::mutex> g(g_live_mu);
         if (!g_live) {
@@ -687,6 +773,13 @@ int nffacl_service_get_stats(nffacl_service *s, nffacl_service_stats *out) {
     out->timeouts = s->timeouts.load(std::memory_order_relaxed);
     out->running = s->running.load(std::memory_order_relaxed) ? 1u : 0u;
     out->table_oob = __atomic_load_n(&s->h_ctrl[2], __ATOMIC_ACQUIRE);
+    std::lock_guard<std::mutex> g(s->mu);
+    const double tpu = double(s->ticks_per_us);
+    out->polls = s->acc[0];
+    out->poll_ns = s->acc[0] ? s->acc[1] * 1000.0 / tpu / double(s->acc[0]) : 0.0;
+    out->groups = s->acc[2];
+    out->group_ns = s->acc[2] ? s->acc[3] * 1000.0 / tpu / double(s->acc[2]) : 0.0;
+    out->answered = s->acc[4];
     return NFFACL_OK;
 }
 

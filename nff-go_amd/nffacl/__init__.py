@@ -139,7 +139,9 @@ _batcher_stats = _sig("nffacl_batcher_get_stats", _i, _vp, ctypes.POINTER(Batche
 _batcher_destroy = _sig("nffacl_batcher_destroy", None, _vp)
 class ServiceStats(ctypes.Structure):
     _fields_ = [("launches", ctypes.c_uint64), ("requests", ctypes.c_uint64), ("timeouts", ctypes.c_uint64),
-                ("running", ctypes.c_uint64), ("table_oob", ctypes.c_uint64)]
+                ("running", ctypes.c_uint64), ("table_oob", ctypes.c_uint64), ("polls", ctypes.c_uint64),
+                ("poll_ns", ctypes.c_double), ("groups", ctypes.c_uint64), ("group_ns", ctypes.c_double),
+                ("answered", ctypes.c_uint64)]
 
 
 _rules_prepare = _sig("nffacl_rules_prepare", _i, _vp, _i)

@@ -90,9 +90,11 @@ int main(int argc, char **argv) {
     nffacl_service_get_stats(packet::detail::service(packet::ACLDevice()), &st);
     std::printf("{\"threads\": %u, \"calls\": %llu, \"mpps\": %.3f, \"lat_us_p50\": %.2f, \"lat_us_p90\": %.2f, "
                 "\"lat_us_p99\": %.2f, \"lat_us_p999\": %.1f, \"wrong\": %llu, \"launches\": %llu, "
-                "\"timeouts\": %llu}\n",
+                "\"timeouts\": %llu, \"polls\": %llu, \"poll_ns\": %.0f, \"groups\": %llu, \"group_ns\": %.0f, "
+                "\"answered\": %llu}\n",
                 threads, (unsigned long long)total.load(), total.load() / dt / 1e6, pct(0.5), pct(0.9), pct(0.99),
                 pct(0.999), (unsigned long long)bad.load(), (unsigned long long)st.launches,
-                (unsigned long long)st.timeouts);
+                (unsigned long long)st.timeouts, (unsigned long long)st.polls, st.poll_ns,
+                (unsigned long long)st.groups, st.group_ns, (unsigned long long)st.answered);
     return bad.load() ? 1 : 0;
 }
