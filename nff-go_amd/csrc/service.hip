@@ -62,10 +62,11 @@ namespace nffacl {
 namespace dev {
 
 struct SvcArgs {
-    const uint8_t *box;     // device alias of the mailboxes (kSvcBoxBytes each)
+    const uint8_t *box;     // device alias of the mailboxes (kSvcBoxBytes each), then the bells (u32 each)
     uint64_t *resp;         // device alias of the responses (kSvcRespStride words each)
     uint32_t *ctrl;         // ctrl[0] != 0: stop (host); ctrl[1] != 0: restart (a wave saw a newer table)
-    uint32_t box_bytes;     // bytes of the mailbox array (buffer range)
+    uint32_t box_bytes;     // bytes of the mailbox array (the bells follow it)
+    uint32_t range_bytes;   // mailboxes + bells (buffer range)
     uint32_t epoch;         // table generations <= epoch were uploaded before this launch
     uint64_t *stats;        // per wave kSvcStatWords u64 (host memory), written at exit
     uint32_t lds_dwords;    // INDEXED tables up to this size are staged in LDS (0: never)
@@ -156,8 +157,7 @@ __global__ void __launch_bounds__(64) k_service(SvcArgs a) {
     const uint32_t lane = lane_id();
     const uint32_t mb = blockIdx.x * 64u + lane;  // mailboxes come in whole waves
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(a.box), 0,
-                                                                        static_cast<int>(a.box_bytes), 0x00020000);
-    const uint32_t box = mb * kSvcBoxBytes;
+                                                                        static_cast<int>(a.range_bytes), 0x00020000);
     uint64_t *resp = a.resp + size_t(mb) * kSvcRespStride;
     uint32_t done = static_cast<uint32_t>(__hip_atomic_load(resp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >> 32);
     const uint64_t t0 = wall_clock64();
@@ -178,19 +178,29 @@ __global__ void __launch_bounds__(64) k_service(SvcArgs a) {
     // (LDS-staged tables issue no vector memory reads that would wait behind
     // it).  A poll reads the whole mailbox of lanes answered within `hot`,
     // only the tag chunk of the others.
+    // A wave with a hot mailbox reads its whole 8 KiB of mailboxes, each
+    // instruction 1 KiB contiguous (lane l: bytes 16 l of that KiB) — a few
+    // large PCIe reads instead of a 16-byte read per chunk per lane — and
+    // hands each lane its own mailbox through LDS; an idle wave reads only
+    // the 64 bells (256 contiguous bytes).
+    __shared__ u32x4 img[64 * kSvcChunks];
+    const uint32_t wave_box = blockIdx.x * 64u * kSvcBoxBytes;
+    const uint32_t bell = a.box_bytes + mb * 4u;
     u32x4 nx[kSvcChunks];
+    uint32_t nbell = 0;
     uint64_t ncw = 0, nt = t0;
     bool nhot = true;
     auto issue = [&]() {
         nt = wall_clock64();
-        nhot = nt - lane_last <= a.hot_ticks;
+        nhot = ballot(nt - lane_last <= a.hot_ticks) != 0u;  // wave-uniform
 #pragma unroll
         for (uint32_t j = 0; j < kSvcChunks; ++j) nx[j] = u32x4{0, 0, 0, 0};
+        nbell = 0;
         if (nhot) {
 #pragma unroll
-            for (uint32_t j = 0; j < kSvcChunks; ++j) nx[j] = ld16_host(rs, box + 16u * j);
+            for (uint32_t j = 0; j < kSvcChunks; ++j) nx[j] = ld16_host(rs, wave_box + 1024u * j + 16u * lane);
         } else {
-            nx[kSvcChunks - 1] = ld16_host(rs, box + 16u * (kSvcChunks - 1));
+            nbell = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(bell), 0, 17);
         }
         ncw = 0;  // stop | restart << 32
         if (lane == 0) ncw = __hip_atomic_load(reinterpret_cast<uint64_t *>(a.ctrl), __ATOMIC_RELAXED,
@@ -199,10 +209,20 @@ __global__ void __launch_bounds__(64) k_service(SvcArgs a) {
     issue();
     while (true) {
         u32x4 c[kSvcChunks];
-#pragma unroll
-        for (uint32_t j = 0; j < kSvcChunks; ++j) c[j] = nx[j];  // waits for the poll issued a pass ago
         const uint64_t cw = ncw, now = nt;
         const bool hot = nhot;
+        if (hot) {  // the poll issued a pass ago: every lane its own mailbox, through LDS
+#pragma unroll
+            for (uint32_t j = 0; j < kSvcChunks; ++j) img[64u * j + lane] = nx[j];
+            wave_lds_sync();
+#pragma unroll
+            for (uint32_t j = 0; j < kSvcChunks; ++j) c[j] = img[kSvcChunks * lane + j];
+            wave_lds_sync();
+        } else {
+#pragma unroll
+            for (uint32_t j = 0; j < kSvcChunks; ++j) c[j] = u32x4{0, 0, 0, 0};
+            c[kSvcChunks - 1].w = nbell;
+        }
         if (now - t0 > a.life_ticks) break;
         issue();  // the next pass's poll, in flight from here
         if ((__builtin_amdgcn_readlane(static_cast<uint32_t>(cw), 0) |
@@ -213,7 +233,7 @@ __global__ void __launch_bounds__(64) k_service(SvcArgs a) {
         const uint64_t t_data = wall_clock64();
         ++n_polls;
         poll_ticks += t_data - now;
-        // a cold mailbox with a new tag turns hot: read whole from the poll after next
+        // a new tag on a bell turns the wave hot: mailboxes read whole from the poll after next
         if (!hot && fresh) lane_last = now;
         bool pend = hot && fresh;
 #pragma unroll
@@ -425,6 +445,7 @@ struct nffacl_service {
     uint64_t timeout_us = 1000000;
     uint8_t *h_mem = nullptr;  // mapped, coherent pinned host memory: boxes | responses | ctrl
     uint8_t *h_box = nullptr;
+    uint32_t *h_bell = nullptr;   // per mailbox: the tag of its latest request (written after the chunks)
     uint64_t *h_resp = nullptr;
     uint32_t *h_ctrl = nullptr;
     uint64_t *h_stats = nullptr;  // per wave: the consumer's counters of its last launch
@@ -634,9 +655,10 @@ int nffacl_service_create(int hip_device, uint32_t mailboxes, uint32_t idle_us, 
     s->n_mb = mailboxes;
     s->mbx.reset(new (std::nothrow) MailboxState[mailboxes]);
     const size_t box_bytes = size_t(mailboxes) * kSvcBoxBytes;
+    const size_t bell_bytes = size_t(mailboxes) * 4;  // a multiple of 256
     const size_t resp_bytes = size_t(mailboxes) * kSvcRespStride * 8;
     const size_t stat_bytes = size_t(mailboxes / 64) * kSvcStatWords * 8;
-    const size_t bytes = box_bytes + resp_bytes + 64 + stat_bytes;
+    const size_t bytes = box_bytes + bell_bytes + resp_bytes + 64 + stat_bytes;
     hipError_t e = s->mbx ? hipSuccess : hipErrorOutOfMemory;
     if (e == hipSuccess)
         e = hipHostMalloc(reinterpret_cast<void **>(&s->h_mem), bytes, hipHostMallocMapped | hipHostMallocCoherent);
@@ -654,16 +676,19 @@ int nffacl_service_create(int hip_device, uint32_t mailboxes, uint32_t idle_us, 
     }
     std::memset(s->h_mem, 0, bytes);
     s->h_box = s->h_mem;
-    s->h_resp = reinterpret_cast<uint64_t *>(s->h_mem + box_bytes);
-    s->h_ctrl = reinterpret_cast<uint32_t *>(s->h_mem + box_bytes + resp_bytes);
+    s->h_bell = reinterpret_cast<uint32_t *>(s->h_mem + box_bytes);
+    const size_t rb = box_bytes + bell_bytes;  // responses from here
+    s->h_resp = reinterpret_cast<uint64_t *>(s->h_mem + rb);
+    s->h_ctrl = reinterpret_cast<uint32_t *>(s->h_mem + rb + resp_bytes);
     const uint64_t tpu = uint64_t(khz) / 1000;  // ticks per µs
     s->ticks_per_us = tpu;
     s->args.box = d_mem;
-    s->args.resp = reinterpret_cast<uint64_t *>(d_mem + box_bytes);
-    s->args.ctrl = reinterpret_cast<uint32_t *>(d_mem + box_bytes + resp_bytes);
-    s->args.stats = reinterpret_cast<uint64_t *>(d_mem + box_bytes + resp_bytes + 64);
-    s->h_stats = reinterpret_cast<uint64_t *>(s->h_mem + box_bytes + resp_bytes + 64);
+    s->args.resp = reinterpret_cast<uint64_t *>(d_mem + rb);
+    s->args.ctrl = reinterpret_cast<uint32_t *>(d_mem + rb + resp_bytes);
+    s->args.stats = reinterpret_cast<uint64_t *>(d_mem + rb + resp_bytes + 64);
+    s->h_stats = reinterpret_cast<uint64_t *>(s->h_mem + rb + resp_bytes + 64);
     s->args.box_bytes = static_cast<uint32_t>(box_bytes);
+    s->args.range_bytes = static_cast<uint32_t>(rb);
     s->args.idle_ticks = uint64_t(idle_us) * tpu;
     s->args.hot_ticks = 200 * tpu;
     s->args.life_ticks = 100000 * tpu;  // 100 ms, then the armer re-launches if calls keep coming
@@ -734,6 +759,7 @@ int nffacl_service_classify(nffacl_service *s, const nffacl_rules *rules, const 
     __m128i *dst = reinterpret_cast<__m128i *>(s->h_box + size_t(mb) * kSvcBoxBytes);
     for (uint32_t j = 0; j < kSvcChunks; ++j)  // ascending: the tag chunk last (x86 stores stay in order)
         _mm_store_si128(dst + j, _mm_load_si128(reinterpret_cast<const __m128i *>(&c[4 * j])));
+    __atomic_store_n(&s->h_bell[mb], tag, __ATOMIC_RELEASE);  // idle waves watch the bells
     std::atomic_thread_fence(std::memory_order_seq_cst);  // request visible before `running` is read
     if (!s->running.load(std::memory_order_seq_cst)) kick(s);
     const uint64_t *r = s->h_resp + size_t(mb) * kSvcRespStride;
