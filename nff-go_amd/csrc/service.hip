@@ -155,11 +155,14 @@ __device__ __forceinline__ uint32_t svc_classify(const uint32_t (&w)[kSvcDescDwo
 __global__ void __launch_bounds__(64) k_service(SvcArgs a) {
     __shared__ FlatScratch<2> W;
     const uint32_t lane = lane_id();
-    const uint32_t mb = blockIdx.x * 64u + lane;  // mailboxes come in whole waves
+    constexpr uint32_t MPW = kSvcMbPerWave;
+    const bool has_mb = lane < MPW;  // lanes 0..MPW-1 own the wave's mailboxes
+    const uint32_t mb = blockIdx.x * MPW + (has_mb ? lane : 0u);
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(a.box), 0,
                                                                         static_cast<int>(a.range_bytes), 0x00020000);
     uint64_t *resp = a.resp + size_t(mb) * kSvcRespStride;
-    uint32_t done = static_cast<uint32_t>(__hip_atomic_load(resp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >> 32);
+    uint32_t done = 0;
+    if (has_mb) done = static_cast<uint32_t>(__hip_atomic_load(resp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >> 32);
     const uint64_t t0 = wall_clock64();
     uint64_t last = t0, lane_last = t0;  // hot at start: the call that armed us is read whole
     uint32_t cur_key = 0xFFFFFFFFu;  // generation << 1 | vlan of the descriptor in `w`
@@ -178,28 +181,32 @@ __global__ void __launch_bounds__(64) k_service(SvcArgs a) {
     // (LDS-staged tables issue no vector memory reads that would wait behind
     // it).  A poll reads the whole mailbox of lanes answered within `hot`,
     // only the tag chunk of the others.
-    // A wave with a hot mailbox reads its whole 8 KiB of mailboxes, each
-    // instruction 1 KiB contiguous (lane l: bytes 16 l of that KiB) — a few
-    // large PCIe reads instead of a 16-byte read per chunk per lane — and
-    // hands each lane its own mailbox through LDS; an idle wave reads only
-    // the 64 bells (256 contiguous bytes).
-    __shared__ u32x4 img[64 * kSvcChunks];
-    const uint32_t wave_box = blockIdx.x * 64u * kSvcBoxBytes;
+    // A wave owns MPW mailboxes.  While one of them is hot the wave reads all
+    // of them whole, each load instruction 1 KiB contiguous (lane l: bytes
+    // 16 l of that KiB, i.e. chunk l % 8 of mailbox l / 8) — a few large PCIe
+    // reads instead of a 16-byte read per chunk per lane — and hands each
+    // mailbox lane its own eight chunks through LDS; an idle wave reads only
+    // its MPW bells (contiguous u32s).  Small waves keep every poll one
+    // round trip short and let the waves of busy mailboxes classify in
+    // parallel on their own SIMDs.
+    constexpr uint32_t kLoads = MPW * kSvcBoxBytes / 1024u;
+    __shared__ u32x4 img[64 * kLoads];
+    const uint32_t wave_box = blockIdx.x * MPW * kSvcBoxBytes;
     const uint32_t bell = a.box_bytes + mb * 4u;
-    u32x4 nx[kSvcChunks];
+    u32x4 nx[kLoads];
     uint32_t nbell = 0;
     uint64_t ncw = 0, nt = t0;
     bool nhot = true;
     auto issue = [&]() {
         nt = wall_clock64();
-        nhot = ballot(nt - lane_last <= a.hot_ticks) != 0u;  // wave-uniform
+        nhot = ballot(has_mb && nt - lane_last <= a.hot_ticks) != 0u;  // wave-uniform
 #pragma unroll
-        for (uint32_t j = 0; j < kSvcChunks; ++j) nx[j] = u32x4{0, 0, 0, 0};
+        for (uint32_t j = 0; j < kLoads; ++j) nx[j] = u32x4{0, 0, 0, 0};
         nbell = 0;
         if (nhot) {
 #pragma unroll
-            for (uint32_t j = 0; j < kSvcChunks; ++j) nx[j] = ld16_host(rs, wave_box + 1024u * j + 16u * lane);
-        } else {
+            for (uint32_t j = 0; j < kLoads; ++j) nx[j] = ld16_host(rs, wave_box + 1024u * j + 16u * lane);
+        } else if (has_mb) {
             nbell = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(bell), 0, 17);
         }
         ncw = 0;  // stop | restart << 32
@@ -211,16 +218,18 @@ __global__ void __launch_bounds__(64) k_service(SvcArgs a) {
         u32x4 c[kSvcChunks];
         const uint64_t cw = ncw, now = nt;
         const bool hot = nhot;
-        if (hot) {  // the poll issued a pass ago: every lane its own mailbox, through LDS
 #pragma unroll
-            for (uint32_t j = 0; j < kSvcChunks; ++j) img[64u * j + lane] = nx[j];
+        for (uint32_t j = 0; j < kSvcChunks; ++j) c[j] = u32x4{0, 0, 0, 0};
+        if (hot) {  // the poll issued a pass ago: every mailbox lane its own chunks, through LDS
+#pragma unroll
+            for (uint32_t j = 0; j < kLoads; ++j) img[64u * j + lane] = nx[j];
             wave_lds_sync();
+            if (has_mb) {
 #pragma unroll
-            for (uint32_t j = 0; j < kSvcChunks; ++j) c[j] = img[kSvcChunks * lane + j];
+                for (uint32_t j = 0; j < kSvcChunks; ++j) c[j] = img[kSvcChunks * lane + j];
+            }
             wave_lds_sync();
         } else {
-#pragma unroll
-            for (uint32_t j = 0; j < kSvcChunks; ++j) c[j] = u32x4{0, 0, 0, 0};
             c[kSvcChunks - 1].w = nbell;
         }
         if (now - t0 > a.life_ticks) break;
@@ -229,7 +238,7 @@ __global__ void __launch_bounds__(64) k_service(SvcArgs a) {
              __builtin_amdgcn_readlane(static_cast<uint32_t>(cw >> 32), 0)) != 0u)
             break;
         const uint32_t tag = c[kSvcChunks - 1].w;
-        const bool fresh = tag != done;
+        const bool fresh = has_mb && tag != done;
         const uint64_t t_data = wall_clock64();
         ++n_polls;
         poll_ticks += t_data - now;
@@ -516,8 +525,8 @@ void armer_main(nffacl_service *s) {
         s->running.store(true, std::memory_order_seq_cst);
         __atomic_store_n(&s->h_ctrl[1], 0u, __ATOMIC_SEQ_CST);
         s->args.epoch = table_epoch();  // every table of this generation or older is in HBM
-        hipLaunchKernelGGL(dev::k_service, dim3(s->n_mb / 64), dim3(64), size_t(s->args.lds_dwords) * 4, s->stream,
-                           s->args);
+        hipLaunchKernelGGL(dev::k_service, dim3(s->n_mb / kSvcMbPerWave), dim3(64), size_t(s->args.lds_dwords) * 4,
+                           s->stream, s->args);
         hipError_t e = hipGetLastError();
         if (e == hipSuccess) e = hipEventRecord(s->done, s->stream);
         if (e == hipSuccess) {
@@ -526,7 +535,7 @@ void armer_main(nffacl_service *s) {
         }
         s->running.store(false, std::memory_order_seq_cst);
         lk.lock();
-        for (uint32_t wv = 0; wv < s->n_mb / 64; ++wv)
+        for (uint32_t wv = 0; wv < s->n_mb / kSvcMbPerWave; ++wv)
             for (uint32_t i = 0; i < kSvcStatWords; ++i) {
                 s->acc[i] += __atomic_load_n(&s->h_stats[wv * kSvcStatWords + i], __ATOMIC_ACQUIRE);
                 __atomic_store_n(&s->h_stats[wv * kSvcStatWords + i], 0ull, __ATOMIC_RELAXED);
@@ -559,7 +568,11 @@ uint32_t my_mailbox(nffacl_service *s) {
         if (c.id == s->id) return c.mb;
     Slot &c = cache[victim++ % 4];
     c.id = s->id;
-    c.mb = s->next_mb.fetch_add(1, std::memory_order_relaxed) % s->n_mb;
+    // consecutive threads on different waves: each wave polls and classifies
+    // for few callers, the waves of busy mailboxes in parallel
+    const uint32_t k = s->next_mb.fetch_add(1, std::memory_order_relaxed) % s->n_mb;
+    const uint32_t waves = s->n_mb / kSvcMbPerWave;
+    c.mb = (k % waves) * kSvcMbPerWave + k / waves;
     return c.mb;
 }
 
@@ -657,7 +670,7 @@ int nffacl_service_create(int hip_device, uint32_t mailboxes, uint32_t idle_us, 
     const size_t box_bytes = size_t(mailboxes) * kSvcBoxBytes;
     const size_t bell_bytes = size_t(mailboxes) * 4;  // a multiple of 256
     const size_t resp_bytes = size_t(mailboxes) * kSvcRespStride * 8;
-    const size_t stat_bytes = size_t(mailboxes / 64) * kSvcStatWords * 8;
+    const size_t stat_bytes = size_t(mailboxes / kSvcMbPerWave) * kSvcStatWords * 8;
     const size_t bytes = box_bytes + bell_bytes + resp_bytes + 64 + stat_bytes;
     hipError_t e = s->mbx ? hipSuccess : hipErrorOutOfMemory;
     if (e == hipSuccess)
