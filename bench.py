@@ -440,15 +440,23 @@ def main():
                 "bit_exact_vs_local": bool(torch.equal(full.cpu(), st["port"].cpu())),
             }
 
-    # ---- PCIe-inclusive rate (not `value`; DESIGN.md) ----
+    # ---- PCIe-inclusive rate (not `value`; DESIGN.md §7) ----
+    # L3ACLPort over host slots: pinned 64-byte slots in, the verdict array
+    # in pinned memory too (the kernels read the slots and write the verdicts
+    # over PCIe, nffacl_classify_host); best of 3 calls of 2^23 packets
     if rank == 0 and not args.no_host and not st["frames_mode"]:
-        m = min(n, 1 << 22)
+        m = min(n, 1 << 23)
         pinned = torch.from_numpy(st["slots"][: m * 64]).pin_memory().numpy()
-        eng.classify_host(pinned, 64, m)
-        t = time.perf_counter()
-        hp, _ = eng.classify_host(pinned, 64, m)
-        dt = time.perf_counter() - t
-        out["host_inclusive_mpps"] = round(m / dt / 1e6, 1)
+        hout = torch.empty(m, dtype=torch.int32).pin_memory().numpy().view(np.uint32)
+        eng.classify_host(pinned, 64, m, out=hout, permit=False)
+        best = float("inf")
+        for _ in range(3):
+            t = time.perf_counter()
+            hp, _ = eng.classify_host(pinned, 64, m, out=hout, permit=False)
+            best = min(best, time.perf_counter() - t)
+        out["host_inclusive_mpps"] = round(m / best / 1e6, 1)
+        out["host_inclusive"] = {"packets": m, "gbps_in": round(m * 64 / best / 1e9, 1),
+                                 "input": "pinned host 64 B slots", "output": "pinned host u32 verdicts"}
         out["host_inclusive_bit_exact_sample"] = bool((hp[idx[idx < m]] == got[idx[idx < m]]).all())
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -332,15 +332,14 @@ void nffacl_engine_destroy(nffacl_engine *eng) {
     // no classification may be running (header contract): the engine's own
     // streams are synchronised, the table retires behind the user streams'
     // recorded work, and home.shutdown() waits for exactly that
-    for (int b = 0; b < 2; ++b)
+    for (int b = 0; b < nffacl_engine::kHostBufs; ++b)
         if (eng->streams[b]) (void)hipStreamSynchronize(eng->streams[b]);
     eng->active.reset();
     eng->home.shutdown();
-    for (int b = 0; b < 2; ++b) {
+    for (int b = 0; b < nffacl_engine::kHostBufs; ++b) {
         if (eng->h_stage[b]) (void)hipHostFree(eng->h_stage[b]);
         if (eng->h_port[b]) (void)hipHostFree(eng->h_port[b]);
         if (eng->d_slots[b]) (void)hipFree(eng->d_slots[b]);
-        if (eng->d_port[b]) (void)hipFree(eng->d_port[b]);
         if (eng->streams[b]) (void)hipStreamDestroy(eng->streams[b]);
         if (eng->done[b]) (void)hipEventDestroy(eng->done[b]);
     }
@@ -403,31 +402,35 @@ int nffacl_classify_frames_device_ex(nffacl_engine *eng, const uint8_t *d_frames
                          static_cast<hipStream_t>(stream), flags);
 }
 
-// Staging sized to the request: small bursts get small pinned buffers, large
-// batches stream through two 1 M-packet stages.
+// Host pipeline buffers, sized to the request: small calls get small pinned
+// buffers, large ones stream through `host_bufs` chunks of 2^host_chunk
+// packets (one stream each).
 static int ensure_host_pipeline(nffacl_engine *eng, uint32_t stride, uint64_t n) {
+    const int nb = std::max(2, std::min(eng->tune.host_bufs, int(nffacl_engine::kHostBufs)));
+    const size_t cap = size_t(1) << std::max(12, std::min(eng->tune.host_chunk, 24));
     size_t chunk = size_t(1) << 12;
-    while (chunk < n && chunk < (size_t(1) << 20)) chunk <<= 1;
-    if (eng->chunk >= chunk && eng->staged_stride >= stride) return NFFACL_OK;
-    chunk = std::max(chunk, eng->chunk);
+    while (chunk < n && chunk < cap) chunk <<= 1;
+    if (eng->chunk >= chunk && eng->staged_stride >= stride && eng->nbufs == nb) return NFFACL_OK;
+    if (eng->nbufs == nb) chunk = std::max(chunk, eng->chunk);
     stride = std::max(stride, eng->staged_stride);
-    for (int b = 0; b < 2; ++b) {
+    for (int b = 0; b < nffacl_engine::kHostBufs; ++b) {
+        if (eng->streams[b]) (void)hipStreamSynchronize(eng->streams[b]);
         if (eng->h_stage[b]) { (void)hipHostFree(eng->h_stage[b]); eng->h_stage[b] = nullptr; }
         if (eng->d_slots[b]) { (void)hipFree(eng->d_slots[b]); eng->d_slots[b] = nullptr; }
         if (eng->h_port[b]) { (void)hipHostFree(eng->h_port[b]); eng->h_port[b] = nullptr; eng->d_hport[b] = nullptr; }
-        if (eng->d_port[b]) { (void)hipFree(eng->d_port[b]); eng->d_port[b] = nullptr; }
     }
     eng->chunk = 0;
-    for (int b = 0; b < 2; ++b) {
+    eng->nbufs = 0;
+    for (int b = 0; b < nb; ++b) {
         HIP_CHECK(hipHostMalloc(reinterpret_cast<void **>(&eng->h_stage[b]), chunk * stride, hipHostMallocDefault));
         HIP_CHECK(hipMalloc(reinterpret_cast<void **>(&eng->d_slots[b]), chunk * stride));
         HIP_CHECK(hipHostMalloc(reinterpret_cast<void **>(&eng->h_port[b]), chunk * 4, hipHostMallocMapped));
         HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void **>(&eng->d_hport[b]), eng->h_port[b], 0));
-        HIP_CHECK(hipMalloc(reinterpret_cast<void **>(&eng->d_port[b]), chunk * 4));
         if (!eng->streams[b]) HIP_CHECK(hipStreamCreateWithFlags(&eng->streams[b], hipStreamNonBlocking));
         if (!eng->done[b]) HIP_CHECK(hipEventCreateWithFlags(&eng->done[b], hipEventDisableTiming));
     }
     eng->chunk = chunk;
+    eng->nbufs = nb;
     eng->staged_stride = stride;
     return NFFACL_OK;
 }
@@ -457,20 +460,24 @@ int nffacl_classify_host_ex(nffacl_engine *eng, const uint8_t *h_slots, uint32_t
     int st = ensure_host_pipeline(eng, stride, n);
     if (st != NFFACL_OK) return st;
     const TablePtr t = acquire_table(eng);  // one table for every chunk of this call
-    // Pinned input (one registered allocation, 16-byte aligned): no copy at
-    // all — the kernel reads the slots over PCIe itself (its lane-contiguous
-    // 1 KiB loads keep the link busy; one DMA direction less to schedule) and
-    // writes the verdicts into mapped pinned memory, the caller's when that is
-    // pinned too.  Otherwise: staged chunks, H2D -> kernel -> D2H.
-    const uint8_t *d_host_slots = nullptr;
-    if (range_is_pinned(h_slots, n * stride) && reinterpret_cast<uintptr_t>(h_slots) % 16 == 0)
-        d_host_slots = static_cast<const uint8_t *>(host_alias(h_slots));
+    // Input: pinned caller memory (one registered allocation) is read where it
+    // lies — by the kernel itself over PCIe (zero-copy: its lane-contiguous
+    // 1 KiB loads keep the link busy, no copy engine), or DMA'd chunk by chunk
+    // into HBM (NFFACL_TUNE_HOST_DMA=1); pageable input is copied into pinned
+    // staging, then DMA'd.  Output: every kernel writes its verdicts over PCIe
+    // into mapped pinned memory — the caller's when that is pinned, else the
+    // chunk's staging, copied out when the chunk completes.
+    const bool pinned_in = range_is_pinned(h_slots, n * stride) && reinterpret_cast<uintptr_t>(h_slots) % 16 == 0;
+    const uint8_t *d_host_slots = pinned_in ? static_cast<const uint8_t *>(host_alias(h_slots)) : nullptr;
+    const bool zero_copy = d_host_slots && eng->tune.host_dma == 0;
     uint32_t *d_host_port = nullptr;
-    if (d_host_slots && h_port && range_is_pinned(h_port, n * 4) && reinterpret_cast<uintptr_t>(h_port) % 4 == 0)
+    if (h_port && range_is_pinned(h_port, n * 4) && reinterpret_cast<uintptr_t>(h_port) % 4 == 0)
         d_host_port = static_cast<uint32_t *>(host_alias(h_port));
     const uint64_t chunk = eng->chunk;
+    const int nb = eng->nbufs;
     const uint64_t nchunks = (n + chunk - 1) / chunk;
-    uint64_t pending_chunk[2] = {~0ull, ~0ull};
+    uint64_t pending_chunk[nffacl_engine::kHostBufs];
+    for (int b = 0; b < nffacl_engine::kHostBufs; ++b) pending_chunk[b] = ~0ull;
     auto drain = [&](int b) -> int {
         if (pending_chunk[b] == ~0ull) return NFFACL_OK;
         HIP_CHECK(hipEventSynchronize(eng->done[b]));
@@ -485,30 +492,30 @@ int nffacl_classify_host_ex(nffacl_engine *eng, const uint8_t *h_slots, uint32_t
         return NFFACL_OK;
     };
     for (uint64_t c = 0; c < nchunks; ++c) {
-        const int b = static_cast<int>(c & 1);
+        const int b = static_cast<int>(c % uint64_t(nb));
         if ((st = drain(b)) != NFFACL_OK) return st;
         const uint64_t first = c * chunk;
         const uint64_t cnt = std::min<uint64_t>(chunk, n - first);
-        if (d_host_slots) {
-            uint32_t *out = d_host_port ? d_host_port + first : eng->d_hport[b];
-            st = launch_slots(eng, t.get(), d_host_slots + first * stride, stride, cnt, out, nullptr, eng->streams[b],
-                              flags);
-            if (st != NFFACL_OK) return st;
+        uint32_t *out = d_host_port ? d_host_port + first : eng->d_hport[b];
+        const uint8_t *in = nullptr;
+        if (zero_copy) {
+            in = d_host_slots + first * stride;
         } else {
             const uint8_t *src = h_slots + first * stride;
-            std::memcpy(eng->h_stage[b], src, cnt * stride);
-            HIP_CHECK(hipMemcpyAsync(eng->d_slots[b], eng->h_stage[b], cnt * stride, hipMemcpyHostToDevice,
-                                     eng->streams[b]));
-            st = launch_slots(eng, t.get(), eng->d_slots[b], stride, cnt, eng->d_port[b], nullptr, eng->streams[b],
-                              flags);
-            if (st != NFFACL_OK) return st;
-            HIP_CHECK(hipMemcpyAsync(eng->h_port[b], eng->d_port[b], cnt * 4, hipMemcpyDeviceToHost, eng->streams[b]));
+            if (!pinned_in) {
+                std::memcpy(eng->h_stage[b], src, cnt * stride);
+                src = eng->h_stage[b];
+            }
+            HIP_CHECK(hipMemcpyAsync(eng->d_slots[b], src, cnt * stride, hipMemcpyHostToDevice, eng->streams[b]));
+            in = eng->d_slots[b];
         }
+        st = launch_slots(eng, t.get(), in, stride, cnt, out, nullptr, eng->streams[b], flags);
+        if (st != NFFACL_OK) return st;
         HIP_CHECK(hipEventRecord(eng->done[b], eng->streams[b]));
         pending_chunk[b] = c;
     }
-    for (int b = 0; b < 2; ++b)
-        if ((st = drain(b)) != NFFACL_OK) return st;
+    for (uint64_t c = nchunks > uint64_t(nb) ? nchunks - nb : 0; c < nchunks; ++c)  // completion order
+        if ((st = drain(static_cast<int>(c % uint64_t(nb)))) != NFFACL_OK) return st;
     return NFFACL_OK;
 }
 

@@ -363,9 +363,11 @@ enum TableMode : int {
 extern __shared__ __attribute__((aligned(16))) uint32_t lds_tab[];
 
 // Table accessors: the whole table staged in LDS, or read through L1/L2.
-// ld4(i): i is a multiple of 4 (entries are 16-byte aligned, table.hpp) and is
-// indexed in vector units so the compiler can emit one ds_read_b128 /
-// global_load_dwordx4 (a byte-offset cast only gets split ds_read2_b32 pairs).
+// ld4(i): i is a multiple of 4 (entries are 16-byte aligned, table.hpp), told
+// to the compiler so that it emits one ds_read_b128 / global_load_dwordx4 and
+// folds the constant part of i into the instruction's offset field (indexing
+// in vector units, i >> 2, cost a mask and an add per load: C2's walk -9 %
+// VALU instructions).
 // List bounds dir[t], dir[t + 1] of a plain u32 directory (one ds_read2 /
 // two dword loads).
 template <class T>
@@ -382,7 +384,8 @@ struct LdsTab {
         bounds32(*this, dir, t, lo, hi);
     }
     __device__ __forceinline__ u32x4 ld4(uint32_t i) const {
-        return reinterpret_cast<const u32x4 *>(lds_tab)[i >> 2];
+        __builtin_assume((i & 3u) == 0u);
+        return *reinterpret_cast<const u32x4 *>(reinterpret_cast<const char *>(lds_tab) + i * 4u);
     }
 };
 struct GlobalTab {
@@ -394,7 +397,8 @@ struct GlobalTab {
         bounds32(*this, dir, t, lo, hi);
     }
     __device__ __forceinline__ u32x4 ld4(uint32_t i) const {
-        return reinterpret_cast<const u32x4 *>(p)[i >> 2];
+        __builtin_assume((i & 3u) == 0u);
+        return *reinterpret_cast<const u32x4 *>(p + i);
     }
 };
 // HYBRID lane form: directories (ld) staged in LDS, entries (ld4) global.
@@ -434,7 +438,8 @@ struct DirTab {
         hi = (((t + 1u) >> kDir16GroupShift) != g ? b1 : b0) + (odd ? w1 & 0xFFFFu : w0 >> 16);
     }
     __device__ __forceinline__ u32x4 ld4(uint32_t i) const {
-        return reinterpret_cast<const u32x4 *>(p)[i >> 2];
+        __builtin_assume((i & 3u) == 0u);
+        return *reinterpret_cast<const u32x4 *>(p + i);
     }
 };
 using SplitTab = DirTab<true>;
@@ -802,7 +807,10 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
             six[j] = (dp & 1u) != 0u;
             // UNCOND: lanes past the wave's candidates load entry 0 of the
             // IPv4 list (untested) instead of branching around the load
-            // (profiles/r2_exact/uncond/)
+            // (profiles/r2_exact/uncond/).  (Round 3: window-relative entry
+            // offsets with one 24-bit multiply-add per candidate — fewer VALU
+            // per round, more per window and +7-11 VGPRs — ran C3 0.502 vs
+            // 0.472 ms, C5 even; profiles/r3_ab/)
             const uint32_t ent = !UNCOND || valid[j] ? k + static_cast<uint32_t>(static_cast<int32_t>(dp) >> 1) : 0u;
             const uint32_t *e = six[j] && (!UNCOND || valid[j]) ? E6 + ent * kHybEnt6Dwords : E4 + ent * kHybEnt4Dwords;
             if (UNCOND || valid[j]) {

@@ -231,7 +231,10 @@ k_indexed_frames(const uint8_t *__restrict__ frames, const uint64_t *__restrict_
     constexpr bool PF = TM == kTabSplit;  // (flat-LDS: +0.6 % on C3, profiles/r1_flat_lds/cold/)
     // (flat-LDS, round 2: one prefetch buffer with copies, 2 rounds — 124
     // VGPRs, no spill — ran 0.487 vs 0.469 ms on C3: the frame loads are not
-    // what the walk waits on; profiles/r2_valu/pfab/)
+    // what the walk waits on; profiles/r2_valu/pfab/.  Round 3: the same
+    // prefetch issued from inside the walk, after the first window's entry
+    // loads so that no entry wait queues behind it: 0.496 vs 0.473 ms,
+    // profiles/r3_ab/)
     // Frame lines load cooperatively (load_frames_rs) and are assembled per
     // lane just before their batch is classified.
     auto run_batch = [&](uint64_t b, uint64_t ds, const u32x4(&v)[4]) {
@@ -303,6 +306,12 @@ bool Tune::from_env(Tune &t, std::string &err) {
     if (set) t.rounds = static_cast<int>(v);
     if (!env_knob("NFFACL_TUNE_LDS", 0, 1, v, set, err)) return false;
     if (set) t.lds = static_cast<int>(v);
+    if (!env_knob("NFFACL_TUNE_HOST_DMA", 0, 1, v, set, err)) return false;
+    if (set) t.host_dma = static_cast<int>(v);
+    if (!env_knob("NFFACL_TUNE_HOST_BUFS", 2, nffacl_engine::kHostBufs, v, set, err)) return false;
+    if (set) t.host_bufs = static_cast<int>(v);
+    if (!env_knob("NFFACL_TUNE_HOST_CHUNK", 12, 24, v, set, err)) return false;
+    if (set) t.host_chunk = static_cast<int>(v);
     return CompileOptions::from_env(t.copt, err);
 }
 

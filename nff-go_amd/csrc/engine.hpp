@@ -36,6 +36,12 @@ struct Tune {
     int per_cu = 0;  // NFFACL_TUNE_PER_CU: workgroups per CU (0 = kernel default)
     int rounds = 0;  // NFFACL_TUNE_ROUNDS: flat walks, loads in flight (0 = compiled, 2 or 4)
     int lds = 1;     // NFFACL_TUNE_LDS: 0 keeps INDEXED tables in global memory
+    // nffacl_classify_host (capi.cpp): pinned input read by the kernel over
+    // PCIe (0) or DMA'd to HBM first (1); buffers = streams in flight (2..4);
+    // packets per chunk, log2
+    int host_dma = 0;      // NFFACL_TUNE_HOST_DMA
+    int host_bufs = 3;     // NFFACL_TUNE_HOST_BUFS
+    int host_chunk = 20;   // NFFACL_TUNE_HOST_CHUNK (log2, 12..24)
     CompileOptions copt;  // NFFACL_TUNE_FLAT / _DIR_KB / _DIR16 (table layout)
     // false (+ `err`) if a set variable is out of range
     static bool from_env(Tune &t, std::string &err);
@@ -67,14 +73,15 @@ struct nffacl_engine {
     nffacl::TablePtr active;
     // Host-inclusive pipeline state (nffacl_classify_host), created lazily.
     std::mutex host_mu;
+    static constexpr int kHostBufs = 4;
     size_t chunk = 0;
-    uint8_t *h_stage[2] = {nullptr, nullptr};
-    uint32_t *h_port[2] = {nullptr, nullptr};   // mapped pinned verdict staging
-    uint32_t *d_hport[2] = {nullptr, nullptr};  // their device aliases (zero-copy path)
-    uint8_t *d_slots[2] = {nullptr, nullptr};
-    uint32_t *d_port[2] = {nullptr, nullptr};
-    hipStream_t streams[2] = {nullptr, nullptr};
-    hipEvent_t done[2] = {nullptr, nullptr};
+    int nbufs = 0;
+    uint8_t *h_stage[kHostBufs] = {};    // pinned input staging (pageable callers)
+    uint32_t *h_port[kHostBufs] = {};    // mapped pinned verdict staging
+    uint32_t *d_hport[kHostBufs] = {};   // their device aliases (the kernels write there)
+    uint8_t *d_slots[kHostBufs] = {};    // HBM input chunks (DMA forms)
+    hipStream_t streams[kHostBufs] = {};
+    hipEvent_t done[kHostBufs] = {};
     uint32_t staged_stride = 0;
 };
 

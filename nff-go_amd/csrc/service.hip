@@ -8,10 +8,11 @@
 // with the *L3Rules passed per call and swapped by the user at any time
 // (step08.go:38-44).  Layout and protocol: service.hpp.
 //
-// Device side: one wave64 per 64 mailboxes (lane = mailbox), polling with
-// 16-byte sc0 sc1 loads (they bypass L1/L2 and read host memory over PCIe),
-// mailboxes that were busy in the last `hot` window read whole each pass,
-// idle ones read only their tag chunk.  Complete requests are grouped by
+// Device side: one wave64 per kSvcMbPerWave (8) mailboxes, polling with
+// sc0 sc1 loads (they bypass L1/L2 and read host memory over PCIe): a wave
+// with a mailbox answered in the last `hot` window reads its 1 KiB of
+// mailboxes whole with one coalesced load per pass, an idle wave reads only
+// its eight bell words.  Complete requests are grouped by
 // table generation (wave-uniform descriptor), parsed and classified by the
 // same device functions as the batch kernels (classify.hpp), and answered
 // with ONE 8-byte system-scope store {tag, port} per request.  The kernel
@@ -443,7 +444,25 @@ namespace {
 struct alignas(64) MailboxState {
     std::atomic<uint32_t> lock{0};  // owner (threads beyond the mailbox count share)
     uint32_t seq = 0;               // last tag posted
+    uint32_t lat_min = 0;           // under lock: recent minimum call latency, ns (0: none yet)
 };
+
+// CPUs this process may keep busy: its affinity mask, capped by a cgroup v2
+// CPU quota ("QUOTA PERIOD" in cpu.max) when one is set.
+uint32_t cpu_budget() {
+    cpu_set_t set;
+    uint32_t n = 0;
+    if (sched_getaffinity(0, sizeof set, &set) == 0) n = static_cast<uint32_t>(CPU_COUNT(&set));
+    if (n == 0) n = std::max(1u, std::thread::hardware_concurrency());
+    if (FILE *f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+        char q[32] = {0};
+        unsigned long period = 0;
+        if (std::fscanf(f, "%31s %lu", q, &period) == 2 && period > 0 && std::isdigit(static_cast<unsigned char>(q[0])))
+            n = std::min<uint32_t>(n, std::max(1ul, (std::strtoul(q, nullptr, 10) + period - 1) / period));
+        std::fclose(f);
+    }
+    return n;
+}
 
 }  // namespace
 
@@ -452,6 +471,13 @@ struct nffacl_service {
     uint32_t id = 0;  // process-unique: keys the callers' thread-local mailbox choice
     uint32_t n_mb = 0;
     uint64_t timeout_us = 1000000;
+    // After posting, a caller sleeps through most of the round trip instead
+    // of spinning it once the callers outnumber half the CPUs this process
+    // may use (sleep_ns < 0: adaptive, per mailbox; 0: never; > 0: fixed;
+    // NFFACL_TUNE_SVC_SLEEP_NS).  Under a CPU quota every spinning caller
+    // burns the quota the others need: throughput = quota / CPU per call.
+    int32_t sleep_ns = -1;
+    uint32_t cpus = 1;
     uint8_t *h_mem = nullptr;  // mapped, coherent pinned host memory: boxes | responses | ctrl
     uint8_t *h_box = nullptr;
     uint32_t *h_bell = nullptr;   // per mailbox: the tag of its latest request (written after the chunks)
@@ -516,6 +542,7 @@ bool any_pending(const nffacl_service *s) {
 
 void armer_main(nffacl_service *s) {
     (void)hipSetDevice(s->device);
+    (void)prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);  // its naps: 20 us, not 20 + 50 us
     std::unique_lock<std::mutex> lk(s->mu);
     while (true) {
         s->cv.wait(lk, [&] { return s->kick || s->stop; });
@@ -531,7 +558,12 @@ void armer_main(nffacl_service *s) {
         if (e == hipSuccess) e = hipEventRecord(s->done, s->stream);
         if (e == hipSuccess) {
             s->launches.fetch_add(1, std::memory_order_relaxed);
-            e = hipEventSynchronize(s->done);  // blocking-sync event: the armer sleeps
+            // Sleep-poll for the kernel's exit: a blocking hipEventSynchronize
+            // still kept one CPU busy for the kernel's whole life (round 3 sweep:
+            // 2.0 CPUs at one caller), and under a CPU quota that CPU is the
+            // callers'.  20 us late at most, once per launch.
+            const timespec nap{0, 20000};
+            while ((e = hipEventQuery(s->done)) == hipErrorNotReady) (void)nanosleep(&nap, nullptr);
         }
         s->running.store(false, std::memory_order_seq_cst);
         lk.lock();
@@ -645,7 +677,16 @@ int nffacl_rules_prepare(const nffacl_rules *rules, int hip_device) {
 int nffacl_service_create(int hip_device, uint32_t mailboxes, uint32_t idle_us, nffacl_service **out) {
     if (!out) return NFFACL_ERR_INVALID_ARG;
     *out = nullptr;
-    if (mailboxes == 0) mailboxes = 128;
+    if (mailboxes == 0) {  // default: 256 (NFFACL_TUNE_SVC_MAILBOXES)
+        long v = 0;
+        bool set = false;
+        std::string err;
+        if (!env_knob("NFFACL_TUNE_SVC_MAILBOXES", 64, 4096, v, set, err)) {
+            set_last_error(err);
+            return NFFACL_ERR_INVALID_ARG;
+        }
+        mailboxes = set ? static_cast<uint32_t>(v) : 256u;
+    }
     if (mailboxes % 64 != 0 || mailboxes > 4096 || idle_us > 10000000u) return NFFACL_ERR_INVALID_ARG;
     if (idle_us == 0) idle_us = 2000;
     int count = 0;
@@ -681,7 +722,7 @@ int nffacl_service_create(int hip_device, uint32_t mailboxes, uint32_t idle_us, 
     if (e == hipSuccess) e = hipDeviceGetStreamPriorityRange(&lo, &hi);
     // its own (highest-priority) stream: kept off the queues of batch work
     if (e == hipSuccess) e = hipStreamCreateWithPriority(&s->stream, hipStreamNonBlocking, hi);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&s->done, hipEventBlockingSync | hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&s->done, hipEventDisableTiming);
     if (e != hipSuccess) {
         set_last_error(std::string("service: ") + hipGetErrorString(e));
         release_service(s);
@@ -718,6 +759,16 @@ int nffacl_service_create(int hip_device, uint32_t mailboxes, uint32_t idle_us, 
             return NFFACL_ERR_INVALID_ARG;
         }
         if (set && v == 0) s->args.lds_dwords = 0;
+        // Callers sleep through most of the PCIe round trip instead of
+        // spinning it: under a CPU quota a spinning caller burns the quota the
+        // other callers need (throughput = quota / CPU time per call)
+        if (!env_knob("NFFACL_TUNE_SVC_SLEEP_NS", -1, 100000, v, set, err)) {
+            set_last_error(err);
+            release_service(s);
+            return NFFACL_ERR_INVALID_ARG;
+        }
+        if (set) s->sleep_ns = static_cast<int32_t>(v);
+        s->cpus = cpu_budget();
     }
     if (s->args.lds_dwords &&
         hipFuncSetAttribute(reinterpret_cast<const void *>(dev::k_service), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -776,6 +827,22 @@ int nffacl_service_classify(nffacl_service *s, const nffacl_rules *rules, const 
     std::atomic_thread_fence(std::memory_order_seq_cst);  // request visible before `running` is read
     if (!s->running.load(std::memory_order_seq_cst)) kick(s);
     const uint64_t *r = s->h_resp + size_t(mb) * kSvcRespStride;
+    // sleep first?  (adaptive: only with more callers than half the CPUs)
+    const bool adaptive = s->sleep_ns < 0 && s->next_mb.load(std::memory_order_relaxed) * 2 > s->cpus;
+    // adaptive nap: 1.5 us short of the mailbox's recent minimum latency
+    const uint32_t nap = adaptive ? (m.lat_min > 1500u ? std::min(m.lat_min - 1500u, 50000u) : 0u)
+                                  : s->sleep_ns > 0 ? static_cast<uint32_t>(s->sleep_ns) : 0u;
+    Clock::time_point posted{};
+    if (adaptive) posted = Clock::now();
+    if (nap) {
+        thread_local bool slack = false;
+        if (!slack) {  // hrtimer wake-ups at the requested time (default slack: 50 us)
+            (void)prctl(PR_SET_TIMERSLACK, 1UL, 0, 0, 0);
+            slack = true;
+        }
+        const timespec ts{0, static_cast<long>(nap)};
+        (void)nanosleep(&ts, nullptr);
+    }
     uint64_t v = 0;
     uint32_t spins = 0;
     Clock::time_point t0{};
@@ -796,6 +863,16 @@ int nffacl_service_classify(nffacl_service *s, const nffacl_rules *rules, const 
                 break;
             }
         }
+    }
+    if (adaptive && st == NFFACL_OK) {
+        // The minimum is robust to the long outliers of a preempted caller;
+        // it creeps up 16 ns per call so that it follows a slower consumer.
+        // A call whose answer was already there at wake-up measures nap +
+        // wake-up time, so an overlong nap shrinks by the 1.5 us margin less
+        // the wake-up time per minimum.
+        const auto lat = std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - posted).count();
+        const uint32_t l = static_cast<uint32_t>(std::max<int64_t>(1, std::min<int64_t>(lat, 1000000)));
+        m.lat_min = m.lat_min == 0u ? l : std::min(m.lat_min + 16u, l);
     }
     m.lock.store(0, std::memory_order_release);
     if (st == NFFACL_ERR_HIP) return failed(st);

@@ -35,9 +35,9 @@ constexpr uint32_t kSvcPktChunks = 7;
 constexpr uint32_t kSvcSlot = 80;          // packet bytes handed to the GPU (as nffgo.hpp kSlot)
 constexpr uint32_t kSvcBoxBytes = kSvcChunks * 16;
 constexpr uint32_t kSvcRespStride = 8;     // u64 words per response (64 B: one line per mailbox)
-constexpr uint32_t kSvcStatWords = 8;
+constexpr uint32_t kSvcStatWords = 8;      // per-wave counters: polls, poll ticks, groups, group ticks, requests
 constexpr uint32_t kSvcLdsDwords = 16384;  // INDEXED tables up to 64 KiB are walked from LDS
-constexpr uint32_t kSvcMbPerWave = 8;      // mailboxes per consumer wave (a multiple of 8: 1 KiB per poll load)      // per-wave counters: polls, poll ticks, groups, group ticks, requests
+constexpr uint32_t kSvcMbPerWave = 8;      // mailboxes per consumer wave (a multiple of 8: 1 KiB per poll load)
 
 // ---- table descriptor (device memory, after each table's blob) ---------------
 //

@@ -237,7 +237,7 @@ inline nffacl_service *service(int dev) {
     static Holder holders[16];
     if (dev < 0 || dev >= 16) throw std::runtime_error("ACL device out of range");
     Holder &h = holders[dev];
-    std::call_once(h.once, [&] { h.st = nffacl_service_create(dev, 128, 2000, &h.svc); });
+    std::call_once(h.once, [&] { h.st = nffacl_service_create(dev, 0, 2000, &h.svc); });
     if (h.st != NFFACL_OK)
         throw std::runtime_error(std::string("nffacl_service_create: ") + nffacl_strerror(h.st) + " " +
                                  nffacl_last_error());

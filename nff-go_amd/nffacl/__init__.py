@@ -375,19 +375,28 @@ class Engine:
         if st != OK:
             _raise(st, "nffacl_classify_frames_device")
 
-    def classify_host(self, slots: np.ndarray, stride: int, n: int | None = None, flags: int = 0):
-        """Host slots (uint8, n*stride bytes) -> (port uint32[n], permit uint8[n])."""
+    def classify_host(self, slots: np.ndarray, stride: int, n: int | None = None, flags: int = 0,
+                      out: np.ndarray | None = None, permit: bool = True):
+        """Host slots (uint8, n*stride bytes) -> (port uint32[n], permit uint8[n] or None).
+        `out`: the port array to fill (e.g. pinned memory, which the kernel
+        writes directly); permit=False skips the per-packet permit bytes."""
         slots = np.ascontiguousarray(slots, np.uint8)
         if n is None:
             n = slots.size // stride
         if slots.size < n * stride:
             raise ValueError("slot buffer too small")
-        port = np.zeros(n, np.uint32)
-        permit = np.zeros(n, np.uint8)
-        st = _classify_host(self._h, slots.ctypes.data, stride, n, port.ctypes.data, permit.ctypes.data, flags)
+        if out is None:
+            port = np.zeros(n, np.uint32)
+        else:
+            if out.dtype != np.uint32 or out.size < n or not out.flags.c_contiguous:
+                raise ValueError("out: contiguous uint32[n] expected")
+            port = out
+        perm = np.zeros(n, np.uint8) if permit else None
+        st = _classify_host(self._h, slots.ctypes.data, stride, n, port.ctypes.data,
+                            perm.ctypes.data if permit else None, flags)
         if st != OK:
             _raise(st, "nffacl_classify_host")
-        return port, permit
+        return port, perm
 
     # Batch forms of the reference's per-packet API (acl.go:495-506)
     def L3ACLPort(self, slots: np.ndarray, stride: int):
@@ -494,7 +503,7 @@ class Service:
     SetSeparator / SetSplitter function (acl.go:495-506, flow.go:128), with
     the rule set passed per call.  ctypes drops the GIL during the call."""
 
-    def __init__(self, device: int = 0, mailboxes: int = 128, idle_us: int = 2000):
+    def __init__(self, device: int = 0, mailboxes: int = 0, idle_us: int = 2000):
         out = ctypes.c_void_p()
         st = _service_create(device, mailboxes, idle_us, ctypes.byref(out))
         if st != OK:

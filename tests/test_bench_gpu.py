@@ -47,7 +47,10 @@ def test_bench_n1_with_extra_configs(gpu_available):
         assert "@1k rules" not in rec["metric"], rec["metric"]  # labelled per config
         assert rec["bit_exact_sample"] and rec["cpu_baseline"]["bit_exact_vs_gpu"], c
         assert rec["roofline"]["frac"] > 0 and rec["value"] > 0
-    assert d["configs"]["c3"]["config"]["algorithmic_bytes_per_packet"] == 76
+    # 8 B descriptor + 64 B line + 4 B verdict, plus the second
+    # 64 B line of the ~0.3 % of frames whose IP options (IHL >= 12) reach
+    # past the first (76.185 B for C3's IMIX mix)
+    assert 76.0 < d["configs"]["c3"]["config"]["algorithmic_bytes_per_packet"] < 76.5
     assert d["configs"]["c5"]["config"]["rules_ip4"] + d["configs"]["c5"]["config"]["rules_ip6"] == 100000
 
 

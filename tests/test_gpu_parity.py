@@ -349,6 +349,34 @@ def test_classify_host_pinned_zero_copy(torch_cuda, stride):
         np.testing.assert_array_equal(out.numpy().view(np.uint32), want)
 
 
+@pytest.mark.parametrize("dma,bufs,chunk", [(0, 2, 12), (0, 4, 14), (1, 2, 12), (1, 3, 13), (1, 4, 20)])
+def test_classify_host_pipeline_variants(torch_cuda, monkeypatch, dma, bufs, chunk):
+    """nffacl_classify_host's forms (NFFACL_TUNE_HOST_*): zero-copy or DMA'd
+    pinned input, pageable input (staged), 2-4 buffers in flight, chunks of
+    2^12-2^20 packets (many chunks: the buffers wrap), verdicts into pinned or
+    pageable memory — all bit-exact vs the oracle."""
+    torch = torch_cuda
+    monkeypatch.setenv("NFFACL_TUNE_HOST_DMA", str(dma))
+    monkeypatch.setenv("NFFACL_TUNE_HOST_BUFS", str(bufs))
+    monkeypatch.setenv("NFFACL_TUNE_HOST_CHUNK", str(chunk))
+    g = synth.gen_rules(synth.SPECS["c2"], synth.RULE_SEEDS["c2"])
+    rules, (a4, a6) = _rules_and_arrays(g.text)
+    n = 11 * (1 << chunk) // 2 + 29 if chunk < 20 else (1 << 20) + 29
+    slots = synth.gen_slots(g, n, 7 + chunk, stride=80)
+    want = oracle.classify_slots(slots, 80, n, a4, a6, threads=THREADS)
+    pinned = torch.from_numpy(slots).pin_memory()
+    out = torch.zeros(n, dtype=torch.int32).pin_memory().numpy().view(np.uint32)
+    with nffacl.Engine(rules) as eng:
+        port, permit = eng.classify_host(slots, 80, n)  # pageable in and out
+        np.testing.assert_array_equal(port, want)
+        np.testing.assert_array_equal(permit, (want != 0).astype(np.uint8))
+        port, _ = eng.classify_host(pinned.numpy(), 80, n, out=out, permit=False)  # pinned in and out
+        np.testing.assert_array_equal(out, want)
+        port, permit = eng.classify_host(pinned.numpy(), 80, n)  # pinned in, pageable out
+        np.testing.assert_array_equal(port, want)
+        np.testing.assert_array_equal(permit, (want != 0).astype(np.uint8))
+
+
 def test_stability_separate_split_proportions(torch_cuda, golden):
     """testSingleWorkingFF.go: separate -> exactly the dst-port-111 third is
     permitted; split -> outputs 1/2 by dst port (test-*.conf)."""

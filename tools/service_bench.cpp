@@ -7,6 +7,8 @@
 //
 //   service_bench RULES SLOTS EXPECT THREADS SECONDS
 // prints one JSON line.
+#include <sys/resource.h>
+
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -76,12 +78,24 @@ int main(int argc, char **argv) {
             total += done;
             bad += wrong;
         });
+    auto cpu_s = [] {
+        rusage ru{};
+        getrusage(RUSAGE_SELF, &ru);
+        return ru.ru_utime.tv_sec + ru.ru_stime.tv_sec + 1e-6 * (ru.ru_utime.tv_usec + ru.ru_stime.tv_usec);
+    };
+    const double c0 = cpu_s();
     const auto t0 = Clock::now();
     go = true;
     std::this_thread::sleep_for(std::chrono::duration<double>(seconds));
     halt = true;
     for (auto &x : th) x.join();
     const double dt = std::chrono::duration<double>(Clock::now() - t0).count();
+    const double cpu = cpu_s() - c0;  // process CPU seconds over the run (all threads)
+    std::string quota = "?";  // cgroup v2 CPU bandwidth limit ("max" or "QUOTA PERIOD")
+    {
+        std::ifstream q("/sys/fs/cgroup/cpu.max");
+        if (q) std::getline(q, quota);
+    }
     std::vector<float> all;
     for (auto &v : lat) all.insert(all.end(), v.begin(), v.end());
     std::sort(all.begin(), all.end());
@@ -91,10 +105,11 @@ int main(int argc, char **argv) {
     std::printf("{\"threads\": %u, \"calls\": %llu, \"mpps\": %.3f, \"lat_us_p50\": %.2f, \"lat_us_p90\": %.2f, "
                 "\"lat_us_p99\": %.2f, \"lat_us_p999\": %.1f, \"wrong\": %llu, \"launches\": %llu, "
                 "\"timeouts\": %llu, \"polls\": %llu, \"poll_ns\": %.0f, \"groups\": %llu, \"group_ns\": %.0f, "
-                "\"answered\": %llu}\n",
+                "\"answered\": %llu, \"cpu_us_per_call\": %.2f, \"cpus_busy\": %.2f, \"cpu_max\": \"%s\"}\n",
                 threads, (unsigned long long)total.load(), total.load() / dt / 1e6, pct(0.5), pct(0.9), pct(0.99),
                 pct(0.999), (unsigned long long)bad.load(), (unsigned long long)st.launches,
                 (unsigned long long)st.timeouts, (unsigned long long)st.polls, st.poll_ns,
-                (unsigned long long)st.groups, st.group_ns, (unsigned long long)st.answered);
+                (unsigned long long)st.groups, st.group_ns, (unsigned long long)st.answered,
+                total.load() ? cpu / double(total.load()) * 1e6 : 0.0, cpu / dt, quota.c_str());
     return bad.load() ? 1 : 0;
 }
