@@ -372,8 +372,8 @@ NFFACL_API void nffacl_batcher_destroy(nffacl_batcher *b);
  * a call writes its packet's first 80 bytes into the calling thread's
  * mailbox and waits until the kernel has written the verdict back — no
  * kernel launch, no driver call per packet.  A caller spins; once the callers
- * outnumber half the CPUs the process may use (affinity, cgroup quota) it
- * first sleeps through most of the round trip, adapted per mailbox, so that
+ * outnumber the CPUs the process may use (affinity, cgroup quota) it first
+ * sleeps through most of the round trip (a nap adapted per mailbox), so that
  * waiting callers leave the CPUs to posting ones.  The kernel exits after
  * `idle_us` without calls (and every 100 ms) and is re-armed by the next
  * call.  Thread-safe; one service per GPU serves every thread.
@@ -395,7 +395,7 @@ typedef struct nffacl_service_stats {
     uint64_t answered;  /* requests answered by the consumer */
 } nffacl_service_stats;
 
-/* mailboxes: a multiple of 64 (one consumer wave per 8; 0 = 256), one per
+/* mailboxes: a multiple of 64 (one consumer wave per 8; 0 = 128), one per
  * calling thread (threads beyond that share mailboxes under a lock);
  * idle_us: consumer lifetime without calls (0 = 2000). */
 NFFACL_API int nffacl_service_create(int hip_device, uint32_t mailboxes, uint32_t idle_us, nffacl_service **out);

@@ -444,7 +444,7 @@ namespace {
 struct alignas(64) MailboxState {
     std::atomic<uint32_t> lock{0};  // owner (threads beyond the mailbox count share)
     uint32_t seq = 0;               // last tag posted
-    uint32_t lat_min = 0;           // under lock: recent minimum call latency, ns (0: none yet)
+    uint32_t nap = 0;               // under lock: this mailbox's adaptive nap after posting, ns
 };
 
 // CPUs this process may keep busy: its affinity mask, capped by a cgroup v2
@@ -472,8 +472,8 @@ struct nffacl_service {
     uint32_t n_mb = 0;
     uint64_t timeout_us = 1000000;
     // After posting, a caller sleeps through most of the round trip instead
-    // of spinning it once the callers outnumber half the CPUs this process
-    // may use (sleep_ns < 0: adaptive, per mailbox; 0: never; > 0: fixed;
+    // of spinning it once the callers outnumber the CPUs this process may use
+    // (sleep_ns < 0: adaptive, per mailbox; 0: never; > 0: fixed;
     // NFFACL_TUNE_SVC_SLEEP_NS).  Under a CPU quota every spinning caller
     // burns the quota the others need: throughput = quota / CPU per call.
     int32_t sleep_ns = -1;
@@ -552,12 +552,12 @@ void armer_main(nffacl_service *s) {
         s->running.store(true, std::memory_order_seq_cst);
         __atomic_store_n(&s->h_ctrl[1], 0u, __ATOMIC_SEQ_CST);
         s->args.epoch = table_epoch();  // every table of this generation or older is in HBM
+        s->launches.fetch_add(1, std::memory_order_relaxed);  // (before the launch: its calls may return first)
         hipLaunchKernelGGL(dev::k_service, dim3(s->n_mb / kSvcMbPerWave), dim3(64), size_t(s->args.lds_dwords) * 4,
                            s->stream, s->args);
         hipError_t e = hipGetLastError();
         if (e == hipSuccess) e = hipEventRecord(s->done, s->stream);
         if (e == hipSuccess) {
-            s->launches.fetch_add(1, std::memory_order_relaxed);
             // Sleep-poll for the kernel's exit: a blocking hipEventSynchronize
             // still kept one CPU busy for the kernel's whole life (round 3 sweep:
             // 2.0 CPUs at one caller), and under a CPU quota that CPU is the
@@ -677,7 +677,7 @@ int nffacl_rules_prepare(const nffacl_rules *rules, int hip_device) {
 int nffacl_service_create(int hip_device, uint32_t mailboxes, uint32_t idle_us, nffacl_service **out) {
     if (!out) return NFFACL_ERR_INVALID_ARG;
     *out = nullptr;
-    if (mailboxes == 0) {  // default: 256 (NFFACL_TUNE_SVC_MAILBOXES)
+    if (mailboxes == 0) {  // default: 128 (NFFACL_TUNE_SVC_MAILBOXES)
         long v = 0;
         bool set = false;
         std::string err;
@@ -685,7 +685,7 @@ int nffacl_service_create(int hip_device, uint32_t mailboxes, uint32_t idle_us, 
             set_last_error(err);
             return NFFACL_ERR_INVALID_ARG;
         }
-        mailboxes = set ? static_cast<uint32_t>(v) : 256u;
+        mailboxes = set ? static_cast<uint32_t>(v) : 128u;
     }
     if (mailboxes % 64 != 0 || mailboxes > 4096 || idle_us > 10000000u) return NFFACL_ERR_INVALID_ARG;
     if (idle_us == 0) idle_us = 2000;
@@ -827,13 +827,10 @@ int nffacl_service_classify(nffacl_service *s, const nffacl_rules *rules, const 
     std::atomic_thread_fence(std::memory_order_seq_cst);  // request visible before `running` is read
     if (!s->running.load(std::memory_order_seq_cst)) kick(s);
     const uint64_t *r = s->h_resp + size_t(mb) * kSvcRespStride;
-    // sleep first?  (adaptive: only with more callers than half the CPUs)
-    const bool adaptive = s->sleep_ns < 0 && s->next_mb.load(std::memory_order_relaxed) * 2 > s->cpus;
-    // adaptive nap: 1.5 us short of the mailbox's recent minimum latency
-    const uint32_t nap = adaptive ? (m.lat_min > 1500u ? std::min(m.lat_min - 1500u, 50000u) : 0u)
-                                  : s->sleep_ns > 0 ? static_cast<uint32_t>(s->sleep_ns) : 0u;
-    Clock::time_point posted{};
-    if (adaptive) posted = Clock::now();
+    // sleep first?  (adaptive: only with more callers than CPUs)
+    const bool adaptive = s->sleep_ns < 0 && s->next_mb.load(std::memory_order_relaxed) > s->cpus;
+    const uint32_t nap = adaptive ? m.nap : s->sleep_ns > 0 ? static_cast<uint32_t>(s->sleep_ns) : 0u;
+    Clock::time_point woke{};
     if (nap) {
         thread_local bool slack = false;
         if (!slack) {  // hrtimer wake-ups at the requested time (default slack: 50 us)
@@ -843,6 +840,8 @@ int nffacl_service_classify(nffacl_service *s, const nffacl_rules *rules, const 
         const timespec ts{0, static_cast<long>(nap)};
         (void)nanosleep(&ts, nullptr);
     }
+    if (adaptive) woke = Clock::now();
+    bool spun = false;
     uint64_t v = 0;
     uint32_t spins = 0;
     Clock::time_point t0{};
@@ -850,6 +849,7 @@ int nffacl_service_classify(nffacl_service *s, const nffacl_rules *rules, const 
     while (true) {
         v = __atomic_load_n(r, __ATOMIC_ACQUIRE);
         if (static_cast<uint32_t>(v >> 32) == tag) break;
+        spun = true;
         _mm_pause();
         if ((++spins & 1023u) == 0) {
             const Clock::time_point now = Clock::now();
@@ -865,14 +865,18 @@ int nffacl_service_classify(nffacl_service *s, const nffacl_rules *rules, const 
         }
     }
     if (adaptive && st == NFFACL_OK) {
-        // The minimum is robust to the long outliers of a preempted caller;
-        // it creeps up 16 ns per call so that it follows a slower consumer.
-        // A call whose answer was already there at wake-up measures nap +
-        // wake-up time, so an overlong nap shrinks by the 1.5 us margin less
-        // the wake-up time per minimum.
-        const auto lat = std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - posted).count();
-        const uint32_t l = static_cast<uint32_t>(std::max<int64_t>(1, std::min<int64_t>(lat, 1000000)));
-        m.lat_min = m.lat_min == 0u ? l : std::min(m.lat_min + 16u, l);
+        // Aim the nap just short of the answer: an answer already there at
+        // wake-up (overslept by an unknown amount) cuts it by an eighth; a
+        // spin after waking lengthens it by half the spin beyond 300 ns,
+        // capped at 1 us per call (a caller preempted while spinning must not
+        // drag it up).
+        if (!spun) {
+            m.nap -= std::max(m.nap / 8u, std::min(m.nap, 100u));
+        } else {
+            const int64_t spin = std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - woke).count();
+            if (spin > 300) m.nap = std::min(m.nap + static_cast<uint32_t>(std::min<int64_t>((spin - 300) / 2, 1000)),
+                                             20000u);
+        }
     }
     m.lock.store(0, std::memory_order_release);
     if (st == NFFACL_ERR_HIP) return failed(st);
