@@ -196,8 +196,11 @@ k_indexed_slots(const uint8_t *__restrict__ slots, uint32_t stride, uint64_t n, 
     }
 }
 
+#ifndef NFFACL_FRAMES_WPE
+#define NFFACL_FRAMES_WPE 1
+#endif
 template <int NS, int TM>
-__global__ void __launch_bounds__(1024)
+__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(NFFACL_FRAMES_WPE)))
 k_indexed_frames(const uint8_t *__restrict__ frames, const uint64_t *__restrict__ desc, uint64_t n,
                  IndexedArgs a, uint32_t *__restrict__ port_out, uint64_t *__restrict__ permit_out) {
     if (TM == kTabLds || TM == kTabSplit || TM == kTabFlatLds || TM == kTabFlatLds4 || TM == kTabFlatLds4U) stage_table(a);

@@ -865,16 +865,16 @@ int nffacl_service_classify(nffacl_service *s, const nffacl_rules *rules, const 
         }
     }
     if (adaptive && st == NFFACL_OK) {
-        // Aim the nap just short of the answer: an answer already there at
-        // wake-up (overslept by an unknown amount) cuts it by an eighth; a
-        // spin after waking lengthens it by half the spin beyond 300 ns,
-        // capped at 1 us per call (a caller preempted while spinning must not
-        // drag it up).
+        // Aim the nap short of the answer (an oversleep costs the whole
+        // wake-up time, a short spin only CPU): an answer already there at
+        // wake-up cuts it by a quarter; a spin after waking lengthens it by a
+        // quarter of the spin beyond 300 ns, at most 500 ns per call (a caller
+        // preempted while spinning must not drag it up).
         if (!spun) {
-            m.nap -= std::max(m.nap / 8u, std::min(m.nap, 100u));
+            m.nap -= std::max(m.nap / 4u, std::min(m.nap, 100u));
         } else {
             const int64_t spin = std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - woke).count();
-            if (spin > 300) m.nap = std::min(m.nap + static_cast<uint32_t>(std::min<int64_t>((spin - 300) / 2, 1000)),
+            if (spin > 300) m.nap = std::min(m.nap + static_cast<uint32_t>(std::min<int64_t>((spin - 300) / 4, 500)),
                                              20000u);
         }
     }

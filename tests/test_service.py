@@ -151,6 +151,41 @@ def test_threads_two_rule_sets(svc):
     assert not errors, errors[:10]
 
 
+@pytest.mark.parametrize("sleep_ns", ["-1", "0", "1500"])
+def test_callers_nap_or_spin(torch_cuda, monkeypatch, sleep_ns):
+    """More callers than mailboxes' waves and than a small CPU budget: callers
+    that nap after posting (adaptive, or fixed) or spin — every answer the
+    oracle's, no timeouts, the consumer never left its table."""
+    monkeypatch.setenv("NFFACL_TUNE_SVC_SLEEP_NS", sleep_ns)
+    g = synth.gen_rules(synth.SPECS["c2"], synth.RULE_SEEDS["c2"])
+    rules = nffacl.L3Rules.parse_text(g.text)
+    n = 3000
+    slots = synth.gen_slots(g, n, 5, stride=80).reshape(n, 80)
+    frames = [bytes(s) for s in slots]
+    want = _oracle_ports(g.text, frames)
+    errors = []
+    threads = 24
+
+    with nffacl.Service(0, mailboxes=64) as s:
+        def worker(t):
+            try:
+                for i in range(t, n, threads):
+                    got = s.classify(rules, frames[i])
+                    if got != want[i]:
+                        errors.append((t, i, got, int(want[i])))
+            except Exception as e:  # surfaced below
+                errors.append(e)
+
+        ths = [threading.Thread(target=worker, args=(t,)) for t in range(threads)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        st = s.stats()
+    assert not errors, errors[:10]
+    assert st["timeouts"] == 0 and st["table_oob"] == 0 and st["requests"] == n, st
+
+
 def test_idle_exit_and_rearm(torch_cuda, golden):
     """The consumer leaves after idle_us without calls and the next call
     re-arms it; destroying a service whose consumer is resident returns
