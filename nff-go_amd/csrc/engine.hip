@@ -196,11 +196,12 @@ k_indexed_slots(const uint8_t *__restrict__ slots, uint32_t stride, uint64_t n, 
     }
 }
 
-#ifndef NFFACL_FRAMES_WPE
-#define NFFACL_FRAMES_WPE 1
-#endif
+// (Round 3: compiled for 6 waves per SIMD — 80 VGPRs, a few spills — with
+// two 768-thread workgroups per CU over 56-64 KB directories: C3 0.464 vs
+// 0.463 ms, the extra waves bought back only what the smaller directories
+// cost; profiles/r3_ab/c3_occupancy/)
 template <int NS, int TM>
-__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(NFFACL_FRAMES_WPE)))
+__global__ void __launch_bounds__(1024)
 k_indexed_frames(const uint8_t *__restrict__ frames, const uint64_t *__restrict__ desc, uint64_t n,
                  IndexedArgs a, uint32_t *__restrict__ port_out, uint64_t *__restrict__ permit_out) {
     if (TM == kTabLds || TM == kTabSplit || TM == kTabFlatLds || TM == kTabFlatLds4 || TM == kTabFlatLds4U) stage_table(a);
