@@ -446,6 +446,18 @@ using SplitTab = DirTab<true>;
 
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 
+// Per-lane choice between two wave-uniform family parameters (IPv4 / IPv6
+// slot arguments).  Both pass through readfirstlane so that they stay in
+// SGPRs and the choice is one v_cndmask: written as a plain select of two
+// struct fields, the compiler turned it into a select of their ADDRESSES
+// and a per-lane global load from the kernel-argument segment — a dependent
+// vector-memory round trip per field per batch (C2: 2 per batch, the flat
+// C3/C5 kernels: ~25), queued behind the packet stream's loads.
+__device__ __forceinline__ uint32_t fam_sel(bool v6, uint32_t x4, uint32_t x6) {
+    const uint32_t u4 = __builtin_amdgcn_readfirstlane(x4), u6 = __builtin_amdgcn_readfirstlane(x6);
+    return v6 ? u6 : u4;
+}
+
 // Mismatch bits of an entry's first 8 dwords (A = words 0..3, B = 4..7):
 // address words, protocol (exact flag) and ports — acl.go:526-539 / 546-557
 // with IPv6 restricted to the top 32 bits of each address.
@@ -489,12 +501,12 @@ __device__ __forceinline__ uint32_t classify_indexed(const T &tab, const Indexed
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
         const SlotArgs &s4 = a.f4.slot[s], &s6 = a.f6.slot[s];
-        const uint32_t shift = v6 ? s6.shift : s4.shift;
-        const uint32_t dir = v6 ? s6.off_dir : s4.off_dir;
-        const uint32_t base = v6 ? s6.off_ent : s4.off_ent;
+        const uint32_t shift = fam_sel(v6, s4.shift, s6.shift);
+        const uint32_t dir = fam_sel(v6, s4.off_dir, s6.off_dir);
+        const uint32_t base = fam_sel(v6, s4.off_ent, s6.off_ent);
         const uint32_t t = key[s] >> shift;  // < n_buckets for any key: both reads in range
         uint32_t lo, hi;
-        tab.bounds(dir, v6 ? s6.off_dir16 : s4.off_dir16, t, lo, hi, a.dir8 != 0u);
+        tab.bounds(dir, fam_sel(v6, s4.off_dir16, s6.off_dir16), t, lo, hi, a.dir8 != 0u);
         c[s] = base + times_ew(lo, v6);
         e[s] = mine ? base + times_ew(hi, v6) : c[s];
     }
@@ -567,10 +579,24 @@ __device__ __forceinline__ uint32_t classify_indexed(const T &tab, const Indexed
     return best != kNone ? out : 0u;
 }
 
+// The leading stage_dwords of the table into LDS, once per workgroup.  Each
+// thread issues up to U 16-byte loads before its first LDS write (a plain
+// copy loop waited out one HBM round trip per 16 KiB: 4-7 in a row at the
+// start of every C2/C3/C5 launch).
 __device__ __forceinline__ void stage_table(const IndexedArgs &a) {
     const u32x4 *src = reinterpret_cast<const u32x4 *>(a.tab);
     u32x4 *dst = reinterpret_cast<u32x4 *>(lds_tab);
-    for (uint32_t i = threadIdx.x; i < a.stage_dwords / 4; i += blockDim.x) dst[i] = src[i];
+    const uint32_t nv = a.stage_dwords / 4, step = blockDim.x;
+    constexpr uint32_t U = 8;
+    for (uint32_t i0 = threadIdx.x; i0 < nv; i0 += U * step) {
+        u32x4 v[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u)
+            if (i0 + u * step < nv) v[u] = src[i0 + u * step];
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u)
+            if (i0 + u * step < nv) dst[i0 + u * step] = v[u];
+    }
     __syncthreads();
 }
 
@@ -719,9 +745,9 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
         for (int s = 0; s < NS; ++s) {
             const SlotArgs &s4 = a.f4.slot[s], &s6 = a.f6.slot[s];
             const uint32_t key = s == kFDst ? kd : s == kFSrc ? ks : s == kFDport ? dport : s == kFSport ? sport : 0u;
-            const uint32_t t = key >> (v6 ? s6.shift : s4.shift);
+            const uint32_t t = key >> (fam_sel(v6, s4.shift, s6.shift));
             uint32_t hi;
-            DirTab<DIRS_IN_LDS>{a.tab, a.tab_dwords}.bounds(v6 ? s6.off_dir : s4.off_dir, v6 ? s6.off_dir16 : s4.off_dir16, t, st[s], hi,
+            DirTab<DIRS_IN_LDS>{a.tab, a.tab_dwords}.bounds(fam_sel(v6, s4.off_dir, s6.off_dir), fam_sel(v6, s4.off_dir16, s6.off_dir16), t, st[s], hi,
                                    a.dir8 != 0u);
             ln[s] = mine ? hi - st[s] : 0u;
         }
@@ -729,19 +755,19 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
         const SlotArgs &s4 = a.f4.slot[s], &s6 = a.f6.slot[s];
-        const uint32_t shift = v6 ? s6.shift : s4.shift;
-        const uint32_t dir = v6 ? s6.off_dir : s4.off_dir;
-        const uint32_t t = ((pick(v6 ? s6.f1 : s4.f1) >> shift) << (v6 ? s6.bits2 : s4.bits2)) |
-                           (pick(v6 ? s6.f2 : s4.f2) >> (v6 ? s6.shift2 : s4.shift2));
+        const uint32_t shift = fam_sel(v6, s4.shift, s6.shift);
+        const uint32_t dir = fam_sel(v6, s4.off_dir, s6.off_dir);
+        const uint32_t t = ((pick(fam_sel(v6, s4.f1, s6.f1)) >> shift) << (fam_sel(v6, s4.bits2, s6.bits2))) |
+                           (pick(fam_sel(v6, s4.f2, s6.f2)) >> (fam_sel(v6, s4.shift2, s6.shift2)));
         if (LDS_DIRS) {
             uint32_t hi;
-            DirTab<DIRS_IN_LDS>{a.tab, a.tab_dwords}.bounds(dir, v6 ? s6.off_dir16 : s4.off_dir16, t, st[s], hi, a.dir8 != 0u);
+            DirTab<DIRS_IN_LDS>{a.tab, a.tab_dwords}.bounds(dir, fam_sel(v6, s4.off_dir16, s6.off_dir16), t, st[s], hi, a.dir8 != 0u);
             ln[s] = mine ? hi - st[s] : 0u;
         } else {
             // generalized slots: a family's unused slots (f1 == kFZero) read nothing
             st[s] = 0u;
             ln[s] = 0u;
-            if (mine && (v6 ? s6.f1 : s4.f1) != kFZero) {
+            if (mine && (fam_sel(v6, s4.f1, s6.f1)) != kFZero) {
                 st[s] = g1(dir + t);
                 ln[s] = g1(dir + t + 1) - st[s];
             }
@@ -907,7 +933,7 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
     const bool rd = hit && out == kHybOutEscape;
     if (ballot(rd)) {
         const uint32_t r = static_cast<uint32_t>(best >> 32);
-        if (rd) out = g1((v6 ? a.f6.off_cold : a.f4.off_cold) + r);
+        if (rd) out = g1(fam_sel(v6, a.f4.off_cold, a.f6.off_cold) + r);
     }
     return out;
 }

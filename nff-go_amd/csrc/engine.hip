@@ -274,9 +274,9 @@ k_indexed_frames(const uint8_t *__restrict__ frames, const uint64_t *__restrict_
         uint64_t ds_next = desc_at(base);
         for (; base < n; base += S) {
             const uint64_t ds = ds_next;
-            ds_next = desc_at(base + S);
             u32x4 v[4];
             load_frames_rs(frames, ds, lane, v);
+            ds_next = desc_at(base + S);  // issued after this batch's frame loads
             run_batch(base, ds, v);
         }
     }
