@@ -15,6 +15,10 @@
 namespace nffacl {
 namespace dev {
 
+// 16 zero bytes in global memory: the load address of a lane with nothing
+// to read, so that loads need no per-lane branch.
+static __device__ u32x4 g_zero16 = {0u, 0u, 0u, 0u};
+
 __device__ __forceinline__ uint32_t funnel16(uint32_t hi, uint32_t lo) {
     // ({hi,lo} >> 16)[31:0] : wire bytes 4k+2 .. 4k+5 as a LE dword
     return __builtin_amdgcn_alignbit(hi, lo, 16);
@@ -266,19 +270,26 @@ __device__ __forceinline__ void transpose_batch(const u32x4 (&v)[4], uint32_t la
 // for lanes past the batch end).  A chunk is read only if it starts inside
 // its frame: a 16-byte aligned load that starts at a frame byte stays in
 // that byte's page, so nothing past the last frame of the buffer is touched.
+// Every lane issues its four loads without a branch: a chunk that starts
+// past its frame's end is read from a 16-byte block of zeros instead
+// (predicated loads left the compiler's wait counting conservative: an
+// s_waitcnt vmcnt(0) that also waited for loads issued after them, such as
+// the next batch's descriptors).
 __device__ __forceinline__ void load_frames_rs(const uint8_t *__restrict__ frames, uint64_t ds, uint32_t lane,
                                                u32x4 (&v)[4]) {
     const uint32_t lo = static_cast<uint32_t>(ds), hi = static_cast<uint32_t>(ds >> 32);
     const uint32_t chunk = 16u * (lane >> 4);
+    const u32x4 *p[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const int src = static_cast<int>((16u * j + (lane & 15u)) << 2);
         const uint32_t l = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(lo)));
         const uint32_t h = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(hi)));
         const uint64_t o = (uint64_t(h) << 32 | l) >> 16;
-        v[j] = u32x4{0, 0, 0, 0};
-        if (chunk < (l & 0xFFFFu)) v[j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(frames + o) + (lane >> 4));
+        p[j] = chunk < (l & 0xFFFFu) ? reinterpret_cast<const u32x4 *>(frames + o) + (lane >> 4) : &g_zero16;
     }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = __builtin_nontemporal_load(p[j]);
 }
 
 // One lane's frame: the first 64 bytes, chunks past `len` not read (see
@@ -664,6 +675,12 @@ struct FlatScratch {
     uint64_t best[64];       // per packet (lane): lowest passing rule index << 32 | output code
 };
 
+// Complete the load that produced `x` here, inside the (rare) branch that
+// issued it.  Left pending across the join, it made the compiler wait for
+// every outstanding vector-memory operation at the value's next use — the
+// batch's own verdict stores included, one HBM write round trip per batch.
+__device__ __forceinline__ void settle(uint32_t &x) { asm volatile("" : "+v"(x)); }
+
 // Order this wave's LDS writes before its following LDS reads of other lanes'
 // words (one wave: program order on the LDS queue; this keeps the compiler
 // from reordering across it).
@@ -934,6 +951,7 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
     if (ballot(rd)) {
         const uint32_t r = static_cast<uint32_t>(best >> 32);
         if (rd) out = g1(fam_sel(v6, a.f4.off_cold, a.f6.off_cold) + r);
+        settle(out);
     }
     return out;
 }

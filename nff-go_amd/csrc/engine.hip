@@ -210,7 +210,9 @@ k_indexed_frames(const uint8_t *__restrict__ frames, const uint64_t *__restrict_
     const uint64_t S = uint64_t(gridDim.x) * wpb * 64;  // grid stride in packets
     uint64_t base = (uint64_t(blockIdx.x) * wpb + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) * 64;
     if (base >= n) return;
-    auto desc_at = [&](uint64_t b) -> uint64_t { return b + lane < n ? desc[b + lane] : 0; };
+    auto desc_at = [&](uint64_t b) -> uint64_t {  // (branch-free, see load_frames_rs)
+        return *(b + lane < n ? desc + b + lane : reinterpret_cast<const uint64_t *>(&g_zero16));
+    };
     // classify the batch at b whose descriptor is ds and first 64 bytes d
     auto classify_batch = [&](uint64_t b, uint64_t ds, uint32_t(&d)[16]) {
         const bool live = b + lane < n;
