@@ -130,15 +130,15 @@ __device__ __forceinline__ void parse_fields(uint32_t (&d)[16], bool live, Field
 // bytes from `base` (4-byte aligned); bytes at or past `lim` read as 0.
 __device__ __forceinline__ void far_dwords(const uint8_t *base, uint32_t lim, uint32_t k,
                                            uint32_t &lo, uint32_t &hi) {
+    // both dwords loaded together, without a branch (a dword wholly past the
+    // extent is read from the zero block): one round trip, not two
     const uint32_t *p = reinterpret_cast<const uint32_t *>(base);
-    auto masked = [&](uint32_t j) -> uint32_t {
-        const int rem = static_cast<int>(lim) - static_cast<int>(4 * j);
-        if (rem <= 0) return 0u;
-        const uint32_t v = p[j];
-        return rem >= 4 ? v : (v & ((1u << (8 * rem)) - 1u));
-    };
-    lo = masked(k);
-    hi = masked(k + 1);
+    const uint32_t *z = reinterpret_cast<const uint32_t *>(&g_zero16);
+    const int r0 = static_cast<int>(lim) - static_cast<int>(4 * k), r1 = r0 - 4;
+    const uint32_t v0 = *(r0 > 0 ? p + k : z), v1 = *(r1 > 0 ? p + k + 1 : z);
+    auto keep = [](int rem) -> uint32_t { return rem >= 4 ? 0xFFFFFFFFu : rem <= 0 ? 0u : (1u << (8 * rem)) - 1u; };
+    lo = v0 & keep(r0);
+    hi = v1 & keep(r1);
 }
 
 // LINEAR: first-match scan in rule order, wave-uniform records.
@@ -486,8 +486,10 @@ __device__ __forceinline__ uint32_t entry_miss_ext(const T &tab, uint32_t off, c
            ((f.t[1] ^ y.z) & z.y) | ((f.t[2] ^ y.w) & z.z) | ((f.t[3] ^ z.x) & z.w);
 }
 
-// x * entry dwords (IPv6 20 = 16 + 4, IPv4 8): shifts, not a quarter-rate multiply.
-__device__ __forceinline__ uint32_t times_ew(uint32_t x, bool v6) { return v6 ? (x << 4) + (x << 2) : x << 3; }
+// x * entry dwords (IPv6 20, IPv4 8): one full-rate 24-bit multiply (entry
+// numbers < 2^24).  (Written as two shift forms under a select, it compiled
+// to a divergent branch per slot with a quarter-rate v_mul_lo_u32 in it.)
+__device__ __forceinline__ uint32_t times_ew(uint32_t x, bool v6) { return __umul24(x, v6 ? 20u : 8u); }
 
 // First match over the four key slots of the lane's family, walked together:
 // every iteration tests the next entry of every slot list, so the wave pays
@@ -855,7 +857,9 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
             // per round, more per window and +7-11 VGPRs — ran C3 0.502 vs
             // 0.472 ms, C5 even; profiles/r3_ab/)
             const uint32_t ent = !UNCOND || valid[j] ? k + static_cast<uint32_t>(static_cast<int32_t>(dp) >> 1) : 0u;
-            const uint32_t *e = six[j] && (!UNCOND || valid[j]) ? E6 + ent * kHybEnt6Dwords : E4 + ent * kHybEnt4Dwords;
+            // (entry numbers < 2^24, table_consistent: a full-rate 24-bit multiply)
+            const bool e6 = six[j] && (!UNCOND || valid[j]);
+            const uint32_t *e = (e6 ? E6 : E4) + __umul24(ent, e6 ? kHybEnt6Dwords : kHybEnt4Dwords);
             if (UNCOND || valid[j]) {
                 A[j] = g3(e);
                 B[j] = g3(e + 3);

@@ -176,8 +176,10 @@ k_indexed_slots(const uint8_t *__restrict__ slots, uint32_t stride, uint64_t n, 
         }
         Fields f;
         // HYBRID walks: option ports from registers (as the frames kernels);
-        // the streaming INDEXED kernel (C2) keeps the divergent far read
-        // (the select chain cost it 2.6 %, round 1)
+        // the streaming INDEXED kernel (C2) keeps the divergent far read:
+        // it is VALU-bound, the select chain cost it 2.6 % (round 1), and
+        // taking every option port from registers (no far read at all at
+        // stride 64) 9 % (round 3, profiles/r3_ab/regports/)
         constexpr bool REG = TM == kTabFlatLds || TM == kTabFlatLds4 || TM == kTabFlatLds4U;
         parse_fields<REG>(cur, live, f, [&](uint32_t k, uint32_t &lo, uint32_t &hi) {
             far_dwords(pkt, stride, k, lo, hi);
@@ -462,6 +464,9 @@ struct IndexedLaunch {
 static bool table_consistent(const DevTable *t) {
     const CompiledTable &m = t->meta;
     const size_t dw = m.blob.size();
+    // entry numbers (and list offsets) stay below 2^24: the kernels scale
+    // them with 24-bit multiplies (classify.hpp times_ew, classify_flat)
+    if (dw / kHybEnt4Dwords >= (size_t(1) << 24)) return false;
     if (m.algo == NFFACL_ALGO_HYBRID && (m.lds_dwords == 0 || m.idx4.entry_dwords == kHybEnt4Dwords))
         return m.idx4.entry_dwords == kHybEnt4Dwords && m.idx6.entry_dwords == kHybEnt6Dwords &&
                m.off_rec4 <= dw && m.off_rec6 <= dw &&
