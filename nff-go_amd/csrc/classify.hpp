@@ -28,7 +28,7 @@ __device__ __forceinline__ uint32_t funnel16(uint32_t hi, uint32_t lo) {
 // (p0<<8|p1) | (p2<<8|p3) << 16 = sport | dport << 16 (SwapBytesUint16,
 // packet/packet.go:713-715, applied by l4ACL acl.go:511, 515).
 __device__ __forceinline__ uint32_t swap_halves(uint32_t w) {
-    return ((w & 0x00FF00FFu) << 8) | ((w >> 8) & 0x00FF00FFu);
+    return __builtin_amdgcn_perm(w, w, 0x02030001u);  // one v_perm: bytes 1 0 3 2
 }
 
 // Non-zero iff some port of `ports` (sport | dport << 16) is outside
@@ -112,17 +112,19 @@ __device__ __forceinline__ void parse_fields(uint32_t (&d)[16], bool live, Field
     }
     f.ports = swap_halves(pw);
     f.proto = f.is6 ? (d[5] & 0xFFu) : (d[5] >> 24);
-    if (f.is6) {
+    // Address words without a branch: wire dwords F(k) = bytes 4k+2..4k+5
+    // for k = 5..12 serve both families (IPv4 src = F6, dst = F7; IPv6 src =
+    // F5..F8, dst = F9..F12).  Words 1..3 are meaningful for IPv6 lanes only
+    // (every consumer reads them for IPv6 packets alone).
+    uint32_t F[8];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            f.s[k] = funnel16(d[6 + k], d[5 + k]);
-            f.t[k] = funnel16(d[10 + k], d[9 + k]);
-        }
-    } else {
-        f.s[0] = funnel16(d[7], d[6]);
-        f.t[0] = funnel16(d[8], d[7]);
+    for (int k = 0; k < 8; ++k) F[k] = funnel16(d[6 + k], d[5 + k]);
+    f.s[0] = f.is6 ? F[0] : F[1];
+    f.t[0] = f.is6 ? F[4] : F[2];
 #pragma unroll
-        for (int k = 1; k < 4; ++k) { f.s[k] = 0; f.t[k] = 0; }
+    for (int k = 1; k < 4; ++k) {
+        f.s[k] = F[k];
+        f.t[k] = F[4 + k];
     }
 }
 
@@ -477,13 +479,40 @@ __device__ __forceinline__ uint32_t entry_miss(const u32x4 &A, const u32x4 &B, c
     return ((f.s[0] ^ A.x) & A.y) | ((f.t[0] ^ A.z) & A.w) | proto | port_miss(f.ports, B.y, B.z);
 }
 
-// Mismatch bits of the IPv6 extension words 8..19 (address words 1..3).
+// Cursor over a table's dwords for the INDEXED walk: LDS tables are walked
+// by absolute LDS byte address, which the DS instruction takes as is (a
+// dword offset cost a shift and an add of the LDS base per access); other
+// tables by dword offset.
+typedef __attribute__((address_space(3))) const u32x4 lds_u32x4;
+__device__ __forceinline__ uint32_t lds_base() {
+    return static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const char *)lds_tab));
+}
 template <class T>
-__device__ __forceinline__ uint32_t entry_miss_ext(const T &tab, uint32_t off, const Fields &f) {
-    const u32x4 x = tab.ld4(off), y = tab.ld4(off + 4), z = tab.ld4(off + 8);
+struct Cursor {
+    static constexpr bool kLds = std::is_same<T, LdsTab>::value;
+    static constexpr uint32_t kScale = kLds ? 4u : 1u;  // cursor units per dword
+    __device__ static __forceinline__ uint32_t of(uint32_t i) { return kLds ? lds_base() + 4u * i : i; }
+    __device__ static __forceinline__ u32x4 at(const T &tab, uint32_t c, uint32_t dw) {
+        if constexpr (kLds) return *(lds_u32x4 *)(uintptr_t)(c + 4u * dw);
+        else return tab.ld4(c + dw);
+    }
+};
+
+// Mismatch bits of the IPv6 extension words 8..19 (address words 1..3) of
+// the entry at cursor c.
+template <class T>
+__device__ __forceinline__ uint32_t entry_miss_ext(const T &tab, uint32_t c, const Fields &f) {
+    using C = Cursor<T>;
+    const u32x4 x = C::at(tab, c, 8), y = C::at(tab, c, 12), z = C::at(tab, c, 16);
     // x = s1 s2 s3 sm1 | y = sm2 sm3 t1 t2 | z = t3 tm1 tm2 tm3
     return ((f.s[1] ^ x.x) & x.w) | ((f.s[2] ^ x.y) & y.x) | ((f.s[3] ^ x.z) & y.y) |
            ((f.t[1] ^ y.z) & z.y) | ((f.t[2] ^ y.w) & z.z) | ((f.t[3] ^ z.x) & z.w);
+}
+
+// Lane mask of a < b (one v_cmp into an SGPR pair).  A ballot of a combined
+// condition compiled to v_cndmask + v_cmp first: two VALU per ballot.
+__device__ __forceinline__ uint64_t lanes_lt(uint32_t a, uint32_t b) {
+    return __builtin_amdgcn_uicmp(a, b, 36 /* ICMP_ULT */);
 }
 
 // x * entry dwords (IPv6 20, IPv4 8): one full-rate 24-bit multiply (entry
@@ -493,56 +522,68 @@ __device__ __forceinline__ uint32_t times_ew(uint32_t x, bool v6) { return __umu
 
 // First match over the four key slots of the lane's family, walked together:
 // every iteration tests the next entry of every slot list, so the wave pays
-// max(list lengths) table round trips, not their sum.  Loops have
-// wave-uniform trip counts (ballots) and predicated bodies.
+// max(list lengths) table round trips, not their sum.  Loops run while some
+// lane has work (lane masks from v_cmp, no ballot of combined conditions);
+// the IPv6 extension words are read under a plain per-lane branch.
 // U = list entries per slot per loop trip: all NS x U entry loads of a trip
-// are issued before any is tested.  The walk keeps dword offsets (cursor,
-// end) per slot, advanced by adds.  Tables whose reads are free to issue for
-// every lane (T::kFreeLoads: LDS, where an inactive lane's read is harmless
-// and cheaper than the exec-mask juggling and register zeroing a predicated
-// load needs) load unconditionally; global tables load only for lanes still
+// are issued before any is tested.  The walk keeps cursors (Cursor<T>) per
+// slot, advanced by adds.  Tables whose reads are free to issue for every
+// lane (T::kFreeLoads: LDS, where an inactive lane's read is harmless and
+// cheaper than the exec-mask juggling and register zeroing a predicated load
+// needs) load unconditionally; global tables load only for lanes still
 // walking (a 16-byte load costs the TA 16 cycles per 64 active lanes; global:
-// -4 % on C3, profiles/r1_masked).
+// -4 % on C3, profiles/r1_masked).  LDS tables (offsets < 2^16 dwords) get
+// their per-family slot parameters as 16-bit halves of one SGPR each, one
+// v_bfe per parameter instead of two moves and a select.
 template <int NS, int U, class T>
 __device__ __forceinline__ uint32_t classify_indexed(const T &tab, const IndexedArgs &a, const Fields &f) {
+    using C = Cursor<T>;
     const bool v6 = f.is6;
     const bool mine = f.is4 || f.is6;
     const uint32_t ew = v6 ? kEnt6Dwords : kEnt4Dwords;
     const uint32_t key[4] = {__builtin_bswap32(f.t[0]), __builtin_bswap32(f.s[0]), f.ports >> 16,
                              f.ports & 0xFFFFu};
-    uint32_t c[NS], e[NS];  // dword offsets: the slot list's next entry, its end
+    const uint32_t half = v6 ? 16u : 0u;
+    auto par = [&](uint32_t x4, uint32_t x6) -> uint32_t {
+        if constexpr (C::kLds) return __builtin_amdgcn_ubfe(__builtin_amdgcn_readfirstlane(x4 | x6 << 16), half, 16);
+        else return fam_sel(v6, x4, x6);
+    };
+    uint32_t c[NS], e[NS];  // cursors: the slot list's next entry, its end
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
         const SlotArgs &s4 = a.f4.slot[s], &s6 = a.f6.slot[s];
-        const uint32_t shift = fam_sel(v6, s4.shift, s6.shift);
-        const uint32_t dir = fam_sel(v6, s4.off_dir, s6.off_dir);
-        const uint32_t base = fam_sel(v6, s4.off_ent, s6.off_ent);
+        const uint32_t shift = par(s4.shift, s6.shift);
+        const uint32_t dir = par(s4.off_dir, s6.off_dir);
+        const uint32_t base = par(s4.off_ent, s6.off_ent);
         const uint32_t t = key[s] >> shift;  // < n_buckets for any key: both reads in range
         uint32_t lo, hi;
-        tab.bounds(dir, fam_sel(v6, s4.off_dir16, s6.off_dir16), t, lo, hi, a.dir8 != 0u);
-        c[s] = base + times_ew(lo, v6);
-        e[s] = mine ? base + times_ew(hi, v6) : c[s];
+        tab.bounds(dir, C::kLds ? 0u : fam_sel(v6, s4.off_dir16, s6.off_dir16), t, lo, hi, a.dir8 != 0u);
+        c[s] = C::of(base + times_ew(lo, v6));
+        // (a select of the bound, not of the cursor: otherwise the compiler
+        // sank the hi read into a branch, two LDS round trips instead of one)
+        e[s] = C::of(base + times_ew(mine ? hi : lo, v6));
     }
+    const uint32_t cstep = C::kScale * ew;  // one entry in cursor units
     uint32_t best = kNone, out = 0;
     while (true) {
-        bool any = false;
+        uint64_t any = 0;
 #pragma unroll
-        for (int s = 0; s < NS; ++s) any |= c[s] < e[s];
-        if (!ballot(any)) break;
+        for (int s = 0; s < NS; ++s) any |= lanes_lt(c[s], e[s]);
+        if (any == 0u) break;
         u32x4 A[NS][U], B[NS][U];
 #pragma unroll
         for (int s = 0; s < NS; ++s)
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const uint32_t off = c[s] + u * ew;
+                const uint32_t cu = c[s] + u * cstep;
                 if (T::kFreeLoads) {
-                    A[s][u] = tab.ld4(off);
-                    B[s][u] = tab.ld4(off + 4);
+                    A[s][u] = C::at(tab, cu, 0);
+                    B[s][u] = C::at(tab, cu, 4);
                 } else {
                     A[s][u] = B[s][u] = u32x4{0, 0, 0, 0};
-                    if (off < e[s]) {
-                        A[s][u] = tab.ld4(off);
-                        B[s][u] = tab.ld4(off + 4);
+                    if (cu < e[s]) {
+                        A[s][u] = C::at(tab, cu, 0);
+                        B[s][u] = C::at(tab, cu, 4);
                     }
                 }
             }
@@ -551,22 +592,19 @@ __device__ __forceinline__ uint32_t classify_indexed(const T &tab, const Indexed
             bool go = true;
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const uint32_t off = c[s] + u * ew;
-                const bool act = go && off < e[s];
+                const uint32_t cu = c[s] + u * cstep;
+                const bool act = go && cu < e[s];
                 const uint32_t idx = B[s][u].x >> kEntIndexShift;
                 const bool earlier = act && idx < best;
                 bool pass = entry_miss(A[s][u], B[s][u], f) == 0u;
-                const bool ext = v6 && earlier && pass;
-                if (ballot(ext)) {
-                    if (ext) pass = entry_miss_ext(tab, off + 8, f) == 0u;
-                }
+                if (v6 && earlier && pass) pass = entry_miss_ext(tab, cu, f) == 0u;
                 const bool take = earlier && pass;
                 best = take ? idx : best;
                 out = take ? B[s][u].w : out;
                 // stop at a hit, or once the ascending list has passed `best`
                 go = earlier && !pass;
             }
-            c[s] = go ? c[s] + U * ew : e[s];
+            c[s] = go ? c[s] + U * cstep : e[s];
         }
     }
     // rules with no selective key: wave-uniform scan in rule order per family
@@ -575,16 +613,15 @@ __device__ __forceinline__ uint32_t classify_indexed(const T &tab, const Indexed
         const FamArgs &fa = fam ? a.f6 : a.f4;
         const bool in_fam = fam ? f.is6 : f.is4;
         const uint32_t w = fam ? kEnt6Dwords : kEnt4Dwords;
+        if (fa.n_resid == 0u) continue;
+        const uint64_t fam_lanes = ballot(in_fam);
         for (uint32_t i = 0; i < fa.n_resid; ++i) {
-            const uint32_t off = fa.off_resid + i * w;
-            const u32x4 A = tab.ld4(off), B = tab.ld4(off + 4);
+            const uint32_t cu = C::of(fa.off_resid + i * w);
+            const u32x4 A = C::at(tab, cu, 0), B = C::at(tab, cu, 4);
             const uint32_t idx = B.x >> kEntIndexShift;
-            const bool want = in_fam && idx < best;
-            if (!ballot(want)) break;  // residual list ascends too
-            bool pass = want && entry_miss(A, B, f) == 0u;
-            if (fam && ballot(pass)) {
-                if (pass) pass = entry_miss_ext(tab, off + 8, f) == 0u;
-            }
+            if ((lanes_lt(idx, best) & fam_lanes) == 0u) break;  // residual list ascends too
+            bool pass = in_fam && idx < best && entry_miss(A, B, f) == 0u;
+            if (fam && pass) pass = entry_miss_ext(tab, cu, f) == 0u;
             best = pass ? idx : best;
             out = pass ? B.w : out;
         }
