@@ -63,7 +63,9 @@ struct Fields {
 // (IHL <= 11, untagged) come from them through a select chain, so only lanes
 // whose ports lie past byte 64 read memory — most waves of C3 have some lane
 // with options, and its dependent far read stalled the whole wave.
-template <bool REG_OPTS = false, class FarDwords>
+// NOPORTS: the caller's table tests no port; f.ports is left 0 and no
+// option-port dword is read.
+template <bool REG_OPTS = false, bool NOPORTS = false, class FarDwords>
 __device__ __forceinline__ void parse_fields(uint32_t (&d)[16], bool live, Fields &f, FarDwords far,
                                              uint32_t flags) {
     const bool vlan = (flags & NFFACL_PARSE_VLAN) != 0;
@@ -84,7 +86,9 @@ __device__ __forceinline__ void parse_fields(uint32_t (&d)[16], bool live, Field
     // IPv6: proto byte 20, src 22..37, dst 38..53, L4 at 54 (packet.go:283-285)
     const uint32_t ihl = (d[3] >> 16) & 0xFu;
     uint32_t pw = f.is6 ? funnel16(d[14], d[13]) : funnel16(d[9], d[8]);
-    if (REG_OPTS) {
+    if (NOPORTS) {
+        pw = 0u;
+    } else if (REG_OPTS) {
         const bool opt = f.is4 && ihl != 5u;
         if (ballot(opt)) {
             // in the (VLAN-shifted) registers the L4 dword is 3 + IHL; valid
@@ -354,6 +358,9 @@ struct IndexedArgs {
 enum TableMode : int {
     kTabGlobal = 0,  // INDEXED, read through L1/L2/MALL
     kTabLds = 1,     // INDEXED, staged whole in LDS
+    kTabLdsNP = 9,   // the same for tables that constrain no port
+                     // (CompiledTable::ports_any): no L4 port extraction
+                     // (no option-port reads) and no port tests
     kTabSplit = 2,   // HYBRID lane form: INDEXED entries in global memory,
                      // directories staged in LDS, one workgroup per CU; the
                      // spare VGPRs buy the frames kernel a two-batch software
@@ -474,9 +481,10 @@ __device__ __forceinline__ uint32_t fam_sel(bool v6, uint32_t x4, uint32_t x6) {
 // Mismatch bits of an entry's first 8 dwords (A = words 0..3, B = 4..7):
 // address words, protocol (exact flag) and ports — acl.go:526-539 / 546-557
 // with IPv6 restricted to the top 32 bits of each address.
+template <bool NP = false>
 __device__ __forceinline__ uint32_t entry_miss(const u32x4 &A, const u32x4 &B, const Fields &f) {
     const uint32_t proto = ((f.proto ^ B.x) & 0xFFu) & (0u - ((B.x >> 8) & 1u));
-    return ((f.s[0] ^ A.x) & A.y) | ((f.t[0] ^ A.z) & A.w) | proto | port_miss(f.ports, B.y, B.z);
+    return ((f.s[0] ^ A.x) & A.y) | ((f.t[0] ^ A.z) & A.w) | proto | (NP ? 0u : port_miss(f.ports, B.y, B.z));
 }
 
 // Cursor over a table's dwords for the INDEXED walk: LDS tables are walked
@@ -535,7 +543,7 @@ __device__ __forceinline__ uint32_t times_ew(uint32_t x, bool v6) { return __umu
 // -4 % on C3, profiles/r1_masked).  LDS tables (offsets < 2^16 dwords) get
 // their per-family slot parameters as 16-bit halves of one SGPR each, one
 // v_bfe per parameter instead of two moves and a select.
-template <int NS, int U, class T>
+template <int NS, int U, class T, bool NP = false>
 __device__ __forceinline__ uint32_t classify_indexed(const T &tab, const IndexedArgs &a, const Fields &f) {
     using C = Cursor<T>;
     const bool v6 = f.is6;
@@ -596,7 +604,7 @@ __device__ __forceinline__ uint32_t classify_indexed(const T &tab, const Indexed
                 const bool act = go && cu < e[s];
                 const uint32_t idx = B[s][u].x >> kEntIndexShift;
                 const bool earlier = act && idx < best;
-                bool pass = entry_miss(A[s][u], B[s][u], f) == 0u;
+                bool pass = entry_miss<NP>(A[s][u], B[s][u], f) == 0u;
                 if (v6 && earlier && pass) pass = entry_miss_ext(tab, cu, f) == 0u;
                 const bool take = earlier && pass;
                 best = take ? idx : best;
@@ -620,7 +628,7 @@ __device__ __forceinline__ uint32_t classify_indexed(const T &tab, const Indexed
             const u32x4 A = C::at(tab, cu, 0), B = C::at(tab, cu, 4);
             const uint32_t idx = B.x >> kEntIndexShift;
             if ((lanes_lt(idx, best) & fam_lanes) == 0u) break;  // residual list ascends too
-            bool pass = in_fam && idx < best && entry_miss(A, B, f) == 0u;
+            bool pass = in_fam && idx < best && entry_miss<NP>(A, B, f) == 0u;
             if (fam && pass) pass = entry_miss_ext(tab, cu, f) == 0u;
             best = pass ? idx : best;
             out = pass ? B.w : out;
@@ -797,14 +805,22 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
     // positional slots (a.generic == 0: slot s keys on field s, 1-D): the key
     // is known at compile time, no per-lane field selects (wave-uniform branch)
     if (LDS_DIRS && a.generic == 0u) {
+        // directories staged in LDS: offsets < 2^16 dwords, so the family
+        // parameters travel as 16-bit SGPR halves (one v_bfe each, as in
+        // classify_indexed); global directories (service.hip): fam_sel
+        const uint32_t half = v6 ? 16u : 0u;
+        auto par = [&](uint32_t x4, uint32_t x6) -> uint32_t {
+            if (DIRS_IN_LDS) return __builtin_amdgcn_ubfe(__builtin_amdgcn_readfirstlane(x4 | x6 << 16), half, 16);
+            return fam_sel(v6, x4, x6);
+        };
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
             const SlotArgs &s4 = a.f4.slot[s], &s6 = a.f6.slot[s];
             const uint32_t key = s == kFDst ? kd : s == kFSrc ? ks : s == kFDport ? dport : s == kFSport ? sport : 0u;
-            const uint32_t t = key >> (fam_sel(v6, s4.shift, s6.shift));
+            const uint32_t t = key >> par(s4.shift, s6.shift);
             uint32_t hi;
-            DirTab<DIRS_IN_LDS>{a.tab, a.tab_dwords}.bounds(fam_sel(v6, s4.off_dir, s6.off_dir), fam_sel(v6, s4.off_dir16, s6.off_dir16), t, st[s], hi,
-                                   a.dir8 != 0u);
+            DirTab<DIRS_IN_LDS>{a.tab, a.tab_dwords}.bounds(par(s4.off_dir, s6.off_dir), par(s4.off_dir16, s6.off_dir16),
+                                                            t, st[s], hi, a.dir8 != 0u);
             ln[s] = mine ? hi - st[s] : 0u;
         }
     } else {

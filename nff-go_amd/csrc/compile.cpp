@@ -1191,6 +1191,10 @@ bool compile_table(const nffacl_rules &rules, int algo, const CompileOptions &op
     }
     if (out.blob.empty()) out.blob.push_back(0);  // keep a valid allocation
     while (out.blob.size() % 4) out.blob.push_back(0);
+    bool any = true;
+    for (size_t i = 4; i < rec4.size() && any; i += kRec4Dwords) any = (rec4[i] & kMetaPortCheck) == 0u;
+    for (size_t i = 16; i < rec6.size() && any; i += kRec6Dwords) any = (rec6[i] & kMetaPortCheck) == 0u;
+    out.ports_any = any ? 1u : 0u;
     return true;
 }
 

@@ -59,6 +59,10 @@ struct CompiledTable {
     // flat-LDS walk with many expected candidates per packet: its entry
     // loads are issued without a per-lane branch (engine.hip kTabFlatLds4U)
     uint32_t flat_uncond = 0;
+    // no rule constrains a port (every record's port bounds are [0, 65535]
+    // both ways): the INDEXED LDS kernel skips the L4 port extraction and
+    // tests (engine.hip kTabLdsNP)
+    uint32_t ports_any = 0;
     // two-level LDS directories with u8 offsets per 16-bucket group (every
     // slot of the table; DimInfo::dir8)
     uint32_t dir8 = 0;

@@ -99,6 +99,7 @@ __device__ __forceinline__ uint32_t classify_any(const IndexedArgs &a, const Fie
     }
     if constexpr (NS <= 4) {  // per-lane walks: the positional four slots
         if (TM == kTabLds) return classify_indexed<NS, 1>(LdsTab{}, a, f);
+        if (TM == kTabLdsNP) return classify_indexed<NS, 1, LdsTab, true>(LdsTab{}, a, f);
         if (TM == kTabSplit) return classify_indexed<NS, 1>(SplitTab{a.tab}, a, f);
         return classify_indexed<NS, 1>(GlobalTab{a.tab}, a, f);
     }
@@ -116,7 +117,7 @@ template <int NS, int TM, int MODE>
 __global__ void __launch_bounds__(1024)
 k_indexed_slots(const uint8_t *__restrict__ slots, uint32_t stride, uint64_t n, IndexedArgs a,
                 uint32_t *__restrict__ port_out, uint64_t *__restrict__ permit_out) {
-    if (TM == kTabLds || TM == kTabSplit || TM == kTabFlatLds || TM == kTabFlatLds4 || TM == kTabFlatLds4U) stage_table(a);
+    if (TM != kTabGlobal && TM != kTabFlat && TM != kTabFlat4) stage_table(a);
     const uint32_t lane = lane_id();
     const uint32_t wpb = blockDim.x >> 6;
     const uint64_t wave0 = uint64_t(blockIdx.x) * wpb + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -181,7 +182,7 @@ k_indexed_slots(const uint8_t *__restrict__ slots, uint32_t stride, uint64_t n, 
         // taking every option port from registers (no far read at all at
         // stride 64) 9 % (round 3, profiles/r3_ab/regports/)
         constexpr bool REG = TM == kTabFlatLds || TM == kTabFlatLds4 || TM == kTabFlatLds4U;
-        parse_fields<REG>(cur, live, f, [&](uint32_t k, uint32_t &lo, uint32_t &hi) {
+        parse_fields<REG, TM == kTabLdsNP>(cur, live, f, [&](uint32_t k, uint32_t &lo, uint32_t &hi) {
             far_dwords(pkt, stride, k, lo, hi);
         }, a.flags);
         const uint32_t res = classify_any<NS, TM>(a, f);
@@ -206,7 +207,7 @@ template <int NS, int TM>
 __global__ void __launch_bounds__(1024)
 k_indexed_frames(const uint8_t *__restrict__ frames, const uint64_t *__restrict__ desc, uint64_t n,
                  IndexedArgs a, uint32_t *__restrict__ port_out, uint64_t *__restrict__ permit_out) {
-    if (TM == kTabLds || TM == kTabSplit || TM == kTabFlatLds || TM == kTabFlatLds4 || TM == kTabFlatLds4U) stage_table(a);
+    if (TM != kTabGlobal && TM != kTabFlat && TM != kTabFlat4) stage_table(a);
     const uint32_t lane = lane_id();
     const uint32_t wpb = blockDim.x >> 6;
     const uint64_t S = uint64_t(gridDim.x) * wpb * 64;  // grid stride in packets
@@ -224,7 +225,7 @@ k_indexed_frames(const uint8_t *__restrict__ frames, const uint64_t *__restrict_
         // the clip is skipped unless some lane of the wave holds a shorter one
         if (ballot(live && len < 64u)) clip16(d, len);
         Fields f;
-        parse_fields<true>(d, live, f, [&](uint32_t k, uint32_t &lo, uint32_t &hi) {
+        parse_fields<true, TM == kTabLdsNP>(d, live, f, [&](uint32_t k, uint32_t &lo, uint32_t &hi) {
             far_dwords(pkt, len, k, lo, hi);
         }, a.flags);
         const uint32_t res = classify_any<NS, TM>(a, f);
@@ -512,7 +513,7 @@ static IndexedLaunch indexed_launch(const nffacl_engine *eng, const DevTable *t)
     } else {
         const size_t bytes = t->meta.blob.size() * sizeof(uint32_t);
         if (bytes <= kLdsTableBytes && tu.lds != 0) {
-            L.tm = dev::kTabLds;
+            L.tm = t->meta.ports_any ? dev::kTabLdsNP : dev::kTabLds;
             staged = bytes;
         }
     }
@@ -562,6 +563,7 @@ static void dispatch_indexed(int ns, int tm, F &&f) {
     auto with_ns = [&](auto nsc) {
         switch (tm) {
         case dev::kTabLds: f(nsc, std::integral_constant<int, dev::kTabLds>{}); break;
+        case dev::kTabLdsNP: f(nsc, std::integral_constant<int, dev::kTabLdsNP>{}); break;
         case dev::kTabSplit: f(nsc, std::integral_constant<int, dev::kTabSplit>{}); break;
         case dev::kTabFlat: f(nsc, std::integral_constant<int, dev::kTabFlat>{}); break;
         case dev::kTabFlat4: f(nsc, std::integral_constant<int, dev::kTabFlat4>{}); break;
@@ -595,7 +597,7 @@ int prepare_kernels() {
     static hipError_t err = hipSuccess;
     std::call_once(once, [] {
         for (int ns = 2; ns <= int(kMaxSlots); ++ns)
-            for (int tm : {int(dev::kTabLds), int(dev::kTabSplit), int(dev::kTabFlatLds), int(dev::kTabFlatLds4),
+            for (int tm : {int(dev::kTabLds), int(dev::kTabLdsNP), int(dev::kTabSplit), int(dev::kTabFlatLds), int(dev::kTabFlatLds4),
                            int(dev::kTabFlatLds4U)}) {
                 if (ns > 4 && tm != dev::kTabFlatLds && tm != dev::kTabFlatLds4 && tm != dev::kTabFlatLds4U)
                     continue;  // flat walks only

@@ -256,6 +256,47 @@ def test_ip_options_frames_vlan(torch_cuda, algo):
 
 
 @pytest.mark.parametrize("algo", ALGOS)
+def test_port_free_rules_options_vlan(torch_cuda, algo):
+    """Rules that constrain no port (C2's shape) compile INDEXED tables that
+    take the no-port kernel (kTabLdsNP: no option-port reads, no port tests):
+    IHL 0..15, tagged and untagged, 64/128-byte slots and packed frames, with
+    and without NFFACL_PARSE_VLAN, against the oracle."""
+    torch = torch_cuda
+    rng = np.random.default_rng(29)
+    n = 4099
+    raw = []
+    for i in range(n):
+        f = bytearray(rng.integers(0, 256, 132, dtype=np.uint8).tobytes())
+        f[12:14] = b"\x08\x00"
+        f[14] = 0x40 | (i % 16)
+        f[23] = [6, 17, 1][i % 3]
+        if (i // 16) % 2:
+            f = f[:12] + bytearray(b"\x81\x00\x00\x05") + f[12:128]
+        raw.append(bytes(f[:128]))
+    text = "\n".join([
+        "ANY 128.0.0.0/1 TCP ANY ANY 2", "0.0.0.0/1 ANY UDP ANY ANY 3", "ANY ANY ICMP ANY ANY 4",
+        "64.0.0.0/2 192.0.0.0/2 ANY ANY ANY 5", "10.0.0.0/8 ANY ANY ANY ANY 6", "ANY 0.0.0.0/3 TCP ANY ANY 7"]) + "\n"
+    rules, (a4, a6) = _rules_and_arrays(text)
+    for stride in (64, 128):
+        slots = slot_buffer(raw, stride)
+        with nffacl.Engine(rules, algo=algo) as eng:
+            p, _ = classify(torch, eng, slots, stride, n)
+        want = oracle.classify_slots(slots, stride, n, a4, a6)
+        np.testing.assert_array_equal(p, want)
+        assert len(set(want.tolist())) > 3
+    frames = np.frombuffer(b"".join(raw), np.uint8).copy()
+    desc = (np.arange(n, dtype=np.uint64) * np.uint64(128)) << np.uint64(16) | np.uint64(128)
+    d_frames, d_desc = to_dev(torch, frames), to_dev(torch, desc.view(np.int64))
+    with nffacl.Engine(rules, algo=algo) as eng:
+        for flags in (0, nffacl.PARSE_VLAN):
+            port = torch.zeros(n, dtype=torch.int32, device="cuda")
+            eng.classify_frames_device(d_frames, d_desc, n, port, None, None, flags)
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(port.cpu().numpy().view(np.uint32),
+                                          oracle.classify_frames(frames, desc, a4, a6, flags=flags))
+
+
+@pytest.mark.parametrize("algo", ALGOS)
 @pytest.mark.parametrize("n", [1, 63, 64, 65, 1000])
 def test_ragged_sizes(torch_cuda, algo, n):
     g = synth.gen_rules(synth.RuleSpec(300), 11)
