@@ -518,7 +518,10 @@ static IndexedLaunch indexed_launch(const nffacl_engine *eng, const DevTable *t)
         }
     }
     if (L.tm != dev::kTabGlobal) {
-        L.block = 1024u;
+        // the no-port kernel: two 768-thread workgroups per CU (24 waves)
+        // beat two of 1024 (0.2119 vs 0.2161 ms on C2; 512 / 640 / 896:
+        // 0.2229 / 0.2216 / 0.2177, profiles/r3_ab/blocks/)
+        L.block = L.tm == dev::kTabLdsNP ? 768u : 1024u;
         // lane form: one workgroup per CU (its VGPRs allow no second one)
         L.per_cu = L.tm == dev::kTabSplit
                        ? 1u
