@@ -146,6 +146,7 @@ class ServiceStats(ctypes.Structure):
 
 _rules_prepare = _sig("nffacl_rules_prepare", _i, _vp, _i)
 _local_device = _sig("nffacl_local_device", _i)
+_device_numa_node = _sig("nffacl_device_numa_node", _i, _i)
 _service_create = _sig("nffacl_service_create", _i, _i, _u32, _u32, _pp)
 _service_classify = _sig("nffacl_service_classify", _i, _vp, _vp, _vp, _u32, _u32, ctypes.POINTER(_u32))
 _service_stats = _sig("nffacl_service_get_stats", _i, _vp, ctypes.POINTER(ServiceStats))
@@ -172,7 +173,7 @@ EXPORTED_SYMBOLS = [
     "nffacl_batcher_create", "nffacl_batcher_submit", "nffacl_batcher_wait", "nffacl_batcher_classify",
     "nffacl_batcher_flush", "nffacl_batcher_get_stats", "nffacl_batcher_destroy",
     "nffacl_batcher_create_device", "nffacl_batcher_submit_rules", "nffacl_batcher_classify_rules",
-    "nffacl_batcher_wait_timeout", "nffacl_local_device",
+    "nffacl_batcher_wait_timeout", "nffacl_local_device", "nffacl_device_numa_node",
     "nffacl_rules_prepare", "nffacl_service_create", "nffacl_service_classify", "nffacl_service_get_stats",
     "nffacl_service_destroy",
 ]
@@ -185,6 +186,12 @@ def abi_version() -> int:
 def local_device() -> int:
     """nffacl_local_device: the HIP device on the calling thread's NUMA node."""
     return _local_device()
+
+
+def device_numa_node(device: int) -> int:
+    """nffacl_device_numa_node: the NUMA node of a device's PCIe attachment
+    (negative status if unknown) — where one-packet callers should run."""
+    return _device_numa_node(device)
 
 
 class NFError(Exception):

@@ -67,3 +67,15 @@ def test_engine_without_device_fails_loudly(gpu_available):
     with pytest.raises(nffacl.NFError) as e:
         nffacl.Engine(rules)
     assert e.value.status in (nffacl.ERR_NO_DEVICE, nffacl.ERR_HIP)
+
+
+def test_device_numa_node(gpu_available):
+    """nffacl_device_numa_node: NO_DEVICE without a GPU; with one, device 0's
+    node (or ERR_HIP where the platform reports none) and INVALID_ARG for a
+    device that does not exist."""
+    if not gpu_available:
+        assert nffacl.device_numa_node(0) == nffacl.ERR_NO_DEVICE
+        return
+    assert nffacl.device_numa_node(0) >= 0 or nffacl.device_numa_node(0) == nffacl.ERR_HIP
+    assert nffacl.device_numa_node(-1) == nffacl.ERR_INVALID_ARG
+    assert nffacl.device_numa_node(4096) == nffacl.ERR_INVALID_ARG

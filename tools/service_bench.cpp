@@ -7,6 +7,7 @@
 //
 //   service_bench RULES SLOTS EXPECT THREADS SECONDS
 // prints one JSON line.
+#include <sched.h>
 #include <sys/resource.h>
 
 #include <algorithm>
@@ -52,6 +53,31 @@ int main(int argc, char **argv) {
     rules->Prepare();
     std::vector<packet::Packet> pk(n);
     for (size_t i = 0; i < n; ++i) pk[i] = packet::Packet{slots.data() + i * stride, stride};
+    // NFFACL_BENCH_PIN=1: run every caller on the GPU's NUMA node (the
+    // deployment INTEGRATION.md recommends: flow-function lcores pinned there)
+    const int gpu_node = nffacl_device_numa_node(packet::ACLDevice());
+    bool pinned = false;
+    if (const char *pin = std::getenv("NFFACL_BENCH_PIN"); pin && std::atoi(pin) == 1 && gpu_node >= 0) {
+        cpu_set_t allowed, want;
+        CPU_ZERO(&want);
+        if (sched_getaffinity(0, sizeof allowed, &allowed) == 0) {
+            std::ifstream f("/sys/devices/system/node/node" + std::to_string(gpu_node) + "/cpulist");
+            std::string list;
+            std::getline(f, list);
+            size_t i = 0;
+            while (i < list.size()) {  // "a-b,c,d-e"
+                size_t j = list.find(',', i);
+                if (j == std::string::npos) j = list.size();
+                const std::string r = list.substr(i, j - i);
+                const size_t dash = r.find('-');
+                const int a = std::atoi(r.c_str()), b = dash == std::string::npos ? a : std::atoi(r.c_str() + dash + 1);
+                for (int c = a; c <= b && c < CPU_SETSIZE; ++c)
+                    if (CPU_ISSET(c, &allowed)) CPU_SET(c, &want);
+                i = j + 1;
+            }
+            pinned = CPU_COUNT(&want) > 0 && sched_setaffinity(0, sizeof want, &want) == 0;
+        }
+    }
     const flow::SplitFunction split = flow::ACLSplitter(rules);
     (void)split(&pk[0]);  // first call: consumer launch + table descriptor
 
@@ -105,11 +131,13 @@ int main(int argc, char **argv) {
     std::printf("{\"threads\": %u, \"calls\": %llu, \"mpps\": %.3f, \"lat_us_p50\": %.2f, \"lat_us_p90\": %.2f, "
                 "\"lat_us_p99\": %.2f, \"lat_us_p999\": %.1f, \"wrong\": %llu, \"launches\": %llu, "
                 "\"timeouts\": %llu, \"polls\": %llu, \"poll_ns\": %.0f, \"groups\": %llu, \"group_ns\": %.0f, "
-                "\"answered\": %llu, \"cpu_us_per_call\": %.2f, \"cpus_busy\": %.2f, \"cpu_max\": \"%s\"}\n",
+                "\"answered\": %llu, \"cpu_us_per_call\": %.2f, \"cpus_busy\": %.2f, \"cpu_max\": \"%s\", "
+                "\"gpu_node\": %d, \"pinned\": %s}\n",
                 threads, (unsigned long long)total.load(), total.load() / dt / 1e6, pct(0.5), pct(0.9), pct(0.99),
                 pct(0.999), (unsigned long long)bad.load(), (unsigned long long)st.launches,
                 (unsigned long long)st.timeouts, (unsigned long long)st.polls, st.poll_ns,
                 (unsigned long long)st.groups, st.group_ns, (unsigned long long)st.answered,
-                total.load() ? cpu / double(total.load()) * 1e6 : 0.0, cpu / dt, quota.c_str());
+                total.load() ? cpu / double(total.load()) * 1e6 : 0.0, cpu / dt, quota.c_str(), gpu_node,
+                pinned ? "true" : "false");
     return bad.load() ? 1 : 0;
 }
