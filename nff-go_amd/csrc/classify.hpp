@@ -717,7 +717,10 @@ __device__ __forceinline__ uint32_t hyb_miss6(const u32x3 &C, const u32x3 &D, ui
 // the first match of the ordered lists, no early exit needed.
 template <int R>
 struct FlatScratch {
-    uint32_t mark[64 * R];   // window position -> (owner lane << 11 | slot << 8 | position) + 1, 0 = none
+    // window position -> (owner lane << 19 | slot << 16 | position << 8 | owner's protocol) + 1, 0 = none
+    // (ascending with the position, as the prefix max needs; the protocol
+    // rides along so that the owner's fields take three ds_bpermute, not four)
+    uint32_t mark[64 * R];
     uint32_t delta[64 * R];  // window position -> (entry number - candidate number) << 1 | IPv6
     uint64_t best[64];       // per packet (lane): lowest passing rule index << 32 | output code
 };
@@ -853,7 +856,6 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
     const uint32_t off = incl - total;  // first candidate number of this packet
     const uint32_t T = __builtin_amdgcn_readlane(incl, 63);
     W.best[lane] = ~0ull;
-    const uint32_t proto_fam = f.proto | (v6 ? 0x100u : 0u);
     const uint32_t *__restrict__ E4 = a.tab + a.f4.off_ent_base;
     const uint32_t *__restrict__ E6 = a.tab + a.f6.off_ent_base;
     // One window of RR rounds (64 RR candidates) starting at candidate `win`,
@@ -872,7 +874,7 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
         for (int s = 0; s < NS; ++s) {
             if (ln[s] != 0u && so < win + 64u * RR && so + ln[s] > win) {
                 const uint32_t pos = so > win ? so - win : 0u;
-                W.mark[pos] = ((lane << 11 | static_cast<uint32_t>(s) << 8) | pos) + 1u;
+                W.mark[pos] = (lane << 19 | static_cast<uint32_t>(s) << 16 | pos << 8 | (f.proto & 0xFFu)) + 1u;
                 W.delta[pos] = ((st[s] - so) << 1) | (v6 ? 1u : 0u);
             }
             so += ln[s];
@@ -884,7 +886,7 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
         // hold lanes past the wave's candidates (the per-round k < T test
         // stays: with it compiled out the scheduler hoists more loads, and
         // the frames kernels spill at 128 VGPRs).
-        uint32_t owner[RR], idx[RR];
+        uint32_t owner[RR], idx[RR], oproto[RR];
         bool valid[RR], six[RR];
         u32x3 A[RR], B[RR], C[RR], D[RR];
         // the rounds' prefix-max scans are independent (only their carries
@@ -900,8 +902,9 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
             if (j + 1 < RR) carry = __builtin_amdgcn_readlane(m, 63);
             const uint32_t k = win + 64u * j + lane;
             valid[j] = k < T;
-            owner[j] = (m - 1u) >> 11;
-            const uint32_t dp = W.delta[(m - 1u) & 0xFFu];
+            owner[j] = (m - 1u) >> 19;
+            oproto[j] = (m - 1u) & 0xFFu;
+            const uint32_t dp = W.delta[((m - 1u) >> 8) & 0xFFu];
             six[j] = (dp & 1u) != 0u;
             // UNCOND: lanes past the wave's candidates load entry 0 of the
             // IPv4 list (untested) instead of branching around the load
@@ -931,8 +934,8 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
             // the owner packet's fields
             const uint32_t o = owner[j];
             const uint32_t oks = bperm(ks, o), okd = bperm(kd, o);
-            const uint32_t opf = bperm(proto_fam, o), opt = bperm(f.ports, o);
-            pass[j] = valid[j] && hyb_miss(A[j], B[j], oks, okd, opf & 0xFFu, opt) == 0u;
+            const uint32_t opt = bperm(f.ports, o);
+            pass[j] = valid[j] && hyb_miss(A[j], B[j], oks, okd, oproto[j], opt) == 0u;
             idx[j] = A[j].z >> kEntIndexShift;
             any6 |= pass[j] && six[j];
         }
