@@ -299,6 +299,7 @@ bool Tune::from_env(Tune &t, std::string &err) {
     bool set = false;
     if (!env_knob("NFFACL_TUNE_COAL", 0, 5, v, set, err)) return false;
     if (set) t.coal = static_cast<int>(v);
+    t.coal_set = set;
     if (!env_knob("NFFACL_TUNE_BLOCK", 64, 1024, v, set, err)) return false;
     if (set && v % 64 != 0) {
         err = "NFFACL_TUNE_BLOCK: expected a multiple of 64";
@@ -670,7 +671,11 @@ int launch_slots(nffacl_engine *eng, DevTable *t, const uint8_t *d_slots, uint32
         a.flags = flags;
         const IndexedLaunch L = indexed_launch(eng, t);
         const uint32_t grid = grid_for(eng, n, L.block, L.per_cu);
-        const int mode = stride == 64 ? eng->tune.coal : 0;
+        // long flat walks (kTabFlatLds4U, C5) default to mode 5, the next
+        // batch's packets in flight: 0.6278 / 0.6312 vs 0.6340 / 0.6328 ms
+        // (profiles/r3_ab/c5_mode5/); everything else to mode 4
+        int mode = stride == 64 ? eng->tune.coal : 0;
+        if (stride == 64 && !eng->tune.coal_set && L.tm == dev::kTabFlatLds4U) mode = 5;
         dispatch_indexed(L.ns, L.tm, [&](auto nsc, auto tmc) {
             launch_slots_tm<decltype(nsc)::value, decltype(tmc)::value>(mode, L, grid, stream, d_slots, stride, n, a,
                                                                       d_port, d_permit);

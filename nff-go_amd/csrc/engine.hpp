@@ -32,6 +32,7 @@ using TablePtr = std::shared_ptr<DevTable>;
 // never on the launch path.
 struct Tune {
     int coal = 4;    // NFFACL_TUNE_COAL: 64-byte slot load mode 0..5 (engine.hip)
+    bool coal_set = false;  // the mode was set explicitly (else: 5 for kTabFlatLds4U walks)
     int block = 0;   // NFFACL_TUNE_BLOCK: threads per workgroup (0 = kernel default)
     int per_cu = 0;  // NFFACL_TUNE_PER_CU: workgroups per CU (0 = kernel default)
     int rounds = 0;  // NFFACL_TUNE_ROUNDS: flat walks, loads in flight (0 = compiled, 2 or 4)
