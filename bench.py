@@ -360,6 +360,63 @@ def cpu_baseline_for(cfg: str, st: dict, budget_s: float):
     return cb, ports
 
 
+SHAPE_RUNS = (  # (name, service kind, threads, packets per call, seconds)
+    ("scalar_1_thread", "scalar", 1, 0, 1.0),
+    ("scalar_32_threads", "scalar", 32, 0, 1.5),
+    ("burst32_16_clones", "burst", 16, 32, 1.5),
+)
+
+
+def call_shapes(cfg: str, text: str, gen, cpu_mpps, local: int):
+    """The reference's own call shapes through the resident consumer, on this
+    config's rules: one packet per call from 1 and 32
+    threads (SetSeparator / SetSplitter, firewall.go:54-57) and 32-packet
+    bursts from 16 clones (VectorSeparateFunction, flow.go:131, 1487-1520),
+    callers pinned to the GPU's NUMA node, every verdict checked against the
+    oracle; beside them the oracle on the same CPUs (cpu_baseline.value: the
+    box's 16-CPU share) — the same-CPU comparison.  Host-driven: packets and
+    verdicts cross PCIe per call (never `value`)."""
+    import ctypes
+    import nffacl
+    from nffacl import synth
+    from oracle import oracle, rules_oracle as ro
+    lib = ctypes.CDLL(str(ROOT / "nff-go_amd" / "libnffshapes.so"))
+    lib.nffshapes_run.restype = ctypes.c_int
+    lib.nffshapes_run.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                  ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                                  ctypes.c_double, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
+    n = 1 << 16
+    slots = synth.gen_slots(gen, n, synth.PACKET_SEEDS.get(cfg, 0) + 31, stride=80)
+    a4, a6 = ro.parse_text_table(text.encode()).arrays()
+    expect = oracle.classify_slots(slots, 80, n, a4, a6, threads=16).astype(np.uint32)
+    rules = nffacl.L3Rules.parse_text(text)
+    node = nffacl.device_numa_node(local)
+    res = {"packets_distinct": n, "slot_bytes": 80, "pinned_numa_node": node if node >= 0 else None,
+           "cpu_same_cpus_mpps": cpu_mpps}
+    svcs = {"scalar": nffacl.Service(local, mailboxes=128), "burst": nffacl.Service(local, mailboxes=32, burst=True)}
+    try:
+        for name, kind, threads, per, secs in SHAPE_RUNS:
+            o = (ctypes.c_double * 9)()
+            st = lib.nffshapes_run(svcs[kind]._h, rules.handle, slots.ctypes.data, 80, n, expect.ctypes.data,
+                                   threads, per, secs, node, o)
+            if st != 0:
+                res[name] = {"error": st}
+                continue
+            sst = svcs[kind].stats()
+            res[name] = {"mpps": round(o[0], 3), "lat_us_p50": round(o[1], 2), "lat_us_p99": round(o[2], 2),
+                         "wrong": int(o[3]), "calls": int(o[4]), "errors": int(o[8]),
+                         "cpu_us_per_packet": round(o[5], 3), "cpus_busy": round(o[6], 2), "pinned": bool(o[7]),
+                         "timeouts": sst["timeouts"], "table_oob": sst["table_oob"]}
+            if cpu_mpps:
+                res[name]["vs_cpu_same_cpus"] = round(o[0] / cpu_mpps, 3)
+    finally:
+        for v in svcs.values():
+            v.close()
+    res["bit_exact"] = all(isinstance(v, dict) and v.get("wrong") == 0 and v.get("errors") == 0
+                           for k, v in res.items() if k in {r[0] for r in SHAPE_RUNS})
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -378,6 +435,8 @@ def main():
     ap.add_argument("--no-host", action="store_true", help="skip the PCIe-inclusive measurement")
     ap.add_argument("--no-scatter", action="store_true",
                     help="N>1: skip the root-scattered (scatter+classify+gather) measurement")
+    ap.add_argument("--no-shapes", action="store_true",
+                    help="N=1: skip the call-shape record (scalar calls / bursts through the resident consumer)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend for N>1 (nccl = RCCL on ROCm)")
     args = ap.parse_args()
@@ -466,6 +525,12 @@ def main():
         ok = ok and cb["bit_exact_vs_gpu"]
     elif rank == 0:
         out["cpu_baseline"] = None
+    shapes = {}
+    do_shapes = rank == 0 and world == 1 and not args.no_shapes and cfg in ("c1", "c2", "c3", "c5")
+    if do_shapes:
+        text, gen = build_rules(cfg)
+        shapes[cfg] = call_shapes(cfg, text, gen, (out.get("cpu_baseline") or {}).get("value"), local)
+        ok = ok and shapes[cfg]["bit_exact"]
     eng.close()
     del st
 
@@ -481,11 +546,17 @@ def main():
             rec["cpu_baseline"] = cb
             ok = ok and cb["bit_exact_vs_gpu"]
         ok = ok and rec["bit_exact_sample"]
+        if do_shapes and c in ("c1", "c2", "c3", "c5"):
+            text, gen = build_rules(c)
+            shapes[c] = call_shapes(c, text, gen, (rec.get("cpu_baseline") or {}).get("value"), local)
+            ok = ok and shapes[c]["bit_exact"]
         out["configs"][c] = rec
         st["eng"].close()
         del st
         torch.cuda.empty_cache()
 
+    if shapes:
+        out["call_shapes"] = shapes
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -62,7 +62,7 @@
 extern "C" {
 #endif
 
-#define NFFACL_ABI_VERSION 4
+#define NFFACL_ABI_VERSION 5
 
 /* Only the entry points below are exported from libnffacl.so (built with
  * -fvisibility=hidden). */
@@ -306,8 +306,12 @@ NFFACL_API int nffacl_classify_host_ex(nffacl_engine *eng, const uint8_t *h_slot
  * sleeps until its verdicts are back.  A batch whose first burst has waited
  * `max_delay_us` ships whatever else is in flight.  Thread-safe: any number of
  * concurrent submitters per batcher.  Every ticket must be waited for exactly
- * once (its batch buffer is reused only then); tickets not yet waited for may
- * hold up to (nbuf - 1) * max_batch packets before submit blocks for a buffer.
+ * once (its batch buffer is reused only then).  Tickets not yet waited for
+ * keep their batches' buffers busy: a batch ships at the latest when its first
+ * burst is max_delay_us old, so a caller that submits without waiting can hold
+ * as few as one burst per buffer.  When every buffer is busy, submit waits for
+ * one to free (back-pressure) at most 1 s and then returns NFFACL_ERR_TIMEOUT
+ * without a ticket (the bursts held are the caller's own to collect).
  * Each batch carries its own status: a failed launch fails the bursts of that
  * batch only.  A batch classifies against one table — the engine's active
  * table, or the rule set a burst was submitted with (nffacl_batcher_*_rules):
@@ -401,19 +405,47 @@ typedef struct nffacl_service_stats {
     double poll_ns;     /* mean poll duration, load issue to data */
     uint64_t groups;    /* request groups classified (one table per group) */
     double group_ns;    /* mean time to classify + answer a group */
-    uint64_t answered;  /* requests answered by the consumer */
+    uint64_t answered;  /* requests answered by the consumer (packets) */
+    uint64_t retries;   /* requests re-posted after a first timeout (see the failure policy below) */
 } nffacl_service_stats;
 
 /* mailboxes: a multiple of 64 (one consumer wave per 8; 0 = 128), one per
  * calling thread (threads beyond that share mailboxes under a lock);
  * idle_us: consumer lifetime without calls (0 = 2000). */
 NFFACL_API int nffacl_service_create(int hip_device, uint32_t mailboxes, uint32_t idle_us, nffacl_service **out);
+/* A burst service (ABI 5): the VectorSeparateFunction shape — every call
+ * carries a clone's whole burst of up to 32 packets (flow/flow.go:131,
+ * 1487-1520: segmentProcess hands the separator one burst at a time and
+ * waits for its answers).  One mailbox per calling thread (mailboxes 1..1024,
+ * 0 = 64), one consumer wave per mailbox; a request is one rule set. */
+NFFACL_API int nffacl_service_create_burst(int hip_device, uint32_t mailboxes, uint32_t idle_us,
+                                           nffacl_service **out);
 /* L3ACLPort of one packet: frame = its Ether header, len its bytes (bytes past
  * len, and past 80, read as 0 — the batcher's 80-byte slot); flags:
  * enum nffacl_parse_flags.  *port <- the verdict (permit = port > 0).  Blocks
- * about one PCIe round trip; NFFACL_ERR_TIMEOUT after 1 s without an answer. */
+ * about one PCIe round trip.  On a burst service: a burst of one.
+ *
+ * Failure policy (the reference's verdict path never errors, acl.go:522-565;
+ * a caller must not crash the flow function it runs in): a call with no answer
+ * after 1 s (NFFACL_TUNE_SVC_TIMEOUT_US) re-posts its request once and re-arms
+ * the consumer (stats.retries); with no answer after another 1 s it withdraws
+ * the request (the consumer answers a withdrawn request without reading any
+ * table, so the rules may be freed at once), sets the verdict(s) to 0 —
+ * reject, the value l3ACL gives a packet that matches no rule — and returns
+ * NFFACL_ERR_TIMEOUT (stats.timeouts).  Bindings use the verdict and count the
+ * event instead of failing the flow function.  Later calls
+ * are served normally once the consumer runs again. */
 NFFACL_API int nffacl_service_classify(nffacl_service *svc, const nffacl_rules *rules, const uint8_t *frame,
                                        uint32_t len, uint32_t flags, uint32_t *port);
+/* L3ACLPort of a burst (burst services only): frames[i] / lens[i] as above
+ * (lens NULL: 80 bytes each), n <= 32; ports[i] <- the verdict of packet i.
+ * One PCIe round trip for the whole burst; failure policy as above. */
+NFFACL_API int nffacl_service_classify_burst(nffacl_service *svc, const nffacl_rules *rules,
+                                             const uint8_t *const *frames, const uint32_t *lens, uint32_t n,
+                                             uint32_t flags, uint32_t *ports);
+/* paused != 0: stop the resident consumer and launch none until resumed (GPU
+ * maintenance; calls meanwhile follow the failure policy); 0: resume. */
+NFFACL_API int nffacl_service_pause(nffacl_service *svc, int paused);
 NFFACL_API int nffacl_service_get_stats(nffacl_service *svc, nffacl_service_stats *out);
 /* Stops the consumer and frees; no call may be running. */
 NFFACL_API void nffacl_service_destroy(nffacl_service *svc);

@@ -240,6 +240,11 @@ int create_impl(nffacl_engine *eng, bool own, uint32_t stride, uint32_t max_batc
             return fail(NFFACL_ERR_INVALID_ARG);
         }
         if (set) b->hold = v != 0;
+        if (!env_knob("NFFACL_TUNE_BATCH_SUBMIT_MS", 1, 60000, v, set, err)) {
+            set_last_error(err);
+            return fail(NFFACL_ERR_INVALID_ARG);
+        }
+        if (set) b->submit_bound = std::chrono::milliseconds(v);
     }
     b->bufs.reset(new (std::nothrow) BatchBuf[nbuf]);
     if (!b->bufs) return fail(NFFACL_ERR_NOMEM);
@@ -276,6 +281,7 @@ int submit_impl(nffacl_batcher *b, DevTable *table, const uint8_t *const *frames
     std::unique_lock<std::mutex> lk(b->mu);
     BatchBuf *x = nullptr;
     uint32_t off = 0, burst = 0;
+    Clock::time_point give_up{};  // set at the first back-pressure wait
     while (true) {
         if (b->stop) return NFFACL_ERR_INVALID_ARG;
         BatchBuf &cur = b->bufs[b->open_idx];
@@ -290,7 +296,17 @@ int submit_impl(nffacl_batcher *b, DevTable *table, const uint8_t *const *frames
             cur.readers.store(0, std::memory_order_relaxed);
             cur.written.store(0, std::memory_order_relaxed);
         } else if (cur.state != BatchBuf::OPEN) {
-            b->cv_free.wait(lk);  // every buffer in flight: back-pressure
+            // every buffer busy: back-pressure.  Bounded: buffers whose
+            // batches are done stay busy until their tickets are collected,
+            // and when the tickets are this caller's own (submitted, not yet
+            // waited for) no amount of waiting frees one.
+            const auto now = Clock::now();
+            if (give_up == Clock::time_point{}) give_up = now + b->submit_bound;
+            if (now >= give_up) {
+                set_last_error("batcher submit: every buffer holds bursts not yet waited for");
+                return NFFACL_ERR_TIMEOUT;
+            }
+            b->cv_free.wait_until(lk, give_up);
             continue;
         }
         if (cur.count > 0 && cur.table != table) {  // another rule set: the next batch

@@ -78,6 +78,9 @@ struct nffacl_batcher {
     uint32_t stride = 64;
     uint32_t max_batch = 0;
     std::chrono::microseconds max_delay{100};  // longest wait behind a full pipeline
+    // longest back-pressure wait of a submit before NFFACL_ERR_TIMEOUT
+    // (NFFACL_TUNE_BATCH_SUBMIT_MS, tests)
+    std::chrono::milliseconds submit_bound{1000};
     uint32_t nbuf = 0;
     std::unique_ptr<nffacl::BatchBuf[]> bufs;
 

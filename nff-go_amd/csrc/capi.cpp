@@ -229,7 +229,7 @@ int nffacl_table_compile(const nffacl_rules *rules, int algo, uint32_t *blob, ui
         o.entry_dwords = fi[f]->entry_dwords;
         o.off_resid = fi[f]->off_resid;
         o.n_resid = fi[f]->n_resid;
-        o.n_slots = ct.slots_g ? fi[f]->used_slots : 4u;
+        o.n_slots = ct.slots_g ? fi[f]->used_slots : std::max(4u, fi[f]->used_slots);
         o.off_ent_base = fi[f]->off_ent_base;
         for (uint32_t k = 0; k < kMaxSlots; ++k) {
             const DimInfo &d = fi[f]->dims[k];

@@ -543,9 +543,22 @@ __device__ __forceinline__ uint32_t times_ew(uint32_t x, bool v6) { return __umu
 // -4 % on C3, profiles/r1_masked).  LDS tables (offsets < 2^16 dwords) get
 // their per-family slot parameters as 16-bit halves of one SGPR each, one
 // v_bfe per parameter instead of two moves and a select.
+#ifndef NFFACL_EXP_LDSDEAD
+#define NFFACL_EXP_LDSDEAD 1
+#endif
+// LDS walks: the cursor of a lane whose list is done points past the LDS
+// allocation (kDeadCursor > every list end, so the loop test stays one
+// v_cmp): its unconditional entry reads return 0 without touching a bank.
+// (Left at its list end, every done lane of a trip read its own random
+// entry: 35 M LDS bank-conflict cycles per C2 launch instead of 10 M,
+// profiles/prof_r3c_c2 vs prof_r2i_c2.)
+constexpr uint32_t kDeadCursor = 0xFFFF0000u;
+
 template <int NS, int U, class T, bool NP = false>
 __device__ __forceinline__ uint32_t classify_indexed(const T &tab, const IndexedArgs &a, const Fields &f) {
     using C = Cursor<T>;
+    constexpr bool kDead = C::kLds && NFFACL_EXP_LDSDEAD == 1;
+    constexpr bool kPred = C::kLds && NFFACL_EXP_LDSDEAD == 2;
     const bool v6 = f.is6;
     const bool mine = f.is4 || f.is6;
     const uint32_t ew = v6 ? kEnt6Dwords : kEnt4Dwords;
@@ -570,6 +583,7 @@ __device__ __forceinline__ uint32_t classify_indexed(const T &tab, const Indexed
         // (a select of the bound, not of the cursor: otherwise the compiler
         // sank the hi read into a branch, two LDS round trips instead of one)
         e[s] = C::of(base + times_ew(mine ? hi : lo, v6));
+        if (kDead) c[s] = c[s] < e[s] ? c[s] : kDeadCursor;
     }
     const uint32_t cstep = C::kScale * ew;  // one entry in cursor units
     uint32_t best = kNone, out = 0;
@@ -584,7 +598,7 @@ __device__ __forceinline__ uint32_t classify_indexed(const T &tab, const Indexed
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const uint32_t cu = c[s] + u * cstep;
-                if (T::kFreeLoads) {
+                if (T::kFreeLoads && !kPred) {
                     A[s][u] = C::at(tab, cu, 0);
                     B[s][u] = C::at(tab, cu, 4);
                 } else {
@@ -612,7 +626,7 @@ __device__ __forceinline__ uint32_t classify_indexed(const T &tab, const Indexed
                 // stop at a hit, or once the ascending list has passed `best`
                 go = earlier && !pass;
             }
-            c[s] = go ? c[s] + U * cstep : e[s];
+            c[s] = go ? c[s] + U * cstep : (kDead ? kDeadCursor : e[s]);
         }
     }
     // rules with no selective key: wave-uniform scan in rule order per family

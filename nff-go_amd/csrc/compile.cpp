@@ -111,6 +111,9 @@ void rec_ranges(const uint32_t *rec, bool v6, KeyRange out[4]) {
 struct DimBuild {
     uint32_t kind = 0;
     uint32_t key_bits = 32;
+    // fine 2-D slot (flat-LDS positional slots 4..7, build_hybrid): bucket =
+    // (key >> shift) << bits2 | key2 >> shift2; lists filled by GSlot::fill
+    uint32_t kind2 = kKeyNone, shift2 = 0, bits2 = 0;
     std::vector<uint32_t> rules;  // record indices, ascending
     std::vector<KeyRange> ranges; // parallel to rules
     // built
@@ -139,6 +142,11 @@ constexpr size_t kCoarseMinMoved = 256;
 
 // Fewest rules worth a source-port slot of their own (see assign_family).
 constexpr size_t kMinSportRules = 128;
+
+// Fine 2-D slots (build_hybrid): a family needs kFineMinRules rules and a
+// slot kFineMinMoved moved rules.
+constexpr uint32_t kFineMinRules = 4096;
+constexpr size_t kFineMinMoved = 256;
 
 // Pick the radix width and count the replicated entries of the dimension's
 // bucket lists: start at ~4 buckets per rule and narrow the radix while wide
@@ -940,6 +948,85 @@ void build_hybrid(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vec
     // measured 4 faster, 0.507 vs 0.540, before adaptive rounds)
     if (flat && lds_dirs) out.flat_rounds = expect > kHybFlat4Candidates ? 4 : 2;
     if (flat && lds_dirs && opt.uncond >= 0) out.flat_uncond = static_cast<uint32_t>(opt.uncond);
+    // Fine 2-D slots (flat-LDS, positional slots 4..7: dst x dport, src x
+    // dport, dst x sport, src x sport): a rule whose best single field is
+    // wide — a short address prefix with the other address ANY, C5's
+    // dominant candidates (1.5 per packet from /8 rules alone) — is
+    // selective in an address-port pair.  Such a rule moves when the pair
+    // grid's bucket covers a fraction of the key space below CompileOptions::fine_gain
+    // of what its 1-D slot's bucket covers; the grids have fixed shapes (a
+    // address bits x p port bits) and their directories come off the budget.
+    DimBuild fine[2][4];
+    bool any_fine = false;
+    if (flat && lds_dirs && !tuned && opt.fine_a > 0 && !opt.coarse) {
+        const uint32_t fa = static_cast<uint32_t>(opt.fine_a), fp = static_cast<uint32_t>(opt.fine_p);
+        static const uint32_t f1s[4] = {kFDst, kFSrc, kFDst, kFSrc}, f2s[4] = {kFDport, kFDport, kFSport, kFSport};
+        size_t fine_bytes = 0;
+        for (int f = 0; f < 2; ++f) {
+            FamilyPlan &pl = plan[f];
+            const uint32_t n = f ? n6 : n4;
+            if (n < kFineMinRules) continue;
+            GSlot g[4];
+            for (int k = 0; k < 4; ++k) g[k].f1 = f1s[k], g[k].b1 = fa, g[k].f2 = f2s[k], g[k].b2 = fp;
+            std::vector<std::vector<uint32_t>> moved(4);
+            std::vector<char> gone(n, 0);
+            for (int d = 0; d < 4; ++d) {
+                const DimBuild &db = pl.dims[d];
+                for (size_t i = 0; i < db.rules.size(); ++i) {
+                    const uint32_t r = db.rules[i];
+                    const double own = double((db.ranges[i].hi >> db.shift) - (db.ranges[i].lo >> db.shift) + 1) /
+                                       double(uint64_t(1) << db.rb);
+                    int best = -1;
+                    double bc = own * opt.fine_gain;
+                    for (int k = 0; k < 4; ++k) {
+                        const double c = double(g[k].count(pl.rr[r])) / double(g[k].n_buckets());
+                        if (c < bc) { bc = c; best = k; }
+                    }
+                    if (best >= 0) { moved[best].push_back(r); gone[r] = 1; }
+                }
+            }
+            for (int k = 0; k < 4; ++k) {
+                if (moved[k].size() < kFineMinMoved) continue;  // not worth a slot: the rules stay
+                std::sort(moved[k].begin(), moved[k].end());
+                g[k].rules = moved[k];
+                g[k].fill(pl.rr);
+                DimBuild &fd = fine[f][k];
+                fd.kind = field_kind(g[k].f1, f == 1);
+                fd.key_bits = 32;
+                fd.rb = g[k].b1 + g[k].b2;
+                fd.shift = 32 - g[k].b1;
+                fd.kind2 = field_kind(g[k].f2, f == 1);
+                fd.bits2 = g[k].b2;
+                fd.shift2 = 16 - g[k].b2;
+                fd.rules = g[k].rules;
+                fd.dir = g[k].dir;
+                fd.ents = g[k].ents;
+                fd.max_list = g[k].max_list;
+                fine_bytes += size_t(dir_form_bytes(double(g[k].n_buckets()), fmt)) + 16;
+                any_fine = true;
+            }
+            for (int d = 0; d < 4; ++d) {  // the moved rules leave their 1-D slots
+                DimBuild &db = pl.dims[d];
+                std::vector<uint32_t> keep;
+                std::vector<KeyRange> keep_r;
+                for (size_t i = 0; i < db.rules.size(); ++i) {
+                    const uint32_t r = db.rules[i];
+                    bool left = false;
+                    if (gone[r])
+                        for (int k = 0; k < 4 && !left; ++k)
+                            left = !fine[f][k].rules.empty() && std::binary_search(fine[f][k].rules.begin(),
+                                                                                   fine[f][k].rules.end(), r);
+                    if (!left) {
+                        keep.push_back(r);
+                        keep_r.push_back(db.ranges[i]);
+                    }
+                }
+                db.rules.swap(keep);
+                db.ranges.swap(keep_r);
+            }
+        }
+        if (any_fine) size_and_fill(all, weight, budget > fine_bytes ? budget - fine_bytes : 1024, fmt);
+    }
     // Coarse address slots (flat-LDS): a rule whose prefix is shorter than
     // its address slot's radix is replicated into 2^(radix - length) buckets
     // (C5 at 15-bit radixes: 3.1-3.5 entries per rule, 6.4 MB of entries,
@@ -999,7 +1086,19 @@ void build_hybrid(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vec
         }
         return true;
     };
-    while (!form_fits(fmt)) {
+    auto fine_fits = [&](int f) {
+        if (f == 0) return true;
+        const uint32_t gs = f == 8 ? kDir8GroupShift : kDir16GroupShift;
+        const uint32_t lim = f == 8 ? 0xFFu : 0xFFFFu;
+        for (int q = 0; q < 2; ++q)
+            for (int k = 0; k < 4; ++k) {
+                const std::vector<uint32_t> &dir = fine[q][k].dir;
+                for (size_t t = 0; t < dir.size(); ++t)
+                    if (dir[t] - dir[(t >> gs) << gs] > lim) return false;
+            }
+        return true;
+    };
+    while (!form_fits(fmt) || !fine_fits(fmt)) {
         fmt = fmt == 8 && want16 ? 16 : 0;
         size_and_fill(ext.data(), wext.data(), budget, fmt, nd);
     }
@@ -1013,6 +1112,22 @@ void build_hybrid(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vec
             if (!compact || !plan[f].dims[k].rules.empty()) order[f].push_back(&plan[f].dims[k]);
         for (int k = 0; k < 2; ++k)
             if (compact && !coarse[f][k].rules.empty()) order[f].push_back(&coarse[f][k]);
+        if (any_fine)  // positional 4..7 (an empty slot: an empty directory of two buckets)
+            for (int k = 0; k < 4; ++k) {
+                DimBuild &fd = fine[f][k];
+                if (fd.rules.empty()) {
+                    fd.kind = field_kind(k & 1 ? kFSrc : kFDst, f == 1);
+                    fd.kind2 = field_kind(k < 2 ? kFDport : kFSport, f == 1);
+                    fd.rb = 1;
+                    fd.shift = 31;
+                    fd.bits2 = 0;
+                    fd.shift2 = 16;
+                    fd.dir.assign(3, 0);
+                    fd.ents.clear();
+                    fd.max_list = 0;
+                }
+                order[f].push_back(&fd);
+            }
     }
     std::vector<uint32_t> &blob = out.blob;
     FamilyIndex *fi[2] = {&out.idx4, &out.idx6};
@@ -1065,6 +1180,9 @@ void build_hybrid(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vec
             DimInfo &di = fi[f]->dims[k];
             di.kind = d.kind;
             di.shift = d.shift;
+            di.kind2 = d.kind2;
+            di.shift2 = d.shift2;
+            di.bits2 = d.bits2;
             di.n_buckets = 1u << d.rb;
             di.n_rules = static_cast<uint32_t>(d.rules.size());
             di.n_ent = d.ents.size();
@@ -1143,6 +1261,12 @@ bool CompileOptions::from_env(CompileOptions &o, std::string &err) {
     if (set) o.slots2d = static_cast<int>(v);
     if (!env_knob("NFFACL_TUNE_SLOT_COST", 0, 1000, v, set, err)) return false;
     if (set) o.slot_cost = double(v) / 100.0;
+    if (!env_knob("NFFACL_TUNE_FINE_A", 0, 12, v, set, err)) return false;
+    if (set) o.fine_a = static_cast<int>(v);
+    if (!env_knob("NFFACL_TUNE_FINE_P", 1, 8, v, set, err)) return false;
+    if (set) o.fine_p = static_cast<int>(v);
+    if (!env_knob("NFFACL_TUNE_FINE_G", 1, 100, v, set, err)) return false;
+    if (set) o.fine_gain = double(v) / 100.0;
     return true;
 }
 

@@ -82,6 +82,11 @@ struct CompileOptions {
     bool dir16 = true;      // NFFACL_TUNE_DIR16: two-level u16 LDS directories allowed
     bool dir8 = true;       // NFFACL_TUNE_DIR8: two-level u8 LDS directories allowed (HYBRID)
     int uncond = -1;        // NFFACL_TUNE_UNCOND: flat-LDS branch-free entry loads (-1 = policy)
+    // NFFACL_TUNE_FINE_A / _P: fine 2-D address x port slots of the flat-LDS
+    // form (positional slots 4..7), a address bits x p port bits; a = 0: none
+    int fine_a = 0;
+    int fine_p = 4;
+    double fine_gain = 0.5;  // NFFACL_TUNE_FINE_G (1/100): a rule moves below this fraction of its 1-D cover
     bool coarse = false;    // NFFACL_TUNE_COARSE: flat-LDS coarse address slots for short prefixes
                             // (C5 table 7.7 -> 3.7 MB but 0.722 vs 0.649 ms: off; profiles/r2_dir8/coarse/)
     // false (+ `err`) if a set variable is out of range

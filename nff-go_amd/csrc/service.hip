@@ -261,6 +261,15 @@ __global__ void __launch_bounds__(64) k_service(SvcArgs a) {
             const uint32_t first = static_cast<uint32_t>(__builtin_ctzll(m));
             const uint32_t key = __builtin_amdgcn_readlane(c[kSvcChunks - 1].z, first);
             const bool mine = pend && c[kSvcChunks - 1].z == key;
+            if (key == kSvcWithdrawn) {  // the caller gave up: answered, no table read
+                if (mine) {
+                    __hip_atomic_store(resp, uint64_t(tag) << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    done = tag;
+                }
+                pend = pend && !mine;
+                m = ballot(pend);
+                continue;
+            }
             if ((key >> 1) > a.epoch) {
                 // a table uploaded after this launch: its bytes are visible to
                 // a NEW launch (the dispatch invalidates the caches), not
@@ -333,6 +342,172 @@ __global__ void __launch_bounds__(64) k_service(SvcArgs a) {
             group_ticks += wall_clock64() - t_group;
         }
         if (restart) break;
+    }
+    if (lane == 0) {
+        uint64_t *st = a.stats + size_t(blockIdx.x) * kSvcStatWords;
+        const uint64_t v[5] = {n_polls, poll_ticks, n_groups, group_ticks, n_req};
+#pragma unroll
+        for (int i = 0; i < 5; ++i) __hip_atomic_store(st + i, v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+// The burst consumer: one wave per burst mailbox (service.hpp), lane i
+// classifies packet i of the mailbox's request.  Polls as k_service: a hot
+// wave (answered within `hot`) reads its whole mailbox with kSvcBurstLoads
+// coalesced 1 KiB loads per pass (the next pass's loads issued before this
+// pass's request is classified), an idle wave reads only its bell word.  A
+// request is one rule set: no grouping, the descriptor is wave-uniform.
+__global__ void __launch_bounds__(64) k_service_burst(SvcArgs a) {
+    __shared__ FlatScratch<2> W;
+    __shared__ u32x4 img[64 * kSvcBurstLoads];
+    const uint32_t lane = lane_id();
+    const uint32_t mb = blockIdx.x;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(a.box), 0,
+                                                                        static_cast<int>(a.range_bytes), 0x00020000);
+    uint64_t *resp = a.resp + size_t(mb) * kSvcBurstRespWords;
+    // the last tag answered: every answer writes word 0 (n >= 1)
+    uint32_t done = __builtin_amdgcn_readfirstlane(
+        static_cast<uint32_t>(__hip_atomic_load(resp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >> 32));
+    const uint64_t t0 = wall_clock64();
+    uint64_t last = t0, ans_last = t0;  // hot at start: the call that armed us is read whole
+    uint32_t cur_key = 0xFFFFFFFFu, staged_gen = 0xFFFFFFFFu;
+    uint32_t w[kSvcDescDwords];
+#pragma unroll
+    for (uint32_t i = 0; i < kSvcDescDwords; ++i) w[i] = 0;
+    const uint32_t *tab = nullptr;
+    uint64_t n_polls = 0, poll_ticks = 0, n_groups = 0, group_ticks = 0, n_req = 0;
+    const uint32_t box = mb * kSvcBurstBoxBytes;
+    const uint32_t bell = a.box_bytes + mb * 4u;
+    constexpr uint32_t kTailLanes = (kSvcBurstChunks * 16 - (kSvcBurstLoads - 1) * 1024 + 15) / 16;
+    u32x4 nx[kSvcBurstLoads];
+    uint32_t nbell = 0;
+    uint64_t ncw = 0, nt = t0;
+    bool nhot = true;
+    auto issue = [&]() {
+        nt = wall_clock64();
+        nhot = nt - ans_last <= a.hot_ticks;  // wave-uniform
+#pragma unroll
+        for (uint32_t j = 0; j < kSvcBurstLoads; ++j) nx[j] = u32x4{0, 0, 0, 0};
+        nbell = 0;
+        if (nhot) {
+#pragma unroll
+            for (uint32_t j = 0; j < kSvcBurstLoads; ++j)
+                if (j + 1 < kSvcBurstLoads || lane < kTailLanes) nx[j] = ld16_host(rs, box + 1024u * j + 16u * lane);
+        } else if (lane == 0) {
+            nbell = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(bell), 0, 17);
+        }
+        ncw = 0;  // stop | restart << 32
+        if (lane == 0) ncw = __hip_atomic_load(reinterpret_cast<uint64_t *>(a.ctrl), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_SYSTEM);
+    };
+    issue();
+    while (true) {
+        const uint64_t cw = ncw, now = nt;
+        const bool hot = nhot;
+        u32x4 h0 = u32x4{0, 0, 0, 0}, h1 = u32x4{0, 0, 0, 0}, c[kSvcPktChunks];
+        if (hot) {  // the poll issued a pass ago, through LDS: lane i gets packet i's chunks
+#pragma unroll
+            for (uint32_t j = 0; j < kSvcBurstLoads; ++j) img[64u * j + lane] = nx[j];
+            wave_lds_sync();
+            h0 = img[0];
+            h1 = img[1];
+#pragma unroll
+            for (uint32_t j = 0; j < kSvcPktChunks; ++j)
+                c[j] = lane < kSvcBurstMax ? img[kSvcBurstHdrChunks + kSvcPktChunks * lane + j] : u32x4{0, 0, 0, 0};
+            wave_lds_sync();
+        } else {
+            h0.w = __builtin_amdgcn_readfirstlane(nbell);
+#pragma unroll
+            for (uint32_t j = 0; j < kSvcPktChunks; ++j) c[j] = u32x4{0, 0, 0, 0};
+        }
+        if (now - t0 > a.life_ticks) break;
+        issue();  // the next pass's poll, in flight from here
+        if ((__builtin_amdgcn_readlane(static_cast<uint32_t>(cw), 0) |
+             __builtin_amdgcn_readlane(static_cast<uint32_t>(cw >> 32), 0)) != 0u)
+            break;
+        const uint32_t tag = __builtin_amdgcn_readfirstlane(h0.w);
+        const uint64_t t_data = wall_clock64();
+        ++n_polls;
+        poll_ticks += t_data - now;
+        if (tag == done) {
+            if (now - last > a.idle_ticks) break;
+            continue;
+        }
+        last = now;
+        if (!hot) {  // a new tag on the bell: the request is read whole from the poll after next
+            ans_last = now;
+            continue;
+        }
+        // complete when every chunk of the header and of packets 0..n-1 carries the tag
+        const uint32_t n = __builtin_amdgcn_readfirstlane(h1.x);
+        const bool live = lane < n;
+        bool torn = h1.w != tag || n == 0u || n > kSvcBurstMax;
+#pragma unroll
+        for (uint32_t j = 0; j < kSvcPktChunks; ++j) torn = torn || (live && c[j].w != tag);
+        if (ballot(torn)) continue;  // raced the host's stores: the next poll has it
+        const uint64_t t_group = wall_clock64();
+        const uint32_t key = __builtin_amdgcn_readfirstlane(h0.z);
+        if (key == kSvcWithdrawn) {  // the caller gave up: answered, no table read
+            if (live) __hip_atomic_store(resp + lane, uint64_t(tag) << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            done = tag;
+            continue;
+        }
+        if ((key >> 1) > a.epoch) {  // a table uploaded after this launch (see k_service)
+            if (lane == 0) __hip_atomic_store(a.ctrl + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            break;
+        }
+        if (key != cur_key) {
+            // (readfirstlane returns int: through uint32_t, or the low word sign-extends)
+            const uint64_t lo = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(h0.x));
+            const uint64_t hi = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(h0.y));
+            const u32x4 *dq = reinterpret_cast<const u32x4 *>(hi << 32 | lo);
+            u32x4 q[kSvcDescDwords / 4];
+#pragma unroll
+            for (uint32_t i = 0; i < kSvcDescDwords / 4; ++i) q[i] = dq[i];
+#pragma unroll
+            for (uint32_t i = 0; i < kSvcDescDwords / 4; ++i) {
+                w[4 * i + 0] = __builtin_amdgcn_readfirstlane(q[i].x);
+                w[4 * i + 1] = __builtin_amdgcn_readfirstlane(q[i].y);
+                w[4 * i + 2] = __builtin_amdgcn_readfirstlane(q[i].z);
+                w[4 * i + 3] = __builtin_amdgcn_readfirstlane(q[i].w);
+            }
+            tab = reinterpret_cast<const uint32_t *>(hi << 32 | lo) - w[2];
+            cur_key = key;
+        }
+        const bool staged = w[0] == kSvcIndexed && w[2] <= a.lds_dwords;
+        if (staged && staged_gen != (key >> 1)) {
+            const u32x4 *src = reinterpret_cast<const u32x4 *>(tab);
+            u32x4 *dst = reinterpret_cast<u32x4 *>(lds_tab);
+            for (uint32_t i = lane; i < (w[2] + 3u) / 4u; i += 64u) dst[i] = src[i];
+            wave_lds_sync();
+            staged_gen = key >> 1;
+        }
+        uint32_t full[3 * kSvcPktChunks], d[16];
+#pragma unroll
+        for (uint32_t j = 0; j < kSvcPktChunks; ++j) {
+            full[3 * j + 0] = c[j].x;
+            full[3 * j + 1] = c[j].y;
+            full[3 * j + 2] = c[j].z;
+        }
+#pragma unroll
+        for (int k = 0; k < 16; ++k) d[k] = full[k];
+        Fields f;
+        parse_fields<true>(d, live, f, [&](uint32_t k, uint32_t &lo, uint32_t &hi) {
+            lo = 0;
+            hi = 0;
+#pragma unroll
+            for (uint32_t j = 0; j < 3 * kSvcPktChunks; ++j) {
+                lo = k == j ? full[j] : lo;
+                hi = k + 1 == j ? full[j] : hi;
+            }
+        }, key & 1u ? uint32_t(NFFACL_PARSE_VLAN) : 0u);
+        const uint32_t port = svc_classify(w, tab, f, W, lane, a.ctrl + 2, staged);
+        if (live) __hip_atomic_store(resp + lane, uint64_t(tag) << 32 | port, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        done = tag;
+        ans_last = now;
+        ++n_groups;
+        n_req += n;
+        group_ticks += wall_clock64() - t_group;
     }
     if (lane == 0) {
         uint64_t *st = a.stats + size_t(blockIdx.x) * kSvcStatWords;
@@ -471,6 +646,13 @@ struct nffacl_service {
     int device = 0;
     uint32_t id = 0;  // process-unique: keys the callers' thread-local mailbox choice
     uint32_t n_mb = 0;
+    // burst service (nffacl_service_create_burst): burst mailboxes, one
+    // consumer wave each (k_service_burst); else scalar mailboxes, 8 per wave
+    bool burst = false;
+    uint32_t box_stride = kSvcBoxBytes;       // bytes per mailbox
+    uint32_t resp_stride = kSvcRespStride;    // u64 response words per mailbox
+    // a call waits this long for its answer, re-posts once, waits again, and
+    // then withdraws its request (NFFACL_TUNE_SVC_TIMEOUT_US)
     uint64_t timeout_us = 1000000;
     // After posting, a caller sleeps through most of the round trip instead
     // of spinning it once the callers outnumber the CPUs this process may use
@@ -499,7 +681,9 @@ struct nffacl_service {
     std::condition_variable cv;
     bool kick = false, stop = false;
     std::thread armer;
-    std::atomic<uint64_t> launches{0}, requests{0}, timeouts{0};
+    std::atomic<uint64_t> launches{0}, requests{0}, timeouts{0}, retries{0};
+    std::atomic<bool> paused{false};  // nffacl_service_pause: no consumer launches
+    uint32_t waves() const { return burst ? n_mb : n_mb / kSvcMbPerWave; }
 };
 
 namespace {
@@ -526,13 +710,14 @@ void stop_all_at_exit() {
     for (nffacl_service *s : *g_live) stop_kernel(s);
 }
 
+// the tag of a mailbox's latest request (scalar: chunk 7, burst: chunk 0)
 uint32_t box_tag(const nffacl_service *s, uint32_t i) {
-    return __atomic_load_n(reinterpret_cast<const uint32_t *>(s->h_box + size_t(i) * kSvcBoxBytes + kSvcBoxBytes - 4),
-                           __ATOMIC_ACQUIRE);
+    const size_t at = size_t(i) * s->box_stride + (s->burst ? 12 : kSvcBoxBytes - 4);
+    return __atomic_load_n(reinterpret_cast<const uint32_t *>(s->h_box + at), __ATOMIC_ACQUIRE);
 }
 
 uint32_t resp_tag(const nffacl_service *s, uint32_t i) {
-    return static_cast<uint32_t>(__atomic_load_n(s->h_resp + size_t(i) * kSvcRespStride, __ATOMIC_ACQUIRE) >> 32);
+    return static_cast<uint32_t>(__atomic_load_n(s->h_resp + size_t(i) * s->resp_stride, __ATOMIC_ACQUIRE) >> 32);
 }
 
 bool any_pending(const nffacl_service *s) {
@@ -549,13 +734,18 @@ void armer_main(nffacl_service *s) {
         s->cv.wait(lk, [&] { return s->kick || s->stop; });
         if (s->stop) break;
         s->kick = false;
+        if (s->paused.load(std::memory_order_acquire)) continue;  // nffacl_service_pause: re-armed by the resume
         lk.unlock();
         s->running.store(true, std::memory_order_seq_cst);
         __atomic_store_n(&s->h_ctrl[1], 0u, __ATOMIC_SEQ_CST);
         s->args.epoch = table_epoch();  // every table of this generation or older is in HBM
         s->launches.fetch_add(1, std::memory_order_relaxed);  // (before the launch: its calls may return first)
-        hipLaunchKernelGGL(dev::k_service, dim3(s->n_mb / kSvcMbPerWave), dim3(64), size_t(s->args.lds_dwords) * 4,
-                           s->stream, s->args);
+        if (s->burst)
+            hipLaunchKernelGGL(dev::k_service_burst, dim3(s->waves()), dim3(64), size_t(s->args.lds_dwords) * 4,
+                               s->stream, s->args);
+        else
+            hipLaunchKernelGGL(dev::k_service, dim3(s->waves()), dim3(64), size_t(s->args.lds_dwords) * 4,
+                               s->stream, s->args);
         hipError_t e = hipGetLastError();
         if (e == hipSuccess) e = hipEventRecord(s->done, s->stream);
         if (e == hipSuccess) {
@@ -568,7 +758,7 @@ void armer_main(nffacl_service *s) {
         }
         s->running.store(false, std::memory_order_seq_cst);
         lk.lock();
-        for (uint32_t wv = 0; wv < s->n_mb / kSvcMbPerWave; ++wv)
+        for (uint32_t wv = 0; wv < s->waves(); ++wv)
             for (uint32_t i = 0; i < kSvcStatWords; ++i) {
                 s->acc[i] += __atomic_load_n(&s->h_stats[wv * kSvcStatWords + i], __ATOMIC_ACQUIRE);
                 __atomic_store_n(&s->h_stats[wv * kSvcStatWords + i], 0ull, __ATOMIC_RELAXED);
@@ -604,8 +794,8 @@ uint32_t my_mailbox(nffacl_service *s) {
     // consecutive threads on different waves: each wave polls and classifies
     // for few callers, the waves of busy mailboxes in parallel
     const uint32_t k = s->next_mb.fetch_add(1, std::memory_order_relaxed) % s->n_mb;
-    const uint32_t waves = s->n_mb / kSvcMbPerWave;
-    c.mb = (k % waves) * kSvcMbPerWave + k / waves;
+    const uint32_t waves = s->waves();
+    c.mb = s->burst ? k : (k % waves) * kSvcMbPerWave + k / waves;
     return c.mb;
 }
 
@@ -707,20 +897,25 @@ int nffacl_rules_prepare(const nffacl_rules *rules, int hip_device) {
     return st;
 }
 
-int nffacl_service_create(int hip_device, uint32_t mailboxes, uint32_t idle_us, nffacl_service **out) {
+}  // extern "C"
+
+namespace {
+
+int service_create(int hip_device, uint32_t mailboxes, uint32_t idle_us, bool burst, nffacl_service **out) {
     if (!out) return NFFACL_ERR_INVALID_ARG;
     *out = nullptr;
-    if (mailboxes == 0) {  // default: 128 (NFFACL_TUNE_SVC_MAILBOXES)
+    if (mailboxes == 0) {  // default: 128 scalar / 64 burst mailboxes (NFFACL_TUNE_SVC_MAILBOXES)
         long v = 0;
         bool set = false;
         std::string err;
-        if (!env_knob("NFFACL_TUNE_SVC_MAILBOXES", 64, 4096, v, set, err)) {
+        if (!env_knob("NFFACL_TUNE_SVC_MAILBOXES", burst ? 1 : 64, 4096, v, set, err)) {
             set_last_error(err);
             return NFFACL_ERR_INVALID_ARG;
         }
-        mailboxes = set ? static_cast<uint32_t>(v) : 128u;
+        mailboxes = set ? static_cast<uint32_t>(v) : burst ? 64u : 128u;
     }
-    if (mailboxes % 64 != 0 || mailboxes > 4096 || idle_us > 10000000u) return NFFACL_ERR_INVALID_ARG;
+    if ((!burst && mailboxes % 64 != 0) || mailboxes > (burst ? 1024u : 4096u) || idle_us > 10000000u)
+        return NFFACL_ERR_INVALID_ARG;
     if (idle_us == 0) idle_us = 2000;
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
@@ -740,11 +935,14 @@ int nffacl_service_create(int hip_device, uint32_t mailboxes, uint32_t idle_us, 
     s->device = hip_device;
     s->id = g_next_id.fetch_add(1, std::memory_order_relaxed);
     s->n_mb = mailboxes;
+    s->burst = burst;
+    s->box_stride = burst ? kSvcBurstBoxBytes : kSvcBoxBytes;
+    s->resp_stride = burst ? kSvcBurstRespWords : kSvcRespStride;
     s->mbx.reset(new (std::nothrow) MailboxState[mailboxes]);
-    const size_t box_bytes = size_t(mailboxes) * kSvcBoxBytes;
-    const size_t bell_bytes = size_t(mailboxes) * 4;  // a multiple of 256
-    const size_t resp_bytes = size_t(mailboxes) * kSvcRespStride * 8;
-    const size_t stat_bytes = size_t(mailboxes / kSvcMbPerWave) * kSvcStatWords * 8;
+    const size_t box_bytes = size_t(mailboxes) * s->box_stride;
+    const size_t bell_bytes = (size_t(mailboxes) * 4 + 255) / 256 * 256;
+    const size_t resp_bytes = size_t(mailboxes) * s->resp_stride * 8;
+    const size_t stat_bytes = size_t(s->waves()) * kSvcStatWords * 8;
     const size_t bytes = box_bytes + bell_bytes + resp_bytes + 64 + stat_bytes;
     hipError_t e = s->mbx ? hipSuccess : hipErrorOutOfMemory;
     if (e == hipSuccess)
@@ -802,11 +1000,19 @@ int nffacl_service_create(int hip_device, uint32_t mailboxes, uint32_t idle_us, 
             return NFFACL_ERR_INVALID_ARG;
         }
         if (set) s->sleep_ns = static_cast<int32_t>(v);
+        if (!env_knob("NFFACL_TUNE_SVC_TIMEOUT_US", 1000, 10000000, v, set, err)) {
+            set_last_error(err);
+            release_service(s);
+            return NFFACL_ERR_INVALID_ARG;
+        }
+        if (set) s->timeout_us = static_cast<uint64_t>(v);
         s->cpus = cpu_budget();
     }
+    const void *kern = burst ? reinterpret_cast<const void *>(dev::k_service_burst)
+                             : reinterpret_cast<const void *>(dev::k_service);
     if (s->args.lds_dwords &&
-        hipFuncSetAttribute(reinterpret_cast<const void *>(dev::k_service), hipFuncAttributeMaxDynamicSharedMemorySize,
-                            static_cast<int>(s->args.lds_dwords * 4)) != hipSuccess) {
+        hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(s->args.lds_dwords * 4)) !=
+            hipSuccess) {
         (void)hipGetLastError();
         s->args.lds_dwords = 0;
     }
@@ -823,9 +1029,130 @@ int nffacl_service_create(int hip_device, uint32_t mailboxes, uint32_t idle_us, 
     return NFFACL_OK;
 }
 
+// One request through mailbox `mb` (its lock held by the caller): `post(tag,
+// key)` writes the request's chunks with `tag` and the table key (the
+// descriptor's generation, or kSvcWithdrawn), `answered(tag)` tells whether
+// every response word of the request carries `tag`.
+//
+// Failure policy (the reference's verdict path never errors, acl.go:522-565):
+// a caller that has no answer after timeout_us re-posts its request under a
+// new tag and re-arms the consumer (counted in `retries`); if that one is not
+// answered within timeout_us either, it WITHDRAWS the request — rewrites it
+// with the key kSvcWithdrawn, which the consumer answers without reading any
+// table — records the table's use on the consumer's stream (the table's
+// retirement then waits for the consumer launch that may still hold the old
+// request) and returns NFFACL_ERR_TIMEOUT (counted in `timeouts`); the
+// caller's verdict is then 0 (reject), the value l3ACL gives a packet no rule
+// matches.  Later calls are served normally once the consumer runs again.
+template <class Post, class Answered>
+int post_and_wait(nffacl_service *s, MailboxState &m, uint32_t mb, DevTable *t, uint32_t key, Post post,
+                  Answered answered) {
+    for (int attempt = 0;; ++attempt) {
+        const uint32_t tag = ++m.seq;
+        post(tag, key);
+        __atomic_store_n(&s->h_bell[mb], tag, __ATOMIC_RELEASE);  // idle waves watch the bells
+        std::atomic_thread_fence(std::memory_order_seq_cst);      // request visible before `running` is read
+        if (!s->running.load(std::memory_order_seq_cst)) kick(s);
+        // sleep first?  (adaptive: only with more callers than CPUs)
+        const bool adaptive = s->sleep_ns < 0 && s->next_mb.load(std::memory_order_relaxed) > s->cpus;
+        const uint32_t nap = attempt ? 0u : adaptive ? m.nap : s->sleep_ns > 0 ? static_cast<uint32_t>(s->sleep_ns) : 0u;
+        Clock::time_point woke{};
+        if (nap) {
+            thread_local bool slack = false;
+            if (!slack) {  // hrtimer wake-ups at the requested time (default slack: 50 us)
+                (void)prctl(PR_SET_TIMERSLACK, 1UL, 0, 0, 0);
+                slack = true;
+            }
+            const timespec ts{0, static_cast<long>(nap)};
+            (void)nanosleep(&ts, nullptr);
+        }
+        if (adaptive) woke = Clock::now();
+        bool spun = false;
+        uint32_t spins = 0;
+        Clock::time_point t0{};
+        int st = NFFACL_OK;
+        while (true) {
+            if (answered(tag)) break;
+            spun = true;
+            _mm_pause();
+            if ((++spins & 1023u) == 0) {
+                const Clock::time_point now = Clock::now();
+                if (spins == 1024) t0 = now;
+                if ((st = s->error.load(std::memory_order_acquire)) != NFFACL_OK) break;
+                if (!s->running.load(std::memory_order_seq_cst)) kick(s);
+                if (now - t0 > std::chrono::microseconds(s->timeout_us)) {
+                    st = NFFACL_ERR_TIMEOUT;
+                    break;
+                }
+            }
+        }
+        if (st == NFFACL_OK) {
+            if (adaptive && attempt == 0) {
+                // Aim the nap short of the answer (an oversleep costs the whole
+                // wake-up time, a short spin only CPU): an answer already there
+                // at wake-up cuts it by a quarter; a spin after waking lengthens
+                // it by a quarter of the spin beyond 300 ns, at most 500 ns per
+                // call (a caller preempted while spinning must not drag it up).
+                if (!spun) {
+                    m.nap -= std::max(m.nap / 4u, std::min(m.nap, 100u));
+                } else {
+                    const int64_t spin =
+                        std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - woke).count();
+                    if (spin > 300)
+                        m.nap = std::min(m.nap + static_cast<uint32_t>(std::min<int64_t>((spin - 300) / 4, 500)), 20000u);
+                }
+            }
+            return NFFACL_OK;
+        }
+        if (st != NFFACL_ERR_TIMEOUT) return st;  // the consumer failed (sticky HIP error)
+        if (attempt == 0) {
+            s->retries.fetch_add(1, std::memory_order_relaxed);
+            continue;  // re-post under a new tag, re-arm
+        }
+        // withdraw: same tag, no table; the table's retirement waits for the
+        // consumer launch that may still hold the request
+        post(tag, kSvcWithdrawn);
+        std::atomic_thread_fence(std::memory_order_seq_cst);
+        (void)t->note_use(s->stream);
+        s->timeouts.fetch_add(1, std::memory_order_relaxed);
+        set_last_error("service: no answer within the timeout (twice); request withdrawn, verdict 0");
+        return NFFACL_ERR_TIMEOUT;
+    }
+}
+
+// One packet as chunk payload (service.hpp): bytes [0, min(len, 80)), zero after.
+inline void packet_chunks(const uint8_t *frame, uint32_t len, uint32_t tag, __m128i *dst) {
+    alignas(16) uint8_t bytes[kSvcPktChunks * 12] = {0};
+    const uint32_t n = std::min(len, kSvcSlot);
+    if (n) std::memcpy(bytes, frame, n);
+    alignas(16) uint32_t c[4];
+    for (uint32_t j = 0; j < kSvcPktChunks; ++j) {
+        std::memcpy(c, bytes + 12 * j, 12);
+        c[3] = tag;
+        _mm_store_si128(dst + j, _mm_load_si128(reinterpret_cast<const __m128i *>(c)));
+    }
+}
+
+inline void store_chunk(__m128i *dst, uint32_t x, uint32_t y, uint32_t z, uint32_t w) {
+    _mm_store_si128(dst, _mm_set_epi32(static_cast<int>(w), static_cast<int>(z), static_cast<int>(y), static_cast<int>(x)));
+}
+
+}  // namespace
+
+extern "C" {
+
+int nffacl_service_create(int hip_device, uint32_t mailboxes, uint32_t idle_us, nffacl_service **out) {
+    return service_create(hip_device, mailboxes, idle_us, false, out);
+}
+
+int nffacl_service_create_burst(int hip_device, uint32_t mailboxes, uint32_t idle_us, nffacl_service **out) {
+    return service_create(hip_device, mailboxes, idle_us, true, out);
+}
+
 int nffacl_service_classify(nffacl_service *s, const nffacl_rules *rules, const uint8_t *frame, uint32_t len,
                             uint32_t flags, uint32_t *port) {
     if (!s || !rules || (!frame && len) || (flags & ~uint32_t(NFFACL_PARSE_VLAN)) != 0) return NFFACL_ERR_INVALID_ARG;
+    if (s->burst) return nffacl_service_classify_burst(s, rules, &frame, &len, 1, flags, port);
     auto failed = [s](int st) {
         std::lock_guard<std::mutex> g(s->mu);
         set_last_error(s->error_msg);
@@ -839,90 +1166,114 @@ int nffacl_service_classify(nffacl_service *s, const nffacl_rules *rules, const 
     const uint32_t mb = my_mailbox(s);
     MailboxState &m = s->mbx[mb];
     while (m.lock.exchange(1, std::memory_order_acquire) != 0) _mm_pause();
-    const uint32_t tag = ++m.seq;
-    // the eight chunks (service.hpp): packet bytes, 12 per chunk, + tag
-    alignas(16) uint8_t bytes[kSvcPktChunks * 12] = {0};
-    const uint32_t n = std::min(len, kSvcSlot);
-    if (n) std::memcpy(bytes, frame, n);
-    alignas(16) uint32_t c[kSvcChunks * 4];
-    for (uint32_t j = 0; j < kSvcPktChunks; ++j) {
-        std::memcpy(&c[4 * j], bytes + 12 * j, 12);
-        c[4 * j + 3] = tag;
-    }
-    const uint64_t desc = reinterpret_cast<uint64_t>(t->d_desc);
-    c[28] = static_cast<uint32_t>(desc);
-    c[29] = static_cast<uint32_t>(desc >> 32);
-    c[30] = t->gen << 1 | (flags & NFFACL_PARSE_VLAN ? 1u : 0u);
-    c[31] = tag;
     __m128i *dst = reinterpret_cast<__m128i *>(s->h_box + size_t(mb) * kSvcBoxBytes);
-    for (uint32_t j = 0; j < kSvcChunks; ++j)  // ascending: the tag chunk last (x86 stores stay in order)
-        _mm_store_si128(dst + j, _mm_load_si128(reinterpret_cast<const __m128i *>(&c[4 * j])));
-    __atomic_store_n(&s->h_bell[mb], tag, __ATOMIC_RELEASE);  // idle waves watch the bells
-    std::atomic_thread_fence(std::memory_order_seq_cst);  // request visible before `running` is read
-    if (!s->running.load(std::memory_order_seq_cst)) kick(s);
+    const uint64_t desc = reinterpret_cast<uint64_t>(t->d_desc);
+    const uint32_t live_key = t->gen << 1 | (flags & NFFACL_PARSE_VLAN ? 1u : 0u);
     const uint64_t *r = s->h_resp + size_t(mb) * kSvcRespStride;
-    // sleep first?  (adaptive: only with more callers than CPUs)
-    const bool adaptive = s->sleep_ns < 0 && s->next_mb.load(std::memory_order_relaxed) > s->cpus;
-    const uint32_t nap = adaptive ? m.nap : s->sleep_ns > 0 ? static_cast<uint32_t>(s->sleep_ns) : 0u;
-    Clock::time_point woke{};
-    if (nap) {
-        thread_local bool slack = false;
-        if (!slack) {  // hrtimer wake-ups at the requested time (default slack: 50 us)
-            (void)prctl(PR_SET_TIMERSLACK, 1UL, 0, 0, 0);
-            slack = true;
-        }
-        const timespec ts{0, static_cast<long>(nap)};
-        (void)nanosleep(&ts, nullptr);
-    }
-    if (adaptive) woke = Clock::now();
-    bool spun = false;
     uint64_t v = 0;
-    uint32_t spins = 0;
-    Clock::time_point t0{};
-    st = NFFACL_OK;
-    while (true) {
-        v = __atomic_load_n(r, __ATOMIC_ACQUIRE);
-        if (static_cast<uint32_t>(v >> 32) == tag) break;
-        spun = true;
-        _mm_pause();
-        if ((++spins & 1023u) == 0) {
-            const Clock::time_point now = Clock::now();
-            if (spins == 1024) t0 = now;
-            if ((st = s->error.load(std::memory_order_acquire)) != NFFACL_OK) break;
-            if (!s->running.load(std::memory_order_seq_cst)) kick(s);
-            if (now - t0 > std::chrono::microseconds(s->timeout_us)) {
-                s->timeouts.fetch_add(1, std::memory_order_relaxed);
-                set_last_error("service: no answer within the timeout");
-                st = NFFACL_ERR_TIMEOUT;
-                break;
-            }
-        }
-    }
-    if (adaptive && st == NFFACL_OK) {
-        // Aim the nap short of the answer (an oversleep costs the whole
-        // wake-up time, a short spin only CPU): an answer already there at
-        // wake-up cuts it by a quarter; a spin after waking lengthens it by a
-        // quarter of the spin beyond 300 ns, at most 500 ns per call (a caller
-        // preempted while spinning must not drag it up).
-        if (!spun) {
-            m.nap -= std::max(m.nap / 4u, std::min(m.nap, 100u));
-        } else {
-            const int64_t spin = std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - woke).count();
-            if (spin > 300) m.nap = std::min(m.nap + static_cast<uint32_t>(std::min<int64_t>((spin - 300) / 4, 500)),
-                                             20000u);
-        }
-    }
+    st = post_and_wait(
+        s, m, mb, t, live_key,
+        [&](uint32_t tag, uint32_t key) {
+            // the eight chunks (service.hpp), ascending: the tag chunk last (x86 stores stay in order)
+            packet_chunks(frame, len, tag, dst);
+            if (key == kSvcWithdrawn) store_chunk(dst + kSvcPktChunks, 0, 0, key, tag);
+            else store_chunk(dst + kSvcPktChunks, static_cast<uint32_t>(desc), static_cast<uint32_t>(desc >> 32), key, tag);
+        },
+        [&](uint32_t tag) {
+            v = __atomic_load_n(r, __ATOMIC_ACQUIRE);
+            return static_cast<uint32_t>(v >> 32) == tag;
+        });
     m.lock.store(0, std::memory_order_release);
     if (st == NFFACL_ERR_HIP) return failed(st);
+    if (st == NFFACL_ERR_TIMEOUT) {
+        if (port) *port = 0;
+        return st;
+    }
     if (st != NFFACL_OK) return st;
     s->requests.fetch_add(1, std::memory_order_relaxed);
     if (port) *port = static_cast<uint32_t>(v);
     return NFFACL_OK;
 }
 
+int nffacl_service_classify_burst(nffacl_service *s, const nffacl_rules *rules, const uint8_t *const *frames,
+                                  const uint32_t *lens, uint32_t n, uint32_t flags, uint32_t *ports) {
+    if (!s || !rules || !s->burst || n > kSvcBurstMax || (n && (!frames || !ports)) ||
+        (flags & ~uint32_t(NFFACL_PARSE_VLAN)) != 0)
+        return NFFACL_ERR_INVALID_ARG;
+    if (n == 0) return NFFACL_OK;
+    for (uint32_t i = 0; i < n; ++i)
+        if (!frames[i] && (!lens || lens[i])) return NFFACL_ERR_INVALID_ARG;
+    auto failed = [s](int st) {
+        std::lock_guard<std::mutex> g(s->mu);
+        set_last_error(s->error_msg);
+        return st;
+    };
+    int st = s->error.load(std::memory_order_acquire);
+    if (st != NFFACL_OK) return failed(st);
+    DevTable *t = rules_table(rules, s->device, st);
+    if (!t) return st;
+    if (t->svc_kind == kSvcNone) return NFFACL_ERR_UNSUPPORTED;
+    const uint32_t mb = my_mailbox(s);
+    MailboxState &m = s->mbx[mb];
+    while (m.lock.exchange(1, std::memory_order_acquire) != 0) _mm_pause();
+    __m128i *dst = reinterpret_cast<__m128i *>(s->h_box + size_t(mb) * kSvcBurstBoxBytes);
+    const uint64_t desc = reinterpret_cast<uint64_t>(t->d_desc);
+    const uint32_t live_key = t->gen << 1 | (flags & NFFACL_PARSE_VLAN ? 1u : 0u);
+    const uint64_t *r = s->h_resp + size_t(mb) * kSvcBurstRespWords;
+    st = post_and_wait(
+        s, m, mb, t, live_key,
+        [&](uint32_t tag, uint32_t key) {
+            const bool wd = key == kSvcWithdrawn;
+            const uint32_t cnt = wd ? 1u : n;
+            for (uint32_t i = 0; i < cnt; ++i)
+                packet_chunks(wd ? nullptr : frames[i], wd ? 0u : lens ? lens[i] : kSvcSlot, tag,
+                              dst + kSvcBurstHdrChunks + kSvcPktChunks * i);
+            store_chunk(dst + 1, cnt, 0, 0, tag);
+            if (wd) store_chunk(dst, 0, 0, key, tag);
+            else store_chunk(dst, static_cast<uint32_t>(desc), static_cast<uint32_t>(desc >> 32), key, tag);
+        },
+        [&](uint32_t tag) {
+            for (uint32_t i = n; i-- > 0;)  // (the words arrive in any order)
+                if (static_cast<uint32_t>(__atomic_load_n(r + i, __ATOMIC_ACQUIRE) >> 32) != tag) return false;
+            return true;
+        });
+    m.lock.store(0, std::memory_order_release);
+    if (st == NFFACL_ERR_HIP) return failed(st);
+    if (st == NFFACL_ERR_TIMEOUT) {
+        std::memset(ports, 0, size_t(n) * 4);
+        return st;
+    }
+    if (st != NFFACL_OK) return st;
+    for (uint32_t i = 0; i < n; ++i) ports[i] = static_cast<uint32_t>(__atomic_load_n(r + i, __ATOMIC_RELAXED));
+    s->requests.fetch_add(n, std::memory_order_relaxed);
+    return NFFACL_OK;
+}
+
+int nffacl_service_pause(nffacl_service *s, int paused) {
+    if (!s) return NFFACL_ERR_INVALID_ARG;
+    if (paused) {
+        s->paused.store(true, std::memory_order_release);
+        __atomic_store_n(s->h_ctrl, 1u, __ATOMIC_RELEASE);  // the resident consumer leaves
+        return NFFACL_OK;
+    }
+    {
+        std::lock_guard<std::mutex> g(s->mu);
+        if (s->stop) return NFFACL_ERR_INVALID_ARG;
+        s->paused.store(false, std::memory_order_release);
+    }
+    // the consumer of the pause has left once `running` drops; then clear the stop word and re-arm
+    const auto limit = Clock::now() + std::chrono::seconds(2);
+    while (s->running.load(std::memory_order_seq_cst) && Clock::now() < limit) std::this_thread::yield();
+    if (s->running.load(std::memory_order_seq_cst)) return NFFACL_ERR_TIMEOUT;
+    __atomic_store_n(s->h_ctrl, 0u, __ATOMIC_RELEASE);
+    kick(s);
+    return NFFACL_OK;
+}
+
 int nffacl_service_get_stats(nffacl_service *s, nffacl_service_stats *out) {
     if (!s || !out) return NFFACL_ERR_INVALID_ARG;
     out->launches = s->launches.load(std::memory_order_relaxed);
+    out->retries = s->retries.load(std::memory_order_relaxed);
     out->requests = s->requests.load(std::memory_order_relaxed);
     out->timeouts = s->timeouts.load(std::memory_order_relaxed);
     out->running = s->running.load(std::memory_order_relaxed) ? 1u : 0u;

@@ -39,6 +39,30 @@ constexpr uint32_t kSvcStatWords = 8;      // per-wave counters: polls, poll tic
 constexpr uint32_t kSvcLdsDwords = 16384;  // INDEXED tables up to 64 KiB are walked from LDS
 constexpr uint32_t kSvcMbPerWave = 8;      // mailboxes per consumer wave (a multiple of 8: 1 KiB per poll load)
 
+// A request withdrawn by a caller that gave up (service.hip, the timeout
+// policy): the chunk-7 key the consumer answers with port 0 without reading
+// any table (the caller may free its rules as soon as it returns).
+constexpr uint32_t kSvcWithdrawn = 0xFFFFFFFEu;
+
+// ---- burst mailbox (host memory, one per calling thread of a burst service) --
+//
+// The VectorSeparateFunction shape (flow/flow.go:131, 1487-1520): a clone's
+// whole burst of up to kSvcBurstMax packets in one request, one answer per
+// packet.  16-byte chunks as above, each carrying the tag in its last dword:
+//   chunk 0:          {desc address lo, desc address hi, generation << 1 | vlan, tag}
+//   chunk 1:          {packets n (1..kSvcBurstMax), 0, 0, tag}
+//   chunk 2 + 7i + j: packet i bytes [12j, 12j + 12) (as the scalar mailbox)
+// One consumer wave per mailbox: lane i < n classifies packet i and writes
+// {tag, port} to its own 8-byte response word (kSvcBurstRespWords per
+// mailbox); the caller waits until all n words carry its tag.
+constexpr uint32_t kSvcBurstMax = 32;
+constexpr uint32_t kSvcBurstHdrChunks = 2;
+constexpr uint32_t kSvcBurstChunks = kSvcBurstHdrChunks + kSvcBurstMax * kSvcPktChunks;  // 226
+constexpr uint32_t kSvcBurstBoxBytes = 4096;  // 4 coalesced 1 KiB poll loads (3 616 bytes used)
+constexpr uint32_t kSvcBurstLoads = (kSvcBurstChunks * 16 + 1023) / 1024;
+constexpr uint32_t kSvcBurstRespWords = kSvcBurstMax;  // 256 B: four lines per mailbox
+static_assert(kSvcBurstChunks * 16 <= kSvcBurstBoxBytes, "burst mailbox");
+
 // ---- table descriptor (device memory, after each table's blob) ---------------
 //
 // What the consumer needs to walk a table, read once per table generation.

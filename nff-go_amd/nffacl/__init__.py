@@ -117,8 +117,13 @@ _l2_classify_device = _sig("nffacl_l2_classify_device", _i, _vp, _vp, _u32, _u64
 _l2_classify_frames = _sig("nffacl_l2_classify_frames_device", _i, _vp, _vp, _vp, _u64, _vp, _vp, _vp)
 _l2_classify_host = _sig("nffacl_l2_classify_host", _i, _vp, _vp, _u32, _u64, _vp, _vp)
 class Ticket(ctypes.Structure):
+    """nffacl_ticket.  `rules` (Python side only) holds the burst's L3Rules
+    until the ticket is waited for: the header requires the rule set to
+    outlive the wait, and an L3Rules collected before it would free the
+    table its batch reads."""
     _fields_ = [("seq", ctypes.c_uint64), ("buf", ctypes.c_uint32), ("off", ctypes.c_uint32),
                 ("n", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+    rules = None
 
 
 class BatcherStats(ctypes.Structure):
@@ -141,7 +146,7 @@ class ServiceStats(ctypes.Structure):
     _fields_ = [("launches", ctypes.c_uint64), ("requests", ctypes.c_uint64), ("timeouts", ctypes.c_uint64),
                 ("running", ctypes.c_uint64), ("table_oob", ctypes.c_uint64), ("polls", ctypes.c_uint64),
                 ("poll_ns", ctypes.c_double), ("groups", ctypes.c_uint64), ("group_ns", ctypes.c_double),
-                ("answered", ctypes.c_uint64)]
+                ("answered", ctypes.c_uint64), ("retries", ctypes.c_uint64)]
 
 
 _rules_prepare = _sig("nffacl_rules_prepare", _i, _vp, _i)
@@ -149,6 +154,9 @@ _local_device = _sig("nffacl_local_device", _i)
 _device_numa_node = _sig("nffacl_device_numa_node", _i, _i)
 _service_create = _sig("nffacl_service_create", _i, _i, _u32, _u32, _pp)
 _service_classify = _sig("nffacl_service_classify", _i, _vp, _vp, _vp, _u32, _u32, ctypes.POINTER(_u32))
+_service_create_burst = _sig("nffacl_service_create_burst", _i, _i, _u32, _u32, _pp)
+_service_classify_burst = _sig("nffacl_service_classify_burst", _i, _vp, _vp, _vp, _vp, _u32, _u32, _vp)
+_service_pause = _sig("nffacl_service_pause", _i, _vp, _i)
 _service_stats = _sig("nffacl_service_get_stats", _i, _vp, ctypes.POINTER(ServiceStats))
 _service_destroy = _sig("nffacl_service_destroy", None, _vp)
 _strerror = _sig("nffacl_strerror", ctypes.c_char_p, _i)
@@ -175,7 +183,8 @@ EXPORTED_SYMBOLS = [
     "nffacl_batcher_create_device", "nffacl_batcher_submit_rules", "nffacl_batcher_classify_rules",
     "nffacl_batcher_wait_timeout", "nffacl_local_device", "nffacl_device_numa_node",
     "nffacl_rules_prepare", "nffacl_service_create", "nffacl_service_classify", "nffacl_service_get_stats",
-    "nffacl_service_destroy",
+    "nffacl_service_destroy", "nffacl_service_create_burst", "nffacl_service_classify_burst",
+    "nffacl_service_pause",
 ]
 
 
@@ -479,6 +488,7 @@ class Batcher:
             st = _batcher_submit_rules(self._h, rules.handle, ptrs.ctypes.data, lp, len(ptrs), ctypes.byref(t))
         if st != OK:
             _raise(st, "nffacl_batcher_submit")
+        t.rules = rules  # alive until wait() has collected the burst
         return t
 
     def wait(self, t: Ticket, timeout_us: int | None = None) -> np.ndarray:
@@ -489,6 +499,9 @@ class Batcher:
             st = _batcher_wait(self._h, ctypes.byref(t), ports.ctypes.data)
         else:
             st = _batcher_wait_timeout(self._h, ctypes.byref(t), ports.ctypes.data, timeout_us)
+        if st == ERR_TIMEOUT:  # not collected: the ticket (and its rules) stay valid
+            _raise(st, "nffacl_batcher_wait")
+        t.rules = None
         if st != OK:
             _raise(st, "nffacl_batcher_wait")
         return ports
@@ -505,18 +518,29 @@ class Batcher:
 
 
 class Service:
-    """Persistent GPU consumer for one-packet calls (nffacl_service_*): the
-    reference's (*Packet).L3ACLPort / L3ACLPermit called per packet from a
-    SetSeparator / SetSplitter function (acl.go:495-506, flow.go:128), with
-    the rule set passed per call.  ctypes drops the GIL during the call."""
+    """Persistent GPU consumer (nffacl_service_*).  Scalar services: one
+    packet per call — the reference's (*Packet).L3ACLPort / L3ACLPermit
+    called from a SetSeparator / SetSplitter function (acl.go:495-506,
+    flow.go:128).  Burst services (burst=True): a clone's whole burst of up
+    to 32 packets per call — the VectorSeparateFunction shape (flow.go:131,
+    1487-1520).  The rule set is passed per call.  ctypes drops the GIL
+    during the calls.
 
-    def __init__(self, device: int = 0, mailboxes: int = 0, idle_us: int = 2000):
+    Failure policy (nffacl.h): `classify` / `classify_burst` raise
+    NFError(ERR_TIMEOUT) when the consumer did not answer (twice); the
+    reference-shaped `L3ACLPort` / `L3ACLPermit` never raise for that — like
+    l3ACL (acl.go:522-565) they return the verdict the library set, 0
+    (reject), and the event is counted in stats()["timeouts"]."""
+
+    def __init__(self, device: int = 0, mailboxes: int = 0, idle_us: int = 2000, burst: bool = False):
         out = ctypes.c_void_p()
-        st = _service_create(device, mailboxes, idle_us, ctypes.byref(out))
+        create = _service_create_burst if burst else _service_create
+        st = create(device, mailboxes, idle_us, ctypes.byref(out))
         if st != OK:
             _raise(st, "nffacl_service_create")
         self._h = out.value
         self.device = device
+        self.burst = burst
 
     def close(self):
         h, self._h = getattr(self, "_h", None), None
@@ -535,22 +559,54 @@ class Service:
     def __exit__(self, *exc):
         self.close()
 
-    def classify(self, rules: L3Rules, frame, flags: int = 0) -> int:
-        """L3ACLPort of one frame (bytes / uint8 array starting at the Ether header)."""
+    def _classify(self, rules: L3Rules, frame, flags: int = 0):
         buf = np.frombuffer(bytes(frame), np.uint8) if not isinstance(frame, np.ndarray) else \
             np.ascontiguousarray(frame, np.uint8)
         port = _u32()
         st = _service_classify(self._h, rules.handle, buf.ctypes.data if len(buf) else None, len(buf), flags,
                                ctypes.byref(port))
+        return st, port.value
+
+    def classify(self, rules: L3Rules, frame, flags: int = 0) -> int:
+        """L3ACLPort of one frame (bytes / uint8 array starting at the Ether header)."""
+        st, port = self._classify(rules, frame, flags)
         if st != OK:
             _raise(st, "nffacl_service_classify")
-        return port.value
+        return port
+
+    def classify_burst(self, rules: L3Rules, ptrs: np.ndarray, lens: np.ndarray | None = None,
+                       flags: int = 0, _raise_timeout: bool = True) -> np.ndarray:
+        """L3ACLPort of a burst (<= 32 frames; pointers and lengths as
+        Batcher.frame_pointers gives them)."""
+        ptrs = np.ascontiguousarray(ptrs, np.uint64)
+        n = len(ptrs)
+        ports = np.zeros(n, np.uint32)
+        lp = None if lens is None else np.ascontiguousarray(lens, np.uint32).ctypes.data
+        st = _service_classify_burst(self._h, rules.handle, ptrs.ctypes.data if n else None, lp, n, flags,
+                                     ports.ctypes.data if n else None)
+        if st != OK and (st != ERR_TIMEOUT or _raise_timeout):
+            _raise(st, "nffacl_service_classify_burst")
+        return ports
 
     def L3ACLPort(self, rules: L3Rules, frame) -> int:
-        return self.classify(rules, frame)
+        st, port = self._classify(rules, frame)
+        if st not in (OK, ERR_TIMEOUT):  # timeout: the policy's verdict (0), counted by the library
+            _raise(st, "nffacl_service_classify")
+        return port
 
     def L3ACLPermit(self, rules: L3Rules, frame) -> bool:
-        return self.classify(rules, frame) > 0
+        return self.L3ACLPort(rules, frame) > 0
+
+    def L3ACLPortBurst(self, rules: L3Rules, ptrs: np.ndarray, lens: np.ndarray | None = None) -> np.ndarray:
+        """The VectorSeparateFunction body: verdicts of a burst (timeouts: 0s, counted)."""
+        return self.classify_burst(rules, ptrs, lens, _raise_timeout=False)
+
+    def pause(self, paused: bool = True):
+        """nffacl_service_pause: stop the resident consumer (calls then follow
+        the failure policy) / resume it."""
+        st = _service_pause(self._h, 1 if paused else 0)
+        if st != OK:
+            _raise(st, "nffacl_service_pause")
 
     def stats(self) -> dict:
         s = ServiceStats()

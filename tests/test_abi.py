@@ -39,7 +39,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert nffacl.abi_version() == 4  # 3: generalized slots in nffacl_table_info
+    assert nffacl.abi_version() == 5  # 3: generalized slots in nffacl_table_info; 5: burst service
 
 
 def test_exports_are_c_linkage_only():

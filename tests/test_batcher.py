@@ -213,3 +213,57 @@ def test_device_batcher_rules_per_burst(torch_cuda, workload):
         st = b.stats()
     assert not errors, errors[:5]
     assert st["bursts"] == 16384 // 32 and st["batches"] < st["bursts"]
+
+
+@pytest.mark.gpu
+def test_unwaited_tickets_bound_submit(torch_cuda, workload, monkeypatch):
+    """One thread submits nbuf + 1 bursts spaced past max_delay without
+    waiting: each burst ships alone and its uncollected ticket keeps its
+    buffer busy, so the (nbuf + 1)-th submit cannot get a buffer from anyone
+    but the caller itself.  It returns ERR_TIMEOUT after the bounded wait
+    (NFFACL_TUNE_BATCH_SUBMIT_MS) instead of blocking forever; once the
+    caller collects its tickets, submits work again and every verdict is
+    exact."""
+    import time
+    g, ptrs, lens, want = _c2_ptrs(workload)
+    eng = nffacl.Engine(nffacl.L3Rules.parse_text(g.text))
+    nbuf = 3
+    monkeypatch.setenv("NFFACL_TUNE_BATCH_SUBMIT_MS", "200")
+    b = nffacl.Batcher(eng, stride=80, max_batch=1024, max_delay_us=100, nbuf=nbuf)
+    monkeypatch.delenv("NFFACL_TUNE_BATCH_SUBMIT_MS")
+    try:
+        ts = []
+        for i in range(nbuf):
+            ts.append(b.submit(ptrs[32 * i:32 * (i + 1)], lens[32 * i:32 * (i + 1)]))
+            time.sleep(0.002)  # > max_delay: the burst's batch ships by itself
+        t0 = time.monotonic()
+        with pytest.raises(nffacl.NFError) as ei:
+            b.submit(ptrs[32 * nbuf:32 * (nbuf + 1)], lens[32 * nbuf:32 * (nbuf + 1)])
+        assert ei.value.status == nffacl.ERR_TIMEOUT
+        assert 0.15 < time.monotonic() - t0 < 5.0
+        for i, t in enumerate(ts):
+            np.testing.assert_array_equal(b.wait(t, timeout_us=2_000_000), want[32 * i:32 * (i + 1)])
+        for i in range(nbuf, nbuf + 8):
+            t = b.submit(ptrs[32 * i:32 * (i + 1)], lens[32 * i:32 * (i + 1)])
+            np.testing.assert_array_equal(b.wait(t, timeout_us=2_000_000), want[32 * i:32 * (i + 1)])
+    finally:
+        b.close()
+        eng.close()
+
+
+@pytest.mark.gpu
+def test_ticket_keeps_rules_alive(torch_cuda, workload):
+    """A rule set made inline and dropped by the caller right after submit
+    (b.submit(..., rules=L3Rules.parse_text(t))) stays alive until the
+    ticket is waited for: the Ticket holds it (nffacl.h: rules must outlive
+    the wait)."""
+    import gc
+    g, ptrs, lens, want = _c2_ptrs(workload)
+    # (each burst names a rule set of its own, so each seals a batch: one buffer per burst)
+    with nffacl.Batcher(None, stride=80, max_batch=1024, max_delay_us=20_000, nbuf=6, device=0) as b:
+        ts = [b.submit(ptrs[32 * i:32 * (i + 1)], lens[32 * i:32 * (i + 1)], rules=nffacl.L3Rules.parse_text(g.text))
+              for i in range(4)]
+        gc.collect()
+        for i, t in enumerate(ts):
+            np.testing.assert_array_equal(b.wait(t, timeout_us=2_000_000), want[32 * i:32 * (i + 1)])
+            assert t.rules is None
