@@ -105,16 +105,21 @@ def build_rules(cfg: str):
 
 
 def pmc_traffic(cfg: str, algo: str, n: int):
-    """HBM bytes per launch from the committed PMC summary, if one matches."""
+    """(HBM bytes per launch, where they come from) from the committed PMC
+    summary of this config's kernel, if one matches: profile-derived (a
+    separate rocprofv3 --pmc run of the same command, FETCH_SIZE x 2 +
+    WRITE_SIZE per the MI355X guide), not measured by this run."""
     path = ROOT / "profiles" / "pmc_traffic.json"
     if not path.exists():
-        return None
+        return None, None
     try:
         d = json.loads(path.read_text())
         e = d.get(f"{cfg}:{algo}:{n}")
-        return None if e is None else float(e["bytes_per_launch"])
+        if e is None:
+            return None, None
+        return float(e["bytes_per_launch"]), f"profile-derived: {e.get('source', '?')} (rocprofv3 --pmc, not this run)"
     except Exception:
-        return None
+        return None, None
 
 
 def cpu_model() -> str:
@@ -324,7 +329,8 @@ def run_config(cfg: str, args, rank: int, world: int, local: int, dev, nd, headl
         "roofline": {
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4),
-            "traffic": pmc_traffic(cfg, algo_name, n),
+            "traffic": pmc_traffic(cfg, algo_name, n)[0],
+            "traffic_source": pmc_traffic(cfg, algo_name, n)[1],
             "kernel_ms_mean": round(float(kms.mean()), 5), "kernel_ms_min": round(float(spread.min()), 5),
             "kernel_ms_p50": round(float(np.median(spread)), 5), "kernel_ms_max": round(float(spread.max()), 5),
             "kernel_ms_all": [round(float(x), 4) for x in spread],
@@ -367,6 +373,18 @@ SHAPE_RUNS = (  # (name, service kind, threads, packets per call, seconds)
 )
 
 
+def shape_runs():
+    """SHAPE_RUNS, or NFFACL_BENCH_SHAPES="kind:threads:per_call:seconds,..." (experiments)."""
+    spec = os.environ.get("NFFACL_BENCH_SHAPES")
+    if not spec:
+        return SHAPE_RUNS
+    runs = []
+    for item in spec.split(","):
+        kind, threads, per, secs = item.split(":")
+        runs.append((f"{kind}{per}_{threads}_threads", kind, int(threads), int(per), float(secs)))
+    return tuple(runs)
+
+
 def call_shapes(cfg: str, text: str, gen, cpu_mpps, local: int):
     """The reference's own call shapes through the resident consumer, on this
     config's rules: one packet per call from 1 and 32
@@ -382,7 +400,8 @@ def call_shapes(cfg: str, text: str, gen, cpu_mpps, local: int):
     from oracle import oracle, rules_oracle as ro
     lib = ctypes.CDLL(str(ROOT / "nff-go_amd" / "libnffshapes.so"))
     lib.nffshapes_run.restype = ctypes.c_int
-    lib.nffshapes_run.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+    lib.nffshapes_run.argtypes = [ctypes.c_void_p, ctypes.c_void_p,  # the loaded libnffacl's entry points
+                                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                   ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
                                   ctypes.c_double, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
     n = 1 << 16
@@ -395,25 +414,35 @@ def call_shapes(cfg: str, text: str, gen, cpu_mpps, local: int):
            "cpu_same_cpus_mpps": cpu_mpps}
     svcs = {"scalar": nffacl.Service(local, mailboxes=128), "burst": nffacl.Service(local, mailboxes=32, burst=True)}
     try:
-        for name, kind, threads, per, secs in SHAPE_RUNS:
+        for name, kind, threads, per, secs in shape_runs():
             o = (ctypes.c_double * 9)()
-            st = lib.nffshapes_run(svcs[kind]._h, rules.handle, slots.ctypes.data, 80, n, expect.ctypes.data,
-                                   threads, per, secs, node, o)
+            fns = (ctypes.cast(nffacl._lib.nffacl_service_classify, ctypes.c_void_p),
+                   ctypes.cast(nffacl._lib.nffacl_service_classify_burst, ctypes.c_void_p))
+            before = svcs[kind].stats()
+            st = lib.nffshapes_run(fns[0], fns[1], svcs[kind]._h, rules.handle, slots.ctypes.data, 80, n,
+                                   expect.ctypes.data, threads, per, secs, node, o)
             if st != 0:
                 res[name] = {"error": st}
                 continue
             sst = svcs[kind].stats()
+            d = {k: sst[k] - before[k] for k in ("polls", "groups", "timeouts", "retries", "launches", "torn")}
             res[name] = {"mpps": round(o[0], 3), "lat_us_p50": round(o[1], 2), "lat_us_p99": round(o[2], 2),
                          "wrong": int(o[3]), "calls": int(o[4]), "errors": int(o[8]),
                          "cpu_us_per_packet": round(o[5], 3), "cpus_busy": round(o[6], 2), "pinned": bool(o[7]),
-                         "timeouts": sst["timeouts"], "table_oob": sst["table_oob"]}
+                         "timeouts": d["timeouts"], "retries": d["retries"], "table_oob": sst["table_oob"],
+                         # the consumer's view (means over its launches so far: poll = PCIe read
+                         # issue -> data, group = classify + answer one request)
+                         "consumer_poll_us": round(sst["poll_ns"] / 1e3, 2),
+                         "consumer_group_us": round(sst["group_ns"] / 1e3, 2),
+                         "polls_per_call": round(d["polls"] / max(1, d["groups"]), 2),
+                         "torn_per_call": round(d["torn"] / max(1, d["groups"]), 3)}
             if cpu_mpps:
                 res[name]["vs_cpu_same_cpus"] = round(o[0] / cpu_mpps, 3)
     finally:
         for v in svcs.values():
             v.close()
     res["bit_exact"] = all(isinstance(v, dict) and v.get("wrong") == 0 and v.get("errors") == 0
-                           for k, v in res.items() if k in {r[0] for r in SHAPE_RUNS})
+                           for k, v in res.items() if k in {r[0] for r in shape_runs()})
     return res
 
 

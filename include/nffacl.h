@@ -407,6 +407,7 @@ typedef struct nffacl_service_stats {
     double group_ns;    /* mean time to classify + answer a group */
     uint64_t answered;  /* requests answered by the consumer (packets) */
     uint64_t retries;   /* requests re-posted after a first timeout (see the failure policy below) */
+    uint64_t torn;      /* polls that read a request while its caller was still writing it (re-read) */
 } nffacl_service_stats;
 
 /* mailboxes: a multiple of 64 (one consumer wave per 8; 0 = 128), one per

@@ -10,6 +10,9 @@
 //     answers — the VectorSeparateFunction shape of segmentProcess
 //     (flow/flow.go:131, 1487-1520).
 // Every verdict is compared with `expect` (the caller's oracle verdicts).
+// The C-ABI entry points come in as function pointers taken from the library
+// the caller loaded (so an experiment build under NFFACL_LIB is the one
+// measured, never a second copy of libnffacl).
 // Threads are pinned to NUMA node `pin_node` (>= 0) — nff-go pins every
 // flow-function clone to a core (low.go:654-666), INTEGRATION.md puts them
 // on the GPU's node.
@@ -67,11 +70,19 @@ extern "C" {
 // out[0] Mpps, [1] p50 latency µs (per call), [2] p99 µs, [3] wrong verdicts,
 // [4] calls, [5] process CPU µs per packet, [6] CPUs busy, [7] 1 if pinned,
 // [8] calls that returned a status other than OK.
-__attribute__((visibility("default"))) int nffshapes_run(nffacl_service *svc, const nffacl_rules *rules,
-                                                         const uint8_t *slots, uint32_t stride, uint64_t n,
-                                                         const uint32_t *expect, uint32_t threads, uint32_t burst,
-                                                         double seconds, int pin_node, double *out) {
-    if (!svc || !rules || !slots || !expect || !out || n < 64 || threads == 0 || burst > 32) return -100;
+typedef int (*classify_fn)(nffacl_service *, const nffacl_rules *, const uint8_t *, uint32_t, uint32_t, uint32_t *);
+typedef int (*burst_fn)(nffacl_service *, const nffacl_rules *, const uint8_t *const *, const uint32_t *, uint32_t,
+                        uint32_t, uint32_t *);
+
+__attribute__((visibility("default"))) int nffshapes_run(void *classify_p, void *burst_p, nffacl_service *svc,
+                                                         const nffacl_rules *rules, const uint8_t *slots,
+                                                         uint32_t stride, uint64_t n, const uint32_t *expect,
+                                                         uint32_t threads, uint32_t burst, double seconds,
+                                                         int pin_node, double *out) {
+    const classify_fn nffacl_service_classify = reinterpret_cast<classify_fn>(classify_p);
+    const burst_fn nffacl_service_classify_burst = reinterpret_cast<burst_fn>(burst_p);
+    if (!classify_p || !burst_p || !svc || !rules || !slots || !expect || !out || n < 64 || threads == 0 || burst > 32)
+        return -100;
     cpu_set_t want;
     const bool pin = pin_node >= 0 && node_cpus(pin_node, want);
     const uint32_t per = burst ? burst : 1;

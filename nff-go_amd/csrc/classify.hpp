@@ -347,6 +347,7 @@ struct IndexedArgs {
     uint32_t flags;         // NFFACL_PARSE_*
     uint32_t dir8;          // HYBRID: two-level directories carry u8 offsets (SplitTab::bounds)
     uint32_t generic;       // HYBRID flat forms: slots key on SlotArgs::f1/f2 (else slot s on field s)
+    uint32_t live;          // positional flat forms: bit s set iff slot s lists rules in some family
     FamArgs f4, f6;
     // persistent consumer (service.hip) only: table size for the bounds
     // checks of its global-memory walk, and the host word they flag
@@ -543,15 +544,18 @@ __device__ __forceinline__ uint32_t times_ew(uint32_t x, bool v6) { return __umu
 // -4 % on C3, profiles/r1_masked).  LDS tables (offsets < 2^16 dwords) get
 // their per-family slot parameters as 16-bit halves of one SGPR each, one
 // v_bfe per parameter instead of two moves and a select.
+// LDS walks, done lanes (NFFACL_EXP_LDSDEAD, an experiment build option):
+// 0 (default) a done lane's cursor stays at its list end and its
+// unconditional entry reads hit a random entry; 1 its cursor moves past the
+// LDS allocation (kDeadCursor > every list end, so the loop test stays one
+// v_cmp) and its reads return 0 without touching a bank; 2 predicated reads.
+// On C2, 1 cuts LDS bank-conflict cycles from 35 M to 11 M per launch but
+// runs 3.5 % slower (0.2235-0.2260 vs 0.2156-0.2163 ms; 2: 0.2235-0.2239),
+// profiles/r4_ab/lds_dead/: the conflicts cost LDS cycles the kernel has to
+// spare, the extra select costs issue slots it has not.
 #ifndef NFFACL_EXP_LDSDEAD
-#define NFFACL_EXP_LDSDEAD 1
+#define NFFACL_EXP_LDSDEAD 0
 #endif
-// LDS walks: the cursor of a lane whose list is done points past the LDS
-// allocation (kDeadCursor > every list end, so the loop test stays one
-// v_cmp): its unconditional entry reads return 0 without touching a bank.
-// (Left at its list end, every done lane of a trip read its own random
-// entry: 35 M LDS bank-conflict cycles per C2 launch instead of 10 M,
-// profiles/prof_r3c_c2 vs prof_r2i_c2.)
 constexpr uint32_t kDeadCursor = 0xFFFF0000u;
 
 template <int NS, int U, class T, bool NP = false>
@@ -833,8 +837,19 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
             const SlotArgs &s4 = a.f4.slot[s], &s6 = a.f6.slot[s];
-            const uint32_t key = s == kFDst ? kd : s == kFSrc ? ks : s == kFDport ? dport : s == kFSport ? sport : 0u;
-            const uint32_t t = key >> par(s4.shift, s6.shift);
+            if (!((a.live >> s) & 1u)) {  // empty in both families (wave-uniform): no lookup
+                st[s] = 0u;
+                ln[s] = 0u;
+                continue;
+            }
+            uint32_t t;
+            if (s < 4) {  // 1-D: [dst, src, dport, sport]
+                const uint32_t key = s == kFDst ? kd : s == kFSrc ? ks : s == kFDport ? dport : sport;
+                t = key >> par(s4.shift, s6.shift);
+            } else {      // fine 2-D grids: [dst x dport, src x dport, dst x sport, src x sport]
+                const uint32_t addr = (s & 1) ? ks : kd, port = s < 6 ? dport : sport;
+                t = ((addr >> par(s4.shift, s6.shift)) << par(s4.bits2, s6.bits2)) | (port >> par(s4.shift2, s6.shift2));
+            }
             uint32_t hi;
             DirTab<DIRS_IN_LDS>{a.tab, a.tab_dwords}.bounds(par(s4.off_dir, s6.off_dir), par(s4.off_dir16, s6.off_dir16),
                                                             t, st[s], hi, a.dir8 != 0u);

@@ -125,9 +125,9 @@ struct DimBuild {
 
 // Radix bits for a dimension holding n rules: about 4 buckets per rule,
 // at most 2^20 buckets (addresses) / 2^16 (ports, i.e. one bucket per port).
-uint32_t pick_rb(size_t n, uint32_t key_bits) {
+uint32_t pick_rb(size_t n, uint32_t key_bits, size_t per_rule = 4) {
     uint32_t rb = 4;
-    while (rb < 20 && (size_t(1) << rb) < 4 * n) ++rb;
+    while (rb < 20 && (size_t(1) << rb) < per_rule * n) ++rb;
     return std::min(rb, key_bits);
 }
 
@@ -143,10 +143,9 @@ constexpr size_t kCoarseMinMoved = 256;
 // Fewest rules worth a source-port slot of their own (see assign_family).
 constexpr size_t kMinSportRules = 128;
 
-// Fine 2-D slots (build_hybrid): a family needs kFineMinRules rules and a
-// slot kFineMinMoved moved rules.
+// Fine 2-D slots (build_hybrid): a family needs kFineMinRules rules (and a
+// slot CompileOptions::fine_min moved rules).
 constexpr uint32_t kFineMinRules = 4096;
-constexpr size_t kFineMinMoved = 256;
 
 // Pick the radix width and count the replicated entries of the dimension's
 // bucket lists: start at ~4 buckets per rule and narrow the radix while wide
@@ -431,6 +430,9 @@ double dir_form_bytes(double nb, int fmt) {
     return 4.0 * (nb + 1);
 }
 
+// LDS directories start at `per_rule` buckets per rule (then narrow to the budget).
+thread_local size_t g_dir_per_rule = 4;  // CompileOptions::dir_per_rule of this thread's compile (compile_table)
+
 void size_directories(DimBuild *const *all, const double *weight, int nd, size_t budget, int fmt) {
     std::vector<uint32_t> rb(nd);
     std::vector<std::vector<double>> mean(nd);
@@ -441,7 +443,7 @@ void size_directories(DimBuild *const *all, const double *weight, int nd, size_t
     for (int i = 0; i < nd; ++i) {
         const DimBuild &d = *all[i];
         if (d.rules.empty()) { rb[i] = 1; continue; }
-        rb[i] = std::max(1u, std::min(pick_rb(d.rules.size(), d.key_bits), d.max_rb));
+        rb[i] = std::max(1u, std::min(pick_rb(d.rules.size(), d.key_bits, g_dir_per_rule), d.max_rb));
         mean[i].assign(rb[i] + 1, 0.0);
         for (uint32_t b = 1; b <= rb[i]; ++b) mean[i][b] = double(entries_at(d, b)) / double(1u << b);
     }
@@ -986,7 +988,7 @@ void build_hybrid(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vec
                 }
             }
             for (int k = 0; k < 4; ++k) {
-                if (moved[k].size() < kFineMinMoved) continue;  // not worth a slot: the rules stay
+                if (moved[k].size() < size_t(opt.fine_min)) continue;  // not worth a slot: the rules stay
                 std::sort(moved[k].begin(), moved[k].end());
                 g[k].rules = moved[k];
                 g[k].fill(pl.rr);
@@ -1267,6 +1269,10 @@ bool CompileOptions::from_env(CompileOptions &o, std::string &err) {
     if (set) o.fine_p = static_cast<int>(v);
     if (!env_knob("NFFACL_TUNE_FINE_G", 1, 100, v, set, err)) return false;
     if (set) o.fine_gain = double(v) / 100.0;
+    if (!env_knob("NFFACL_TUNE_FINE_MIN", 1, 1 << 20, v, set, err)) return false;
+    if (set) o.fine_min = static_cast<int>(v);
+    if (!env_knob("NFFACL_TUNE_DIR_PER_RULE", 1, 64, v, set, err)) return false;
+    if (set) o.dir_per_rule = static_cast<int>(v);
     return true;
 }
 
@@ -1278,6 +1284,7 @@ bool compile_table(const nffacl_rules &rules, int algo, const CompileOptions &op
         return false;
     }
     out = CompiledTable{};
+    g_dir_per_rule = static_cast<size_t>(opt.dir_per_rule);
     std::vector<uint32_t> rec4, rec6;
     rec4.reserve(rules.ip4.size() * kRec4Dwords);
     rec6.reserve(rules.ip6.size() * kRec6Dwords);

@@ -87,6 +87,8 @@ struct CompileOptions {
     int fine_a = 0;
     int fine_p = 4;
     double fine_gain = 0.5;  // NFFACL_TUNE_FINE_G (1/100): a rule moves below this fraction of its 1-D cover
+    int fine_min = 256;      // NFFACL_TUNE_FINE_MIN: fewest moved rules worth a fine slot
+    int dir_per_rule = 4;    // NFFACL_TUNE_DIR_PER_RULE: LDS directory buckets per rule before the budget cut
     bool coarse = false;    // NFFACL_TUNE_COARSE: flat-LDS coarse address slots for short prefixes
                             // (C5 table 7.7 -> 3.7 MB but 0.722 vs 0.649 ms: off; profiles/r2_dir8/coarse/)
     // false (+ `err`) if a set variable is out of range

@@ -344,7 +344,8 @@ static SvcDesc service_desc(const CompiledTable &m) {
         return d;
     }
     const bool flat_lds = m.algo == NFFACL_ALGO_HYBRID && m.lds_dwords > 0 && m.idx4.entry_dwords == kHybEnt4Dwords;
-    if (d.ns > 4 || m.slots_g || (m.algo == NFFACL_ALGO_HYBRID && !flat_lds)) return d;  // kSvcNone
+    if ((d.ns > 4 && !flat_lds) || d.ns > kMaxSlots || m.slots_g || (m.algo == NFFACL_ALGO_HYBRID && !flat_lds))
+        return d;  // kSvcNone
     d.kind = flat_lds ? kSvcFlat : kSvcIndexed;
     const uint32_t off_cold[2] = {m.off_rec4, m.off_rec6};
     for (int f = 0; f < 2; ++f) {
@@ -353,9 +354,9 @@ static SvcDesc service_desc(const CompiledTable &m) {
         o.n_resid = fi[f]->n_resid;
         o.off_cold = off_cold[f];
         o.off_ent_base = fi[f]->off_ent_base;
-        for (int s = 0; s < 4; ++s) {
+        for (uint32_t s = 0; s < kMaxSlots; ++s) {
             const DimInfo &di = fi[f]->dims[s];
-            o.slot[s][0] = di.shift;
+            o.slot[s][0] = di.shift | di.shift2 << 8 | di.bits2 << 16;
             o.slot[s][1] = di.off_dir;
             o.slot[s][2] = di.off_ent;
             o.slot[s][3] = di.off_dir16;
@@ -447,6 +448,9 @@ static dev::IndexedArgs indexed_args(const DevTable *t) {
     };
     fam(t->meta.idx4, t->meta.off_rec4, a.f4);
     fam(t->meta.idx6, t->meta.off_rec6, a.f6);
+    a.live = 0;
+    for (uint32_t k = 0; k < kMaxSlots; ++k)
+        if (t->meta.slots_g || t->meta.idx4.dims[k].n_rules || t->meta.idx6.dims[k].n_rules) a.live |= 1u << k;
     return a;
 }
 

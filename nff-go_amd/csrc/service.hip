@@ -110,38 +110,46 @@ struct CheckedTab {
     }
 };
 
-// Classify one group (wave-uniform descriptor `w`, table `tab`).
-__device__ __forceinline__ uint32_t svc_classify(const uint32_t (&w)[kSvcDescDwords], const uint32_t *tab,
-                                                 const Fields &f, FlatScratch<2> &W, uint32_t lane, uint32_t *oob,
-                                                 bool staged) {
-    const uint32_t kind = w[0], ns = w[1];
-    if (kind == kSvcLinear) return classify_linear(f, tab + w[4], w[5], tab + w[6], w[7]);
+// Classify one group (table `tab`, its descriptor `wd` staged in this wave's
+// LDS: read where used, so the 80 descriptor words are not held in SGPRs
+// across the polling loop).
+__device__ __forceinline__ uint32_t svc_classify(const uint32_t *wd, const uint32_t *tab, const Fields &f,
+                                                 FlatScratch<2> &W, uint32_t lane, uint32_t *oob, bool staged) {
+    // (held in VGPRs until used: readfirstlane'd up front they kept ~80 SGPRs
+    // live and spilled; the walks take their per-family values with fam_sel)
+    auto w = [&](uint32_t i) -> uint32_t { return wd[i]; };
+    const uint32_t kind = __builtin_amdgcn_readfirstlane(wd[0]), ns = __builtin_amdgcn_readfirstlane(wd[1]);
+    if (kind == kSvcLinear) return classify_linear(f, tab + w(4), w(5), tab + w(6), w(7));
     IndexedArgs a{};
     a.tab = tab;
-    a.dir8 = w[3];
+    a.dir8 = w(3);
     a.generic = 0;
-    a.tab_dwords = w[2];
+    a.tab_dwords = w(2);
     a.oob = oob;
+    a.live = 0xFFu;
+    constexpr uint32_t kFam = 4 + 4 * kMaxSlots;
 #pragma unroll
     for (int fam = 0; fam < 2; ++fam) {
         FamArgs &fa = fam ? a.f6 : a.f4;
-        const uint32_t b = 8 + 20 * fam;
-        fa.off_resid = w[b + 0];
-        fa.n_resid = w[b + 1];
-        fa.off_cold = w[b + 2];
-        fa.off_ent_base = w[b + 3];
+        const uint32_t b = 8 + kFam * fam;
+        fa.off_resid = w(b + 0);
+        fa.n_resid = w(b + 1);
+        fa.off_cold = w(b + 2);
+        fa.off_ent_base = w(b + 3);
 #pragma unroll
-        for (int s = 0; s < 4; ++s)
-            fa.slot[s] = SlotArgs{w[b + 4 + 4 * s], w[b + 5 + 4 * s], w[b + 6 + 4 * s], w[b + 7 + 4 * s],
-                                  static_cast<uint32_t>(s), kFZero, 0, 0};
+        for (uint32_t s = 0; s < kMaxSlots; ++s) {
+            const uint32_t sh = w(b + 4 + 4 * s);
+            fa.slot[s] = SlotArgs{sh & 0xFFu, w(b + 5 + 4 * s), w(b + 6 + 4 * s), w(b + 7 + 4 * s),
+                                  s, kFZero, (sh >> 8) & 0xFFu, (sh >> 16) & 0xFFu};
+        }
     }
-    if (kind == kSvcIndexed && staged) {  // the whole table in LDS (lds_tab[0, w[2]))
+    if (kind == kSvcIndexed && staged) {  // the whole table in LDS (lds_tab[0, tab_dwords))
         if (ns == 2) return classify_indexed<2, 1>(LdsTab{}, a, f);
         if (ns == 3) return classify_indexed<3, 1>(LdsTab{}, a, f);
         return classify_indexed<4, 1>(LdsTab{}, a, f);
     }
     if (kind == kSvcIndexed) {
-        const CheckedTab ct{tab, w[2], oob};
+        const CheckedTab ct{tab, a.tab_dwords, oob};
         if (ns == 2) return classify_indexed<2, 1>(ct, a, f);
         if (ns == 3) return classify_indexed<3, 1>(ct, a, f);
         return classify_indexed<4, 1>(ct, a, f);
@@ -149,7 +157,11 @@ __device__ __forceinline__ uint32_t svc_classify(const uint32_t (&w)[kSvcDescDwo
     if (kind == kSvcFlat) {
         if (ns == 2) return classify_flat<2, 2, true, false, false>(a, f, W, lane);
         if (ns == 3) return classify_flat<3, 2, true, false, false>(a, f, W, lane);
-        return classify_flat<4, 2, true, false, false>(a, f, W, lane);
+        if (ns == 4) return classify_flat<4, 2, true, false, false>(a, f, W, lane);
+        if (ns == 5) return classify_flat<5, 2, true, false, false>(a, f, W, lane);
+        if (ns == 6) return classify_flat<6, 2, true, false, false>(a, f, W, lane);
+        if (ns == 7) return classify_flat<7, 2, true, false, false>(a, f, W, lane);
+        return classify_flat<8, 2, true, false, false>(a, f, W, lane);
     }
     return 0u;
 }
@@ -169,9 +181,8 @@ __global__ void __launch_bounds__(64) k_service(SvcArgs a) {
     uint64_t last = t0, lane_last = t0;  // hot at start: the call that armed us is read whole
     uint32_t cur_key = 0xFFFFFFFFu;  // generation << 1 | vlan of the descriptor in `w`
     uint32_t staged_gen = 0xFFFFFFFFu;  // generation of the table staged in LDS
-    uint32_t w[kSvcDescDwords];
-#pragma unroll
-    for (uint32_t i = 0; i < kSvcDescDwords; ++i) w[i] = 0;
+    __shared__ __attribute__((aligned(16))) uint32_t wd[kSvcDescDwords];  // the current table's descriptor
+    uint32_t w_kind = 0, w_dwords = 0;  // its kind and table size (wave-uniform)
     const uint32_t *tab = nullptr;
     // where the time goes (wall-clock ticks, written to host memory at exit):
     // polls and their ticks (issue to data), groups classified and their
@@ -287,26 +298,20 @@ __global__ void __launch_bounds__(64) k_service(SvcArgs a) {
                 const uint64_t lo = static_cast<uint32_t>(__builtin_amdgcn_readlane(c[kSvcChunks - 1].x, first));
                 const uint64_t hi = static_cast<uint32_t>(__builtin_amdgcn_readlane(c[kSvcChunks - 1].y, first));
                 const u32x4 *dq = reinterpret_cast<const u32x4 *>(hi << 32 | lo);
-                u32x4 q[kSvcDescDwords / 4];
-#pragma unroll
-                for (uint32_t i = 0; i < kSvcDescDwords / 4; ++i) q[i] = dq[i];
-#pragma unroll
-                for (uint32_t i = 0; i < kSvcDescDwords / 4; ++i) {
-                    w[4 * i + 0] = __builtin_amdgcn_readfirstlane(q[i].x);
-                    w[4 * i + 1] = __builtin_amdgcn_readfirstlane(q[i].y);
-                    w[4 * i + 2] = __builtin_amdgcn_readfirstlane(q[i].z);
-                    w[4 * i + 3] = __builtin_amdgcn_readfirstlane(q[i].w);
-                }
-                tab = reinterpret_cast<const uint32_t *>(hi << 32 | lo) - w[2];
+                if (lane < kSvcDescDwords / 4) reinterpret_cast<u32x4 *>(wd)[lane] = dq[lane];
+                wave_lds_sync();
+                w_kind = __builtin_amdgcn_readfirstlane(wd[0]);
+                w_dwords = __builtin_amdgcn_readfirstlane(wd[2]);
+                tab = reinterpret_cast<const uint32_t *>(hi << 32 | lo) - w_dwords;
                 cur_key = key;
             }
             // small INDEXED tables are walked from LDS: staged once per table
             // (per launch), and then no table read waits behind the PCIe polls
-            const bool staged = w[0] == kSvcIndexed && w[2] <= a.lds_dwords;
+            const bool staged = w_kind == kSvcIndexed && w_dwords <= a.lds_dwords;
             if (staged && staged_gen != (key >> 1)) {
                 const u32x4 *src = reinterpret_cast<const u32x4 *>(tab);
                 u32x4 *dst = reinterpret_cast<u32x4 *>(lds_tab);
-                for (uint32_t i = lane; i < (w[2] + 3u) / 4u; i += 64u) dst[i] = src[i];
+                for (uint32_t i = lane; i < (w_dwords + 3u) / 4u; i += 64u) dst[i] = src[i];
                 wave_lds_sync();
                 staged_gen = key >> 1;
             }
@@ -329,7 +334,7 @@ __global__ void __launch_bounds__(64) k_service(SvcArgs a) {
                     hi = k + 1 == j ? full[j] : hi;
                 }
             }, key & 1u ? uint32_t(NFFACL_PARSE_VLAN) : 0u);
-            const uint32_t port = svc_classify(w, tab, f, W, lane, a.ctrl + 2, staged);
+            const uint32_t port = svc_classify(wd, tab, f, W, lane, a.ctrl + 2, staged);
             if (mine) {
                 __hip_atomic_store(resp, uint64_t(tag) << 32 | port, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 done = tag;
@@ -371,11 +376,10 @@ __global__ void __launch_bounds__(64) k_service_burst(SvcArgs a) {
     const uint64_t t0 = wall_clock64();
     uint64_t last = t0, ans_last = t0;  // hot at start: the call that armed us is read whole
     uint32_t cur_key = 0xFFFFFFFFu, staged_gen = 0xFFFFFFFFu;
-    uint32_t w[kSvcDescDwords];
-#pragma unroll
-    for (uint32_t i = 0; i < kSvcDescDwords; ++i) w[i] = 0;
+    __shared__ __attribute__((aligned(16))) uint32_t wd[kSvcDescDwords];  // the current table's descriptor
+    uint32_t w_kind = 0, w_dwords = 0;  // its kind and table size (wave-uniform)
     const uint32_t *tab = nullptr;
-    uint64_t n_polls = 0, poll_ticks = 0, n_groups = 0, group_ticks = 0, n_req = 0;
+    uint64_t n_polls = 0, poll_ticks = 0, n_groups = 0, group_ticks = 0, n_req = 0, n_torn = 0;
     const uint32_t box = mb * kSvcBurstBoxBytes;
     const uint32_t bell = a.box_bytes + mb * 4u;
     constexpr uint32_t kTailLanes = (kSvcBurstChunks * 16 - (kSvcBurstLoads - 1) * 1024 + 15) / 16;
@@ -444,7 +448,10 @@ __global__ void __launch_bounds__(64) k_service_burst(SvcArgs a) {
         bool torn = h1.w != tag || n == 0u || n > kSvcBurstMax;
 #pragma unroll
         for (uint32_t j = 0; j < kSvcPktChunks; ++j) torn = torn || (live && c[j].w != tag);
-        if (ballot(torn)) continue;  // raced the host's stores: the next poll has it
+        if (ballot(torn)) {  // raced the host's stores: the next poll has it
+            ++n_torn;
+            continue;
+        }
         const uint64_t t_group = wall_clock64();
         const uint32_t key = __builtin_amdgcn_readfirstlane(h0.z);
         if (key == kSvcWithdrawn) {  // the caller gave up: answered, no table read
@@ -461,24 +468,18 @@ __global__ void __launch_bounds__(64) k_service_burst(SvcArgs a) {
             const uint64_t lo = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(h0.x));
             const uint64_t hi = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(h0.y));
             const u32x4 *dq = reinterpret_cast<const u32x4 *>(hi << 32 | lo);
-            u32x4 q[kSvcDescDwords / 4];
-#pragma unroll
-            for (uint32_t i = 0; i < kSvcDescDwords / 4; ++i) q[i] = dq[i];
-#pragma unroll
-            for (uint32_t i = 0; i < kSvcDescDwords / 4; ++i) {
-                w[4 * i + 0] = __builtin_amdgcn_readfirstlane(q[i].x);
-                w[4 * i + 1] = __builtin_amdgcn_readfirstlane(q[i].y);
-                w[4 * i + 2] = __builtin_amdgcn_readfirstlane(q[i].z);
-                w[4 * i + 3] = __builtin_amdgcn_readfirstlane(q[i].w);
-            }
-            tab = reinterpret_cast<const uint32_t *>(hi << 32 | lo) - w[2];
+            if (lane < kSvcDescDwords / 4) reinterpret_cast<u32x4 *>(wd)[lane] = dq[lane];
+            wave_lds_sync();
+            w_kind = __builtin_amdgcn_readfirstlane(wd[0]);
+            w_dwords = __builtin_amdgcn_readfirstlane(wd[2]);
+            tab = reinterpret_cast<const uint32_t *>(hi << 32 | lo) - w_dwords;
             cur_key = key;
         }
-        const bool staged = w[0] == kSvcIndexed && w[2] <= a.lds_dwords;
+        const bool staged = w_kind == kSvcIndexed && w_dwords <= a.lds_dwords;
         if (staged && staged_gen != (key >> 1)) {
             const u32x4 *src = reinterpret_cast<const u32x4 *>(tab);
             u32x4 *dst = reinterpret_cast<u32x4 *>(lds_tab);
-            for (uint32_t i = lane; i < (w[2] + 3u) / 4u; i += 64u) dst[i] = src[i];
+            for (uint32_t i = lane; i < (w_dwords + 3u) / 4u; i += 64u) dst[i] = src[i];
             wave_lds_sync();
             staged_gen = key >> 1;
         }
@@ -501,7 +502,7 @@ __global__ void __launch_bounds__(64) k_service_burst(SvcArgs a) {
                 hi = k + 1 == j ? full[j] : hi;
             }
         }, key & 1u ? uint32_t(NFFACL_PARSE_VLAN) : 0u);
-        const uint32_t port = svc_classify(w, tab, f, W, lane, a.ctrl + 2, staged);
+        const uint32_t port = svc_classify(wd, tab, f, W, lane, a.ctrl + 2, staged);
         if (live) __hip_atomic_store(resp + lane, uint64_t(tag) << 32 | port, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         done = tag;
         ans_last = now;
@@ -511,9 +512,9 @@ __global__ void __launch_bounds__(64) k_service_burst(SvcArgs a) {
     }
     if (lane == 0) {
         uint64_t *st = a.stats + size_t(blockIdx.x) * kSvcStatWords;
-        const uint64_t v[5] = {n_polls, poll_ticks, n_groups, group_ticks, n_req};
+        const uint64_t v[6] = {n_polls, poll_ticks, n_groups, group_ticks, n_req, n_torn};
 #pragma unroll
-        for (int i = 0; i < 5; ++i) __hip_atomic_store(st + i, v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        for (int i = 0; i < 6; ++i) __hip_atomic_store(st + i, v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -1285,6 +1286,7 @@ int nffacl_service_get_stats(nffacl_service *s, nffacl_service_stats *out) {
     out->groups = s->acc[2];
     out->group_ns = s->acc[2] ? s->acc[3] * 1000.0 / tpu / double(s->acc[2]) : 0.0;
     out->answered = s->acc[4];
+    out->torn = s->acc[5];
     return NFFACL_OK;
 }
 

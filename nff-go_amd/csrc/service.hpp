@@ -17,6 +17,8 @@
 
 #include <cstdint>
 
+#include "table.hpp"
+
 namespace nffacl {
 
 // ---- mailbox (host memory, one per calling thread) ---------------------------
@@ -77,12 +79,14 @@ enum SvcKind : uint32_t {
 
 struct SvcFamily {
     uint32_t off_resid, n_resid, off_cold, off_ent_base;
-    uint32_t slot[4][4];  // per positional slot: shift, off_dir, off_ent, off_dir16
+    // per positional slot: shift | shift2 << 8 | bits2 << 16, off_dir, off_ent, off_dir16
+    // (slots 4..7: the flat form's fine 2-D grids, compile.cpp build_hybrid)
+    uint32_t slot[kMaxSlots][4];
 };
 
 struct SvcDesc {
     uint32_t kind;        // SvcKind
-    uint32_t ns;          // slots walked (2..4)
+    uint32_t ns;          // slots walked (2..8; INDEXED 2..4)
     uint32_t back;        // dwords from the blob start to this descriptor
     uint32_t dir8;        // two-level directories with u8 offsets
     uint32_t off_rec4, n4, off_rec6, n6;  // LINEAR records

@@ -224,8 +224,9 @@ inline void L3ACLPortBatch(const Packet *const *pkts, size_t n, uint32_t *ports,
 }
 
 namespace detail {
-// One persistent consumer per GPU for the whole process (nffacl_service_*).
-inline nffacl_service *service(int dev) {
+// One persistent consumer per GPU for the whole process (nffacl_service_*):
+// scalar mailboxes (burst = false) or burst mailboxes (one per clone).
+inline nffacl_service *service(int dev, bool burst = false) {
     struct Holder {
         std::once_flag once;
         nffacl_service *svc = nullptr;
@@ -234,14 +235,27 @@ inline nffacl_service *service(int dev) {
             if (svc) nffacl_service_destroy(svc);
         }
     };
-    static Holder holders[16];
+    static Holder holders[2][16];
     if (dev < 0 || dev >= 16) throw std::runtime_error("ACL device out of range");
-    Holder &h = holders[dev];
-    std::call_once(h.once, [&] { h.st = nffacl_service_create(dev, 0, 2000, &h.svc); });
+    Holder &h = holders[burst ? 1 : 0][dev];
+    std::call_once(h.once, [&] {
+        h.st = burst ? nffacl_service_create_burst(dev, 0, 2000, &h.svc) : nffacl_service_create(dev, 0, 2000, &h.svc);
+    });
     if (h.st != NFFACL_OK)
         throw std::runtime_error(std::string("nffacl_service_create: ") + nffacl_strerror(h.st) + " " +
                                  nffacl_last_error());
     return h.svc;
+}
+
+// The service failure policy (nffacl.h): a call the consumer did not answer
+// (twice) returns NFFACL_ERR_TIMEOUT with verdict 0 — reject, what l3ACL
+// gives a packet no rule matches — and is counted in the service's stats.
+// The reference's verdict path never errors (acl.go:522-565), so the mirror
+// returns that verdict instead of throwing out of a flow function; any other
+// status is a programming error and throws.
+inline void check_service(int st, const char *what) {
+    if (st != NFFACL_OK && st != NFFACL_ERR_TIMEOUT)
+        throw std::runtime_error(std::string(what) + ": " + nffacl_strerror(st) + " " + nffacl_last_error());
 }
 }  // namespace detail
 
@@ -249,11 +263,28 @@ inline nffacl_service *service(int dev) {
 // persistent consumer, against the rule set's own table.
 inline uint32_t Packet::L3ACLPort(const L3Rules &rules) const {
     uint32_t port = 0;
-    const int st = nffacl_service_classify(detail::service(ACLDevice()), rules.handle(), Ether, Len, 0, &port);
-    if (st != NFFACL_OK)
-        throw std::runtime_error(std::string("nffacl_service_classify: ") + nffacl_strerror(st) + " " +
-                                 nffacl_last_error());
+    detail::check_service(nffacl_service_classify(detail::service(ACLDevice()), rules.handle(), Ether, Len, 0, &port),
+                          "nffacl_service_classify");
     return port;
+}
+
+// L3ACLPort of a burst (the VectorSeparateFunction shape, flow.go:131): one
+// request per 32 packets to this thread's burst mailbox of the GPU's
+// consumer — one PCIe round trip per burst, no kernel launch.
+inline void L3ACLPortBurst(const Packet *const *pkts, size_t n, uint32_t *ports, const L3Rules &rules) {
+    const uint8_t *frames[32];
+    uint32_t lens[32];
+    nffacl_service *svc = detail::service(ACLDevice(), true);
+    for (size_t off = 0; off < n; off += 32) {
+        const size_t m = std::min<size_t>(32, n - off);
+        for (size_t i = 0; i < m; ++i) {
+            frames[i] = pkts[off + i]->Ether;
+            lens[i] = pkts[off + i]->Len;
+        }
+        detail::check_service(nffacl_service_classify_burst(svc, rules.handle(), frames, lens,
+                                                            static_cast<uint32_t>(m), 0, ports + off),
+                              "nffacl_service_classify_burst");
+    }
 }
 
 // ---- L2 ACL (acl.go:68-117, 356-383, 457-491) ----------------------------------
@@ -369,7 +400,8 @@ using VectorSplitFunction =  // flow.go:139
     std::function<void(packet::Packet *const *pkts, const bool *mask, uint8_t *answers)>;
 
 // The reference's vector separator over L3ACLPermit
-// (testSingleWorkingFF.go:538-546) as one GPU call per burst.
+// (testSingleWorkingFF.go:538-546) as one request per burst to the GPU's
+// resident consumer (packet::L3ACLPortBurst).
 inline VectorSeparateFunction ACLVectorSeparator(std::shared_ptr<const packet::L3Rules> rules) {
     return [rules](packet::Packet *const *pkts, const bool *mask, bool *answers) {
         const packet::Packet *sel[vBurstSize];
@@ -378,7 +410,7 @@ inline VectorSeparateFunction ACLVectorSeparator(std::shared_ptr<const packet::L
         for (int i = 0; i < vBurstSize; ++i)
             if (mask[i] && pkts[i]) { sel[n] = pkts[i]; idx[n++] = i; }
         uint32_t ports[vBurstSize] = {0};
-        packet::L3ACLPortBatch(sel, n, ports, *rules);
+        packet::L3ACLPortBurst(sel, n, ports, *rules);
         for (size_t k = 0; k < n; ++k) answers[idx[k]] = ports[k] > 0;
     };
 }
@@ -392,7 +424,7 @@ inline VectorSplitFunction ACLVectorSplitter(std::shared_ptr<const packet::L3Rul
         for (int i = 0; i < vBurstSize; ++i)
             if (mask[i] && pkts[i]) { sel[n] = pkts[i]; idx[n++] = i; }
         uint32_t ports[vBurstSize] = {0};
-        packet::L3ACLPortBatch(sel, n, ports, *rules);
+        packet::L3ACLPortBurst(sel, n, ports, *rules);
         for (size_t k = 0; k < n; ++k) answers[idx[k]] = static_cast<uint8_t>(ports[k]);
     };
 }

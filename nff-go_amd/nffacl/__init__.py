@@ -146,7 +146,7 @@ class ServiceStats(ctypes.Structure):
     _fields_ = [("launches", ctypes.c_uint64), ("requests", ctypes.c_uint64), ("timeouts", ctypes.c_uint64),
                 ("running", ctypes.c_uint64), ("table_oob", ctypes.c_uint64), ("polls", ctypes.c_uint64),
                 ("poll_ns", ctypes.c_double), ("groups", ctypes.c_uint64), ("group_ns", ctypes.c_double),
-                ("answered", ctypes.c_uint64), ("retries", ctypes.c_uint64)]
+                ("answered", ctypes.c_uint64), ("retries", ctypes.c_uint64), ("torn", ctypes.c_uint64)]
 
 
 _rules_prepare = _sig("nffacl_rules_prepare", _i, _vp, _i)

@@ -686,6 +686,10 @@ static void TestRuleReloadStep08(T &t) {
                 batcher->Classify(local->rules.get(), burst, flow::vBurstSize, ports);
                 for (int i = 0; i < flow::vBurstSize; ++i)
                     if (ports[i] != expect(local->k, which[i])) ++bad;
+                // the same burst as one request to the resident consumer (burst mailbox)
+                packet::L3ACLPortBurst(burst, flow::vBurstSize, ports, *local->rules);
+                for (int i = 0; i < flow::vBurstSize; ++i)
+                    if (ports[i] != expect(local->k, which[i])) ++bad;
                 const int i = (it + c) % 4;
                 if (pk[i].L3ACLPort(*local->rules) != expect(local->k, i)) ++bad;
                 ++seen[local->k];

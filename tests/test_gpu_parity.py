@@ -518,6 +518,40 @@ def test_full_size_c5_hybrid(torch_cuda, monkeypatch, flat):
     np.testing.assert_array_equal(outs[nffacl.ALGO_AUTO].cpu().numpy().view(np.uint32)[idx], want)
 
 
+def test_full_size_c3_hybrid(torch_cuda):
+    """C3 at the bench size: 2^24 IMIX (64/570/1518 at 7:4:1) packed frames,
+    10 k L3+L4 rules — HYBRID (AUTO's choice) == INDEXED read from global
+    memory on every frame, classifying two halves separately == the whole
+    batch, and a 2^14 random sample equals the oracle."""
+    torch = torch_cuda
+    g = synth.gen_rules(synth.SPECS["c3"], synth.RULE_SEEDS["c3"])
+    rules, (a4, a6) = _rules_and_arrays(g.text)
+    n = 1 << 24
+    frames, desc = synth.gen_imix(g, n, synth.PACKET_SEEDS["c3"])
+    d_frames = to_dev(torch, frames)
+    d_desc = torch.from_numpy(desc.view(np.int64)).to("cuda")
+    outs = {}
+    for algo in (nffacl.ALGO_AUTO, nffacl.ALGO_INDEXED):
+        with nffacl.Engine(rules, algo=algo) as eng:
+            assert eng.algo == (nffacl.ALGO_HYBRID if algo == nffacl.ALGO_AUTO else nffacl.ALGO_INDEXED)
+            port = torch.zeros(n, dtype=torch.int32, device="cuda")
+            eng.classify_frames_device(d_frames, d_desc, n, port)
+            if algo == nffacl.ALGO_AUTO:
+                half = torch.zeros(n, dtype=torch.int32, device="cuda")
+                h = n // 2 + 64 * 5 + 29
+                eng.classify_frames_device(d_frames, d_desc, h, half)
+                eng.classify_frames_device(d_frames, d_desc.data_ptr() + h * 8, n - h, half.data_ptr() + h * 4)
+                torch.cuda.synchronize()
+                assert torch.equal(port, half)
+            torch.cuda.synchronize()
+            outs[algo] = port
+    assert torch.equal(outs[nffacl.ALGO_AUTO], outs[nffacl.ALGO_INDEXED])
+    rng = np.random.default_rng(11)
+    idx = np.sort(rng.choice(n, 1 << 14, replace=False))
+    want = oracle.classify_frames(frames, desc[idx], a4, a6, threads=THREADS)
+    np.testing.assert_array_equal(outs[nffacl.ALGO_AUTO].cpu().numpy().view(np.uint32)[idx], want)
+
+
 @pytest.mark.parametrize("coarse,dir8", [("1", "1"), ("0", "0")])
 def test_c5_flat_lds_layout_options(torch_cuda, monkeypatch, coarse, dir8):
     """The flat-LDS layout options besides the default (u8 directories, no
