@@ -245,6 +245,8 @@ typedef struct nffacl_table_info {
     uint32_t lds_dwords; /* HYBRID: blob[0, lds_dwords) = the directories staged in LDS */
     uint64_t blob_dwords;
     nffacl_family_info fam[2]; /* [0] IPv4, [1] IPv6 */
+    uint32_t off_params; /* HYBRID flat-LDS positional forms: the slot parameter block in the LDS image (0: none) */
+    uint32_t reserved;
 } nffacl_table_info;
 
 NFFACL_API int nffacl_table_compile(const nffacl_rules *rules, int algo, uint32_t *blob,

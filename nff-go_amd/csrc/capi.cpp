@@ -220,6 +220,8 @@ int nffacl_table_compile(const nffacl_rules *rules, int algo, uint32_t *blob, ui
     info->algo = ct.algo;
     info->blob_dwords = ct.blob.size();
     info->lds_dwords = ct.lds_dwords;
+    info->off_params = ct.off_params;
+    info->reserved = 0;
     const FamilyIndex *fi[2] = {&ct.idx4, &ct.idx6};
     const uint32_t off_rec[2] = {ct.off_rec4, ct.off_rec6}, n_rec[2] = {ct.n4, ct.n6};
     for (int f = 0; f < 2; ++f) {

@@ -348,6 +348,8 @@ struct IndexedArgs {
     uint32_t dir8;          // HYBRID: two-level directories carry u8 offsets (SplitTab::bounds)
     uint32_t generic;       // HYBRID flat forms: slots key on SlotArgs::f1/f2 (else slot s on field s)
     uint32_t live;          // positional flat forms: bit s set iff slot s lists rules in some family
+    uint32_t off_params;    // flat-LDS positional forms: dword offset (in the LDS image) of the slot
+                            // parameter block (table.hpp kFlatParams), 0 = take them from SlotArgs
     FamArgs f4, f6;
     // persistent consumer (service.hip) only: table size for the bounds
     // checks of its global-memory walk, and the host word they flag
@@ -379,6 +381,11 @@ enum TableMode : int {
     kTabFlatLds4U = 8, // the same, entry loads of every non-empty round issued
                        // without a per-lane branch (tables with many candidates
                        // per packet: CompiledTable::flat_uncond)
+    kTabFlatLdsG = 10, // flat-LDS over generalized slots (CompiledTable::slots_g:
+                       // the coarse / SLOTS2D layout experiments), 4 rounds,
+                       // branch-free loads — a kernel of its own, so that the
+                       // positional kernels carry no generic lookup code (its
+                       // kernel-argument registers spilled in every one of them)
 };
 
 extern __shared__ __attribute__((aligned(16))) uint32_t lds_tab[];
@@ -790,7 +797,7 @@ __device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
     return x;
 }
 
-template <int NS, int R, bool LDS_DIRS, bool UNCOND = false, bool DIRS_IN_LDS = true>
+template <int NS, int R, bool LDS_DIRS, bool UNCOND = false, bool DIRS_IN_LDS = true, bool GEN = false>
 __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fields &f, FlatScratch<R> &W,
                                                   uint32_t lane) {
     const bool v6 = f.is6;
@@ -825,7 +832,7 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
     uint32_t st[NS], ln[NS];
     // positional slots (a.generic == 0: slot s keys on field s, 1-D): the key
     // is known at compile time, no per-lane field selects (wave-uniform branch)
-    if (LDS_DIRS && a.generic == 0u) {
+    if (LDS_DIRS && !GEN) {
         // directories staged in LDS: offsets < 2^16 dwords, so the family
         // parameters travel as 16-bit SGPR halves (one v_bfe each, as in
         // classify_indexed); global directories (service.hip): fam_sel
@@ -842,17 +849,40 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
                 ln[s] = 0u;
                 continue;
             }
+            // the slot's parameters: one broadcast ds_read_b128 of the
+            // table's LDS parameter block (kFlatParams; every flat-LDS
+            // positional table has one) — kept as kernel arguments they held
+            // 2 SGPRs per slot and family across the batch loop and spilled
+            // (C5 NS = 6: 113 SGPR spills, 320 v_readlane in the loop); the
+            // service's walk (directories in global memory) takes SlotArgs
+            uint32_t shift, dir, dir16, bits2 = 0, shift2 = 0;
+            if (DIRS_IN_LDS) {
+                const u32x4 P = *(lds_u32x4 *)(uintptr_t)(lds_base() + 4u * (a.off_params + kFlatParamDwords * s));
+                shift = __builtin_amdgcn_ubfe(P.x, half, 16);
+                dir = __builtin_amdgcn_ubfe(P.y, half, 16);
+                dir16 = __builtin_amdgcn_ubfe(P.z, half, 16);
+                const uint32_t fine = __builtin_amdgcn_ubfe(P.w, half, 16);
+                bits2 = fine & 0xFFu;
+                shift2 = fine >> 8;
+            } else {
+                shift = par(s4.shift, s6.shift);
+                dir = par(s4.off_dir, s6.off_dir);
+                dir16 = par(s4.off_dir16, s6.off_dir16);
+                if (s >= 4) {
+                    bits2 = par(s4.bits2, s6.bits2);
+                    shift2 = par(s4.shift2, s6.shift2);
+                }
+            }
             uint32_t t;
             if (s < 4) {  // 1-D: [dst, src, dport, sport]
                 const uint32_t key = s == kFDst ? kd : s == kFSrc ? ks : s == kFDport ? dport : sport;
-                t = key >> par(s4.shift, s6.shift);
+                t = key >> shift;
             } else {      // fine 2-D grids: [dst x dport, src x dport, dst x sport, src x sport]
                 const uint32_t addr = (s & 1) ? ks : kd, port = s < 6 ? dport : sport;
-                t = ((addr >> par(s4.shift, s6.shift)) << par(s4.bits2, s6.bits2)) | (port >> par(s4.shift2, s6.shift2));
+                t = ((addr >> shift) << bits2) | (port >> shift2);
             }
             uint32_t hi;
-            DirTab<DIRS_IN_LDS>{a.tab, a.tab_dwords}.bounds(par(s4.off_dir, s6.off_dir), par(s4.off_dir16, s6.off_dir16),
-                                                            t, st[s], hi, a.dir8 != 0u);
+            DirTab<DIRS_IN_LDS>{a.tab, a.tab_dwords}.bounds(dir, dir16, t, st[s], hi, a.dir8 != 0u);
             ln[s] = mine ? hi - st[s] : 0u;
         }
     } else {
@@ -944,6 +974,9 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
             const uint32_t ent = !UNCOND || valid[j] ? k + static_cast<uint32_t>(static_cast<int32_t>(dp) >> 1) : 0u;
             // (entry numbers < 2^24, table_consistent: a full-rate 24-bit multiply)
             const bool e6 = six[j] && (!UNCOND || valid[j]);
+            // (round 4: one uniform base + a 32-bit byte offset per entry, the
+            // saddr load form, -56 static VALU: C5 0.6547 / 0.6527 vs 0.6520 /
+            // 0.6491 ms, C3 even; profiles/r4_ab/saddr/ — not kept)
             const uint32_t *e = (e6 ? E6 : E4) + __umul24(ent, e6 ? kHybEnt6Dwords : kHybEnt4Dwords);
             if (UNCOND || valid[j]) {
                 A[j] = g3(e);

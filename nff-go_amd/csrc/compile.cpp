@@ -963,6 +963,7 @@ void build_hybrid(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vec
     if (flat && lds_dirs && !tuned && opt.fine_a > 0 && !opt.coarse) {
         const uint32_t fa = static_cast<uint32_t>(opt.fine_a), fp = static_cast<uint32_t>(opt.fine_p);
         static const uint32_t f1s[4] = {kFDst, kFSrc, kFDst, kFSrc}, f2s[4] = {kFDport, kFDport, kFSport, kFSport};
+        const uint32_t allowed = static_cast<uint32_t>(opt.fine_slots);  // bit k: positional slot 4 + k
         size_t fine_bytes = 0;
         for (int f = 0; f < 2; ++f) {
             FamilyPlan &pl = plan[f];
@@ -981,6 +982,7 @@ void build_hybrid(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vec
                     int best = -1;
                     double bc = own * opt.fine_gain;
                     for (int k = 0; k < 4; ++k) {
+                        if (!((allowed >> k) & 1u)) continue;
                         const double c = double(g[k].count(pl.rr[r])) / double(g[k].n_buckets());
                         if (c < bc) { bc = c; best = k; }
                     }
@@ -1169,6 +1171,25 @@ void build_hybrid(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vec
             for (size_t w = 0; w < words; ++w) blob.push_back(rel(2 * w) | rel(2 * w + 1) << 16);
         }
     while (blob.size() % 4) blob.push_back(0);
+    // flat-LDS positional forms: the slot parameter block (table.hpp
+    // kFlatParamDwords), staged with the directories (offsets < 2^16 dwords)
+    if (flat && lds_dirs && !compact) {  // (the image is < 2^16 dwords: kHybLdsDirMaxBytes)
+        out.off_params = static_cast<uint32_t>(blob.size());
+        for (uint32_t k = 0; k < kMaxSlots; ++k) {
+            uint32_t w[kFlatParamDwords] = {0, 0, 0, 0};
+            for (int f = 0; f < 2; ++f) {
+                const uint32_t sh = 16u * f;
+                if (k >= order[f].size()) continue;
+                const DimBuild &d = *order[f][k];
+                const DimInfo &di = fi[f]->dims[k];
+                w[0] |= (d.shift & 0xFFFFu) << sh;
+                w[1] |= (di.off_dir & 0xFFFFu) << sh;
+                w[2] |= (di.off_dir16 & 0xFFFFu) << sh;
+                w[3] |= ((d.bits2 & 0xFFu) | (d.shift2 & 0xFFu) << 8) << sh;
+            }
+            blob.insert(blob.end(), w, w + kFlatParamDwords);
+        }
+    }
     out.lds_dwords = lds_dirs ? static_cast<uint32_t>(blob.size()) : 0u;
     for (int f = 0; f < 2; ++f) {
         const bool v6 = f == 1;
@@ -1271,6 +1292,8 @@ bool CompileOptions::from_env(CompileOptions &o, std::string &err) {
     if (set) o.fine_gain = double(v) / 100.0;
     if (!env_knob("NFFACL_TUNE_FINE_MIN", 1, 1 << 20, v, set, err)) return false;
     if (set) o.fine_min = static_cast<int>(v);
+    if (!env_knob("NFFACL_TUNE_FINE_SLOTS", 1, 15, v, set, err)) return false;
+    if (set) o.fine_slots = static_cast<int>(v);
     if (!env_knob("NFFACL_TUNE_DIR_PER_RULE", 1, 64, v, set, err)) return false;
     if (set) o.dir_per_rule = static_cast<int>(v);
     return true;

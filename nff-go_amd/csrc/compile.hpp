@@ -70,6 +70,7 @@ struct CompiledTable {
     // idx*.used_slots = slots in use, all non-empty)
     bool slots_g = false;
     uint32_t off_empty_dir = 0;  // slots_g: dword offset of an empty directory {0, 0}
+    uint32_t off_params = 0;     // flat-LDS positional forms: the slot parameter block (table.hpp kFlatParams), 0 = none
 };
 
 // Table-layout overrides for tuning experiments (unset in production).
@@ -88,6 +89,7 @@ struct CompileOptions {
     int fine_p = 4;
     double fine_gain = 0.5;  // NFFACL_TUNE_FINE_G (1/100): a rule moves below this fraction of its 1-D cover
     int fine_min = 256;      // NFFACL_TUNE_FINE_MIN: fewest moved rules worth a fine slot
+    int fine_slots = 15;     // NFFACL_TUNE_FINE_SLOTS: bit k allows fine slot 4 + k
     int dir_per_rule = 4;    // NFFACL_TUNE_DIR_PER_RULE: LDS directory buckets per rule before the budget cut
     bool coarse = false;    // NFFACL_TUNE_COARSE: flat-LDS coarse address slots for short prefixes
                             // (C5 table 7.7 -> 3.7 MB but 0.722 vs 0.649 ms: off; profiles/r2_dir8/coarse/)

@@ -90,12 +90,13 @@ __device__ __forceinline__ uint32_t classify_any(const IndexedArgs &a, const Fie
         const uint32_t lane = lane_id();
         return classify_flat<NS, R, false>(a, f, W[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)], lane);
     }
-    if (TM == kTabFlatLds || TM == kTabFlatLds4 || TM == kTabFlatLds4U) {  // scratch after the staged directories (stage_dwords: multiple of 4)
+    if (TM == kTabFlatLds || TM == kTabFlatLds4 || TM == kTabFlatLds4U || TM == kTabFlatLdsG) {
+        // scratch after the staged directories (stage_dwords: multiple of 4)
         constexpr int R = TM == kTabFlatLds ? 2 : 4;
         FlatScratch<R> *W = reinterpret_cast<FlatScratch<R> *>(lds_tab + a.stage_dwords);
         const uint32_t lane = lane_id();
-        return classify_flat<NS, R, true, TM == kTabFlatLds4U>(a, f, W[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)],
-                                                               lane);
+        return classify_flat<NS, R, true, TM == kTabFlatLds4U || TM == kTabFlatLdsG, true, TM == kTabFlatLdsG>(
+            a, f, W[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)], lane);
     }
     if constexpr (NS <= 4) {  // per-lane walks: the positional four slots
         if (TM == kTabLds) return classify_indexed<NS, 1>(LdsTab{}, a, f);
@@ -181,7 +182,7 @@ k_indexed_slots(const uint8_t *__restrict__ slots, uint32_t stride, uint64_t n, 
         // it is VALU-bound, the select chain cost it 2.6 % (round 1), and
         // taking every option port from registers (no far read at all at
         // stride 64) 9 % (round 3, profiles/r3_ab/regports/)
-        constexpr bool REG = TM == kTabFlatLds || TM == kTabFlatLds4 || TM == kTabFlatLds4U;
+        constexpr bool REG = TM == kTabFlatLds || TM == kTabFlatLds4 || TM == kTabFlatLds4U || TM == kTabFlatLdsG;
         parse_fields<REG, TM == kTabLdsNP>(cur, live, f, [&](uint32_t k, uint32_t &lo, uint32_t &hi) {
             far_dwords(pkt, stride, k, lo, hi);
         }, a.flags);
@@ -448,6 +449,7 @@ static dev::IndexedArgs indexed_args(const DevTable *t) {
     };
     fam(t->meta.idx4, t->meta.off_rec4, a.f4);
     fam(t->meta.idx6, t->meta.off_rec6, a.f6);
+    a.off_params = hyb ? t->meta.off_params : 0u;
     a.live = 0;
     for (uint32_t k = 0; k < kMaxSlots; ++k)
         if (t->meta.slots_g || t->meta.idx4.dims[k].n_rules || t->meta.idx6.dims[k].n_rules) a.live |= 1u << k;
@@ -476,7 +478,10 @@ static bool table_consistent(const DevTable *t) {
     if (m.algo == NFFACL_ALGO_HYBRID && (m.lds_dwords == 0 || m.idx4.entry_dwords == kHybEnt4Dwords))
         return m.idx4.entry_dwords == kHybEnt4Dwords && m.idx6.entry_dwords == kHybEnt6Dwords &&
                m.off_rec4 <= dw && m.off_rec6 <= dw &&
-               size_t(m.lds_dwords) * sizeof(uint32_t) <= kHybLdsDirMaxBytes && m.lds_dwords <= dw;
+               size_t(m.lds_dwords) * sizeof(uint32_t) <= kHybLdsDirMaxBytes && m.lds_dwords <= dw &&
+               // flat-LDS positional forms read their slot parameters from the staged image
+               (m.lds_dwords == 0 || m.slots_g ||
+                (m.off_params > 0 && m.off_params + kFlatParamDwords * kMaxSlots <= m.lds_dwords));
     if (m.algo == NFFACL_ALGO_HYBRID)
         return size_t(m.lds_dwords) * sizeof(uint32_t) <= kLdsTableBytes && m.lds_dwords <= dw &&
                m.idx4.entry_dwords == kEnt4Dwords && m.idx6.entry_dwords == kEnt6Dwords;
@@ -509,6 +514,10 @@ static IndexedLaunch indexed_launch(const nffacl_engine *eng, const DevTable *t)
         const int rounds = tu.rounds ? tu.rounds : static_cast<int>(t->meta.flat_rounds);
         const bool r4 = rounds == 4 && lds4 <= kLdsBytes;
         L.tm = r4 ? (t->meta.flat_uncond ? dev::kTabFlatLds4U : dev::kTabFlatLds4) : dev::kTabFlatLds;
+        if (t->meta.slots_g) {  // generalized slots: the generic kernel (4 rounds)
+            L.tm = dev::kTabFlatLdsG;
+            L.lds_bytes = lds4;
+        }
         L.lds_bytes = r4 ? lds4 : image + sizeof(dev::FlatScratch<2>) * (L.block / 64);
         return L;
     }
@@ -554,7 +563,7 @@ template <int NS, int TM>
 static hipError_t allow_lds_modes() {
     hipError_t e = allow_lds(dev::k_indexed_slots<NS, TM, 0>);
     if (e == hipSuccess) e = allow_lds(dev::k_indexed_slots<NS, TM, 4>);
-    if (TM == dev::kTabFlatLds || TM == dev::kTabFlatLds4 || TM == dev::kTabFlatLds4U)
+    if (TM == dev::kTabFlatLds || TM == dev::kTabFlatLds4 || TM == dev::kTabFlatLds4U || TM == dev::kTabFlatLdsG)
         if (e == hipSuccess) e = allow_lds(dev::k_indexed_slots<NS, TM, 5>);
     if (TM == dev::kTabLds) {
         if (e == hipSuccess) e = allow_lds(dev::k_indexed_slots<NS, dev::kTabLds, 1>);
@@ -578,6 +587,7 @@ static void dispatch_indexed(int ns, int tm, F &&f) {
         case dev::kTabFlatLds: f(nsc, std::integral_constant<int, dev::kTabFlatLds>{}); break;
         case dev::kTabFlatLds4: f(nsc, std::integral_constant<int, dev::kTabFlatLds4>{}); break;
         case dev::kTabFlatLds4U: f(nsc, std::integral_constant<int, dev::kTabFlatLds4U>{}); break;
+        case dev::kTabFlatLdsG: f(nsc, std::integral_constant<int, dev::kTabFlatLdsG>{}); break;
         default: f(nsc, std::integral_constant<int, dev::kTabGlobal>{}); break;
         }
     };
@@ -588,6 +598,7 @@ static void dispatch_indexed(int ns, int tm, F &&f) {
         case dev::kTabFlatLds: f(nsc, std::integral_constant<int, dev::kTabFlatLds>{}); break;
         case dev::kTabFlatLds4: f(nsc, std::integral_constant<int, dev::kTabFlatLds4>{}); break;
         case dev::kTabFlatLds4U: f(nsc, std::integral_constant<int, dev::kTabFlatLds4U>{}); break;
+        case dev::kTabFlatLdsG: f(nsc, std::integral_constant<int, dev::kTabFlatLdsG>{}); break;
         default: f(nsc, std::integral_constant<int, dev::kTabFlat4>{}); break;
         }
     };
@@ -606,8 +617,9 @@ int prepare_kernels() {
     std::call_once(once, [] {
         for (int ns = 2; ns <= int(kMaxSlots); ++ns)
             for (int tm : {int(dev::kTabLds), int(dev::kTabLdsNP), int(dev::kTabSplit), int(dev::kTabFlatLds), int(dev::kTabFlatLds4),
-                           int(dev::kTabFlatLds4U)}) {
-                if (ns > 4 && tm != dev::kTabFlatLds && tm != dev::kTabFlatLds4 && tm != dev::kTabFlatLds4U)
+                           int(dev::kTabFlatLds4U), int(dev::kTabFlatLdsG)}) {
+                if (ns > 4 && tm != dev::kTabFlatLds && tm != dev::kTabFlatLds4 && tm != dev::kTabFlatLds4U &&
+                    tm != dev::kTabFlatLdsG)
                     continue;  // flat walks only
                 dispatch_indexed(ns, tm, [&](auto nsc, auto tmc) {
                     const hipError_t e = allow_lds_modes<decltype(nsc)::value, decltype(tmc)::value>();
@@ -628,7 +640,8 @@ static void launch_slots_tm(int mode, const IndexedLaunch &L, uint32_t grid, hip
                             uint32_t *d_port, uint64_t *d_permit) {
     const dim3 g(grid), b(L.block);
     const size_t lds = TM == dev::kTabGlobal ? 0 : L.lds_bytes;
-    if constexpr (TM == dev::kTabFlatLds || TM == dev::kTabFlatLds4 || TM == dev::kTabFlatLds4U) {  // load modes 0, 4, 5
+    if constexpr (TM == dev::kTabFlatLds || TM == dev::kTabFlatLds4 || TM == dev::kTabFlatLds4U ||
+                  TM == dev::kTabFlatLdsG) {  // load modes 0, 4, 5
         if (mode == 0)
             hipLaunchKernelGGL((dev::k_indexed_slots<NS, TM, 0>), g, b, lds, stream, d_slots, stride, n, a, d_port, d_permit);
         else if (mode == 5)
@@ -679,7 +692,7 @@ int launch_slots(nffacl_engine *eng, DevTable *t, const uint8_t *d_slots, uint32
         // batch's packets in flight: 0.6278 / 0.6312 vs 0.6340 / 0.6328 ms
         // (profiles/r3_ab/c5_mode5/); everything else to mode 4
         int mode = stride == 64 ? eng->tune.coal : 0;
-        if (stride == 64 && !eng->tune.coal_set && L.tm == dev::kTabFlatLds4U) mode = 5;
+        if (stride == 64 && !eng->tune.coal_set && (L.tm == dev::kTabFlatLds4U || L.tm == dev::kTabFlatLdsG)) mode = 5;
         dispatch_indexed(L.ns, L.tm, [&](auto nsc, auto tmc) {
             launch_slots_tm<decltype(nsc)::value, decltype(tmc)::value>(mode, L, grid, stream, d_slots, stride, n, a,
                                                                       d_port, d_permit);

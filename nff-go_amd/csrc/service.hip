@@ -662,6 +662,11 @@ struct nffacl_service {
     // burns the quota the others need: throughput = quota / CPU per call.
     int32_t sleep_ns = -1;
     uint32_t cpus = 1;
+    // requests written with non-temporal (streaming) stores + sfence: the
+    // lines go to memory, not into the writing core's cache, so the GPU's
+    // snooped PCIe reads of them need no cache-to-IO transfer
+    // (NFFACL_TUNE_SVC_NT)
+    bool nt = false;
     uint8_t *h_mem = nullptr;  // mapped, coherent pinned host memory: boxes | responses | ctrl
     uint8_t *h_box = nullptr;
     uint32_t *h_bell = nullptr;   // per mailbox: the tag of its latest request (written after the chunks)
@@ -1007,6 +1012,12 @@ int service_create(int hip_device, uint32_t mailboxes, uint32_t idle_us, bool bu
             return NFFACL_ERR_INVALID_ARG;
         }
         if (set) s->timeout_us = static_cast<uint64_t>(v);
+        if (!env_knob("NFFACL_TUNE_SVC_NT", 0, 1, v, set, err)) {
+            set_last_error(err);
+            release_service(s);
+            return NFFACL_ERR_INVALID_ARG;
+        }
+        if (set) s->nt = v != 0;
         s->cpus = cpu_budget();
     }
     const void *kern = burst ? reinterpret_cast<const void *>(dev::k_service_burst)
@@ -1051,6 +1062,7 @@ int post_and_wait(nffacl_service *s, MailboxState &m, uint32_t mb, DevTable *t, 
     for (int attempt = 0;; ++attempt) {
         const uint32_t tag = ++m.seq;
         post(tag, key);
+        if (s->nt) _mm_sfence();  // the streaming stores are visible before the bell
         __atomic_store_n(&s->h_bell[mb], tag, __ATOMIC_RELEASE);  // idle waves watch the bells
         std::atomic_thread_fence(std::memory_order_seq_cst);      // request visible before `running` is read
         if (!s->running.load(std::memory_order_seq_cst)) kick(s);
@@ -1113,6 +1125,7 @@ int post_and_wait(nffacl_service *s, MailboxState &m, uint32_t mb, DevTable *t, 
         // withdraw: same tag, no table; the table's retirement waits for the
         // consumer launch that may still hold the request
         post(tag, kSvcWithdrawn);
+        if (s->nt) _mm_sfence();
         std::atomic_thread_fence(std::memory_order_seq_cst);
         (void)t->note_use(s->stream);
         s->timeouts.fetch_add(1, std::memory_order_relaxed);
@@ -1121,8 +1134,13 @@ int post_and_wait(nffacl_service *s, MailboxState &m, uint32_t mb, DevTable *t, 
     }
 }
 
+inline void put16(__m128i *dst, __m128i v, bool nt) {
+    if (nt) _mm_stream_si128(dst, v);
+    else _mm_store_si128(dst, v);
+}
+
 // One packet as chunk payload (service.hpp): bytes [0, min(len, 80)), zero after.
-inline void packet_chunks(const uint8_t *frame, uint32_t len, uint32_t tag, __m128i *dst) {
+inline void packet_chunks(const uint8_t *frame, uint32_t len, uint32_t tag, __m128i *dst, bool nt) {
     alignas(16) uint8_t bytes[kSvcPktChunks * 12] = {0};
     const uint32_t n = std::min(len, kSvcSlot);
     if (n) std::memcpy(bytes, frame, n);
@@ -1130,12 +1148,12 @@ inline void packet_chunks(const uint8_t *frame, uint32_t len, uint32_t tag, __m1
     for (uint32_t j = 0; j < kSvcPktChunks; ++j) {
         std::memcpy(c, bytes + 12 * j, 12);
         c[3] = tag;
-        _mm_store_si128(dst + j, _mm_load_si128(reinterpret_cast<const __m128i *>(c)));
+        put16(dst + j, _mm_load_si128(reinterpret_cast<const __m128i *>(c)), nt);
     }
 }
 
-inline void store_chunk(__m128i *dst, uint32_t x, uint32_t y, uint32_t z, uint32_t w) {
-    _mm_store_si128(dst, _mm_set_epi32(static_cast<int>(w), static_cast<int>(z), static_cast<int>(y), static_cast<int>(x)));
+inline void store_chunk(__m128i *dst, uint32_t x, uint32_t y, uint32_t z, uint32_t w, bool nt) {
+    put16(dst, _mm_set_epi32(static_cast<int>(w), static_cast<int>(z), static_cast<int>(y), static_cast<int>(x)), nt);
 }
 
 }  // namespace
@@ -1176,9 +1194,10 @@ int nffacl_service_classify(nffacl_service *s, const nffacl_rules *rules, const 
         s, m, mb, t, live_key,
         [&](uint32_t tag, uint32_t key) {
             // the eight chunks (service.hpp), ascending: the tag chunk last (x86 stores stay in order)
-            packet_chunks(frame, len, tag, dst);
-            if (key == kSvcWithdrawn) store_chunk(dst + kSvcPktChunks, 0, 0, key, tag);
-            else store_chunk(dst + kSvcPktChunks, static_cast<uint32_t>(desc), static_cast<uint32_t>(desc >> 32), key, tag);
+            packet_chunks(frame, len, tag, dst, s->nt);
+            if (key == kSvcWithdrawn) store_chunk(dst + kSvcPktChunks, 0, 0, key, tag, s->nt);
+            else store_chunk(dst + kSvcPktChunks, static_cast<uint32_t>(desc), static_cast<uint32_t>(desc >> 32), key, tag,
+                             s->nt);
         },
         [&](uint32_t tag) {
             v = __atomic_load_n(r, __ATOMIC_ACQUIRE);
@@ -1228,10 +1247,10 @@ int nffacl_service_classify_burst(nffacl_service *s, const nffacl_rules *rules, 
             const uint32_t cnt = wd ? 1u : n;
             for (uint32_t i = 0; i < cnt; ++i)
                 packet_chunks(wd ? nullptr : frames[i], wd ? 0u : lens ? lens[i] : kSvcSlot, tag,
-                              dst + kSvcBurstHdrChunks + kSvcPktChunks * i);
-            store_chunk(dst + 1, cnt, 0, 0, tag);
-            if (wd) store_chunk(dst, 0, 0, key, tag);
-            else store_chunk(dst, static_cast<uint32_t>(desc), static_cast<uint32_t>(desc >> 32), key, tag);
+                              dst + kSvcBurstHdrChunks + kSvcPktChunks * i, s->nt);
+            store_chunk(dst + 1, cnt, 0, 0, tag, s->nt);
+            if (wd) store_chunk(dst, 0, 0, key, tag, s->nt);
+            else store_chunk(dst, static_cast<uint32_t>(desc), static_cast<uint32_t>(desc >> 32), key, tag, s->nt);
         },
         [&](uint32_t tag) {
             for (uint32_t i = n; i-- > 0;)  // (the words arrive in any order)

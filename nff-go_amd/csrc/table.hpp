@@ -140,6 +140,13 @@ enum KeyKind : uint32_t {
 
 // Slots per family in the HYBRID global-directory form (nffacl.h NFFACL_MAX_SLOTS).
 constexpr uint32_t kMaxSlots = 8;
+
+// Flat-LDS positional forms: the slot parameter block in the LDS image
+// (CompiledTable::off_params), kFlatParamDwords per slot s = 0..kMaxSlots-1,
+// each word holding the IPv4 value in bits 0..15 and the IPv6 value in 16..31:
+//   [0] shift  [1] directory offset  [2] two-level offsets' offset
+//   [3] fine 2-D grids: bits2 | shift2 << 8
+constexpr uint32_t kFlatParamDwords = 4;
 // Packet-side key fields of a slot (kernel key[] order): destination address
 // (IPv6: top 32 bits), source address, destination port, source port, zero.
 enum SlotField : uint32_t { kFDst = 0, kFSrc = 1, kFDport = 2, kFSport = 3, kFZero = 4 };

@@ -35,7 +35,7 @@ class FamInfo(ctypes.Structure):
 
 class TableInfo(ctypes.Structure):
     _fields_ = [("algo", ctypes.c_int32), ("lds_dwords", ctypes.c_uint32), ("blob_dwords", ctypes.c_uint64),
-                ("fam", FamInfo * 2)]
+                ("fam", FamInfo * 2), ("off_params", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
 
 
 def compile_table(rules: nffacl.L3Rules, algo=nffacl.ALGO_INDEXED):
@@ -494,3 +494,46 @@ def test_hybrid_c5_coarse_slots_and_directory_forms(coarse, dir8, monkeypatch):
         assert 4 not in kinds and kinds.count(0) == 2 and kinds.count(1) == 2
     else:
         assert info.fam[0].n_slots == 4
+
+
+def check_param_block(blob, info):
+    """The flat-LDS slot parameter block (table.hpp kFlatParamDwords) holds
+    each positional slot's shift, directory offsets and fine-grid bits for
+    both families, and lies inside the staged LDS image."""
+    assert info.off_params > 0 and info.off_params + 4 * MAX_SLOTS <= info.lds_dwords
+    P = blob[info.off_params:info.off_params + 4 * MAX_SLOTS].reshape(MAX_SLOTS, 4)
+    for f in range(2):
+        fi = info.fam[f]
+        for s in range(fi.n_slots):
+            d = fi.dims[s]
+            w = (P[s] >> np.uint32(16 * f)) & np.uint32(0xFFFF)
+            assert int(w[0]) == d.shift and int(w[1]) == d.off_dir and int(w[2]) == d.off_dir16, (f, s)
+            if s >= 4:
+                assert int(w[3]) & 0xFF == d.bits2 and int(w[3]) >> 8 == d.shift2, (f, s)
+
+
+@pytest.mark.parametrize("cfg,env", [
+    ("c5", {}),
+    ("c5", {"NFFACL_TUNE_FINE_A": "8", "NFFACL_TUNE_FINE_P": "4", "NFFACL_TUNE_FINE_MIN": "16"}),
+    ("c5", {"NFFACL_TUNE_FINE_A": "8", "NFFACL_TUNE_FINE_P": "3", "NFFACL_TUNE_FINE_SLOTS": "3"}),
+    ("c3", {"NFFACL_TUNE_FINE_A": "8", "NFFACL_TUNE_FINE_MIN": "16", "NFFACL_TUNE_DIR_PER_RULE": "16"}),
+])
+def test_hybrid_fine_slots_and_param_block(monkeypatch, cfg, env):
+    """Fine 2-D address x port grids (positional slots 4..7) and the LDS
+    parameter block: the emulated walk of the compiled blob equals the
+    oracle, the grids are 2-D slots on (address, port), and the parameter
+    block matches the slot table."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    g = synth.gen_rules(synth.SPECS[cfg], synth.RULE_SEEDS[cfg])
+    n = 1 << 13
+    slots = synth.gen_slots(g, n, synth.PACKET_SEEDS[cfg] + 3)
+    info = check_hybrid(g.text, slots, n)
+    rules = nffacl.L3Rules.parse_text(g.text)
+    blob, info = compile_table(rules, nffacl.ALGO_HYBRID)
+    check_param_block(blob, info)
+    fine = [info.fam[0].dims[k] for k in range(4, info.fam[0].n_slots) if info.fam[0].dims[k].n_rules]
+    if "NFFACL_TUNE_FINE_A" in env:
+        assert fine and all(d.kind2 != KIND_NONE for d in fine)
+    else:
+        assert not fine

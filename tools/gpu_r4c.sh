@@ -15,6 +15,7 @@ for c in c5 c3; do
   timeout -k 10 600 python tools/ab_env.py $c 4 base=NFFACL_AB:0 $V > "$OUT/ab_$c.json" 2> "$OUT/ab_$c.err" || exit 1
   python -c "import json,sys;d=json.load(open(sys.argv[1]));print(sys.argv[1], {k:(round(v['median_ms'],4),v['bit_exact_vs_first']) for k,v in d['variants'].items()})" "$OUT/ab_$c.json"
 done
+NOTEST=1 CFGS="c5 c3" ROUNDS=3 bash tools/gpu_libab.sh "$T/saddr" nff-go_amd/libnffacl.so nff-go_amd/build_exp/saddr0.so || exit 1
 NFFACL_BENCH_SHAPES="burst:1:32:1.0,burst:4:32:1.0,burst:16:32:1.5,burst:32:32:1.5,scalar:32:0:1.0" \
   timeout -k 10 300 python bench.py --extra none --no-cpu-baseline --no-host --steps 5 --warmup 2 \
     > "$OUT/bench_shapes.json" 2> "$OUT/bench_shapes.err" || exit 1
