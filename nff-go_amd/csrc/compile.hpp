@@ -85,12 +85,13 @@ struct CompileOptions {
     int uncond = -1;        // NFFACL_TUNE_UNCOND: flat-LDS branch-free entry loads (-1 = policy)
     // NFFACL_TUNE_FINE_A / _P: fine 2-D address x port slots of the flat-LDS
     // form (positional slots 4..7), a address bits x p port bits; a = 0: none
-    int fine_a = 0;
+    int fine_a = 8;          // 8 x 4 on slots 4-5: C5 0.583 vs 0.626 ms (profiles/r4_ab/fine/)
     int fine_p = 4;
     double fine_gain = 0.5;  // NFFACL_TUNE_FINE_G (1/100): a rule moves below this fraction of its 1-D cover
     int fine_min = 256;      // NFFACL_TUNE_FINE_MIN: fewest moved rules worth a fine slot
-    int fine_slots = 15;     // NFFACL_TUNE_FINE_SLOTS: bit k allows fine slot 4 + k
-    int dir_per_rule = 4;    // NFFACL_TUNE_DIR_PER_RULE: LDS directory buckets per rule before the budget cut
+    int fine_slots = 3;      // NFFACL_TUNE_FINE_SLOTS: bit k allows fine slot 4 + k (3: dst x dport, src x dport)
+    int dir_per_rule = 16;   // NFFACL_TUNE_DIR_PER_RULE: LDS directory buckets per rule before the budget cut
+                             // (C3 0.4005 vs 0.4122 ms at 4: profiles/r4_ab/fine/ab_c3_dir_per_rule.json)
     bool coarse = false;    // NFFACL_TUNE_COARSE: flat-LDS coarse address slots for short prefixes
                             // (C5 table 7.7 -> 3.7 MB but 0.722 vs 0.649 ms: off; profiles/r2_dir8/coarse/)
     // false (+ `err`) if a set variable is out of range

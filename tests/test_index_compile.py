@@ -487,6 +487,7 @@ def test_hybrid_c5_coarse_slots_and_directory_forms(coarse, dir8, monkeypatch):
     slots = synth.gen_slots(g, n, synth.PACKET_SEEDS["c5"])
     monkeypatch.setenv("NFFACL_TUNE_COARSE", coarse)
     monkeypatch.setenv("NFFACL_TUNE_DIR8", dir8)
+    monkeypatch.setenv("NFFACL_TUNE_FINE_A", "0")  # the four 1-D slots only (fine grids: below)
     info = check_hybrid(g.text, slots, n)
     assert info.fam[0].dims[0].dir8 == int(dir8)
     kinds = [info.fam[0].dims[k].kind for k in range(info.fam[0].n_slots)]
@@ -514,7 +515,9 @@ def check_param_block(blob, info):
 
 @pytest.mark.parametrize("cfg,env", [
     ("c5", {}),
-    ("c5", {"NFFACL_TUNE_FINE_A": "8", "NFFACL_TUNE_FINE_P": "4", "NFFACL_TUNE_FINE_MIN": "16"}),
+    ("c5", {"NFFACL_TUNE_FINE_A": "0"}),
+    ("c5", {"NFFACL_TUNE_FINE_A": "8", "NFFACL_TUNE_FINE_P": "4", "NFFACL_TUNE_FINE_MIN": "16",
+            "NFFACL_TUNE_FINE_SLOTS": "15"}),
     ("c5", {"NFFACL_TUNE_FINE_A": "8", "NFFACL_TUNE_FINE_P": "3", "NFFACL_TUNE_FINE_SLOTS": "3"}),
     ("c3", {"NFFACL_TUNE_FINE_A": "8", "NFFACL_TUNE_FINE_MIN": "16", "NFFACL_TUNE_DIR_PER_RULE": "16"}),
 ])
@@ -533,7 +536,9 @@ def test_hybrid_fine_slots_and_param_block(monkeypatch, cfg, env):
     blob, info = compile_table(rules, nffacl.ALGO_HYBRID)
     check_param_block(blob, info)
     fine = [info.fam[0].dims[k] for k in range(4, info.fam[0].n_slots) if info.fam[0].dims[k].n_rules]
-    if "NFFACL_TUNE_FINE_A" in env:
+    if env.get("NFFACL_TUNE_FINE_A") == "0":
+        assert not fine and info.fam[0].n_slots == 4
+    else:  # default: 8 x 4 grids on slots 4-5 (dst x dport, src x dport)
         assert fine and all(d.kind2 != KIND_NONE for d in fine)
-    else:
-        assert not fine
+        if cfg == "c5" and not env:
+            assert info.fam[0].n_slots == 6
