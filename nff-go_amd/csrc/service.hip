@@ -75,6 +75,7 @@ struct SvcArgs {
     uint64_t idle_ticks;    // leave after this long without a request (wall clock ticks)
     uint64_t hot_ticks;     // a mailbox answered within this window is read whole every pass
     uint64_t life_ticks;    // leave after this long in any case
+    uint32_t full_poll;     // burst consumer: hot waves read the whole mailbox every pass (NFFACL_TUNE_SVC_FULLPOLL)
 };
 
 // One 16-byte chunk of host memory, sc0 sc1 (past L1 and L2: host memory
@@ -357,11 +358,14 @@ __global__ void __launch_bounds__(64) k_service(SvcArgs a) {
 }
 
 // The burst consumer: one wave per burst mailbox (service.hpp), lane i
-// classifies packet i of the mailbox's request.  Polls as k_service: a hot
-// wave (answered within `hot`) reads its whole mailbox with kSvcBurstLoads
-// coalesced 1 KiB loads per pass (the next pass's loads issued before this
-// pass's request is classified), an idle wave reads only its bell word.  A
-// request is one rule set: no grouping, the descriptor is wave-uniform.
+// classifies packet i of the mailbox's request.  A hot wave (answered within
+// `hot`) polls only the mailbox's two header chunks (32 B) and reads the
+// packets' chunks once, when the header carries a new tag (full_poll: the
+// whole mailbox every pass); an idle wave reads only its bell word.  (Round 4: hot waves used to read the whole 3.6 KB mailbox every
+// pass; 16 of them kept ~45 GB/s of PCIe reads in flight against a ~58 GB/s
+// link and each poll took 4-5 us instead of the 1.2 us of an idle link —
+// tools/pcie_probe.hip, profiles/r4_service/.)  A request is one rule set:
+// no grouping, the descriptor is wave-uniform.
 __global__ void __launch_bounds__(64) k_service_burst(SvcArgs a) {
     __shared__ FlatScratch<2> W;
     __shared__ u32x4 img[64 * kSvcBurstLoads];
@@ -382,54 +386,36 @@ __global__ void __launch_bounds__(64) k_service_burst(SvcArgs a) {
     uint64_t n_polls = 0, poll_ticks = 0, n_groups = 0, group_ticks = 0, n_req = 0, n_torn = 0;
     const uint32_t box = mb * kSvcBurstBoxBytes;
     const uint32_t bell = a.box_bytes + mb * 4u;
-    constexpr uint32_t kTailLanes = (kSvcBurstChunks * 16 - (kSvcBurstLoads - 1) * 1024 + 15) / 16;
-    u32x4 nx[kSvcBurstLoads];
-    uint32_t nbell = 0;
-    uint64_t ncw = 0, nt = t0;
-    bool nhot = true;
-    auto issue = [&]() {
-        nt = wall_clock64();
-        nhot = nt - ans_last <= a.hot_ticks;  // wave-uniform
-#pragma unroll
-        for (uint32_t j = 0; j < kSvcBurstLoads; ++j) nx[j] = u32x4{0, 0, 0, 0};
-        nbell = 0;
-        if (nhot) {
-#pragma unroll
-            for (uint32_t j = 0; j < kSvcBurstLoads; ++j)
-                if (j + 1 < kSvcBurstLoads || lane < kTailLanes) nx[j] = ld16_host(rs, box + 1024u * j + 16u * lane);
-        } else if (lane == 0) {
-            nbell = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(bell), 0, 17);
-        }
-        ncw = 0;  // stop | restart << 32
-        if (lane == 0) ncw = __hip_atomic_load(reinterpret_cast<uint64_t *>(a.ctrl), __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_SYSTEM);
-    };
-    issue();
     while (true) {
-        const uint64_t cw = ncw, now = nt;
-        const bool hot = nhot;
-        u32x4 h0 = u32x4{0, 0, 0, 0}, h1 = u32x4{0, 0, 0, 0}, c[kSvcPktChunks];
-        if (hot) {  // the poll issued a pass ago, through LDS: lane i gets packet i's chunks
-#pragma unroll
-            for (uint32_t j = 0; j < kSvcBurstLoads; ++j) img[64u * j + lane] = nx[j];
-            wave_lds_sync();
-            h0 = img[0];
-            h1 = img[1];
-#pragma unroll
-            for (uint32_t j = 0; j < kSvcPktChunks; ++j)
-                c[j] = lane < kSvcBurstMax ? img[kSvcBurstHdrChunks + kSvcPktChunks * lane + j] : u32x4{0, 0, 0, 0};
-            wave_lds_sync();
-        } else {
-            h0.w = __builtin_amdgcn_readfirstlane(nbell);
-#pragma unroll
-            for (uint32_t j = 0; j < kSvcPktChunks; ++j) c[j] = u32x4{0, 0, 0, 0};
-        }
+        // one poll per pass, issued here: a poll issued before the answer is
+        // out can never hold the caller's next request (it waits for the
+        // answer), and a second poll in flight doubles the reads (round 4:
+        // pre-issued polls, 11.6 vs 6.4 us per call at one clone)
+        const uint64_t now = wall_clock64();
         if (now - t0 > a.life_ticks) break;
-        issue();  // the next pass's poll, in flight from here
+        const bool hot = now - ans_last <= a.hot_ticks;  // wave-uniform
+        u32x4 hh = u32x4{0, 0, 0, 0};  // lane 0 chunk 0, lane 1 chunk 1
+        u32x4 body[kSvcBurstLoads];
+#pragma unroll
+        for (uint32_t j = 0; j < kSvcBurstLoads; ++j) body[j] = u32x4{0, 0, 0, 0};
+        uint32_t bl = 0;
+        uint64_t cw = 0;  // stop | restart << 32
+        if (hot && a.full_poll) {
+#pragma unroll
+            for (uint32_t j = 0; j < kSvcBurstLoads; ++j) body[j] = ld16_host(rs, box + 1024u * j + 16u * lane);
+            hh = body[0];
+        } else if (hot) {
+            if (lane < kSvcBurstHdrChunks) hh = ld16_host(rs, box + 16u * lane);
+        } else if (lane == 0) {
+            bl = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(bell), 0, 17);
+        }
+        if (lane == 0) cw = __hip_atomic_load(reinterpret_cast<uint64_t *>(a.ctrl), __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_SYSTEM);
+        const uint32_t tag = hot ? static_cast<uint32_t>(__builtin_amdgcn_readlane(hh.w, 0))
+                                 : static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(bl));
         if ((__builtin_amdgcn_readlane(static_cast<uint32_t>(cw), 0) |
              __builtin_amdgcn_readlane(static_cast<uint32_t>(cw >> 32), 0)) != 0u)
             break;
-        const uint32_t tag = __builtin_amdgcn_readfirstlane(h0.w);
         const uint64_t t_data = wall_clock64();
         ++n_polls;
         poll_ticks += t_data - now;
@@ -438,20 +424,44 @@ __global__ void __launch_bounds__(64) k_service_burst(SvcArgs a) {
             continue;
         }
         last = now;
-        if (!hot) {  // a new tag on the bell: the request is read whole from the poll after next
+        if (!hot) {  // a new tag on the bell: the next pass polls the header
             ans_last = now;
             continue;
         }
-        // complete when every chunk of the header and of packets 0..n-1 carries the tag
-        const uint32_t n = __builtin_amdgcn_readfirstlane(h1.x);
+        // header complete (both chunks carry the tag): read the packets' chunks
+        const uint32_t n = __builtin_amdgcn_readlane(hh.x, 1);
+        if (static_cast<uint32_t>(__builtin_amdgcn_readlane(hh.w, 1)) != tag || n == 0u || n > kSvcBurstMax) {
+            ++n_torn;  // raced the host's stores: the next poll has it
+            continue;
+        }
+        if (!a.full_poll) {
+            const uint32_t nl = ((kSvcBurstHdrChunks + kSvcPktChunks * n) * 16u + 1023u) / 1024u;  // 1 KiB loads
+#pragma unroll
+            for (uint32_t j = 0; j < kSvcBurstLoads; ++j)
+                body[j] = j < nl ? ld16_host(rs, box + 1024u * j + 16u * lane) : u32x4{0, 0, 0, 0};
+        }
+        // through LDS: lane i gets packet i's chunks
+#pragma unroll
+        for (uint32_t j = 0; j < kSvcBurstLoads; ++j) img[64u * j + lane] = body[j];
+        wave_lds_sync();
+        u32x4 c[kSvcPktChunks];
+#pragma unroll
+        for (uint32_t j = 0; j < kSvcPktChunks; ++j)
+            c[j] = lane < kSvcBurstMax ? img[kSvcBurstHdrChunks + kSvcPktChunks * lane + j] : u32x4{0, 0, 0, 0};
+        wave_lds_sync();
+        // complete when every chunk of packets 0..n-1 carries the tag
         const bool live = lane < n;
-        bool torn = h1.w != tag || n == 0u || n > kSvcBurstMax;
+        bool torn = false;
 #pragma unroll
         for (uint32_t j = 0; j < kSvcPktChunks; ++j) torn = torn || (live && c[j].w != tag);
-        if (ballot(torn)) {  // raced the host's stores: the next poll has it
+        if (ballot(torn)) {  // the packets' stores not all visible yet: the next poll re-reads them
             ++n_torn;
             continue;
         }
+        u32x4 h0;
+        h0.x = __builtin_amdgcn_readlane(hh.x, 0);
+        h0.y = __builtin_amdgcn_readlane(hh.y, 0);
+        h0.z = __builtin_amdgcn_readlane(hh.z, 0);
         const uint64_t t_group = wall_clock64();
         const uint32_t key = __builtin_amdgcn_readfirstlane(h0.z);
         if (key == kSvcWithdrawn) {  // the caller gave up: answered, no table read
@@ -1018,6 +1028,12 @@ int service_create(int hip_device, uint32_t mailboxes, uint32_t idle_us, bool bu
             return NFFACL_ERR_INVALID_ARG;
         }
         if (set) s->nt = v != 0;
+        if (!env_knob("NFFACL_TUNE_SVC_FULLPOLL", 0, 1, v, set, err)) {
+            set_last_error(err);
+            release_service(s);
+            return NFFACL_ERR_INVALID_ARG;
+        }
+        s->args.full_poll = set && v != 0 ? 1u : 0u;
         s->cpus = cpu_budget();
     }
     const void *kern = burst ? reinterpret_cast<const void *>(dev::k_service_burst)
@@ -1139,17 +1155,30 @@ inline void put16(__m128i *dst, __m128i v, bool nt) {
     else _mm_store_si128(dst, v);
 }
 
-// One packet as chunk payload (service.hpp): bytes [0, min(len, 80)), zero after.
+// One packet as chunk payload (service.hpp): bytes [0, min(len, 80)), zero
+// after, 12 per chunk with the tag in word 3.  A whole 80-byte prefix is read
+// straight from the frame (chunks 0-5: 16-byte loads ending at byte 76; chunk
+// 6: bytes 72-79); shorter frames go through a zeroed copy.  (Round 4: the
+// byte-wise copy took 2.4 us per 32-packet burst on the host — a third of a
+// burst call — against 0.2-0.5 us for this.)
 inline void packet_chunks(const uint8_t *frame, uint32_t len, uint32_t tag, __m128i *dst, bool nt) {
-    alignas(16) uint8_t bytes[kSvcPktChunks * 12] = {0};
-    const uint32_t n = std::min(len, kSvcSlot);
-    if (n) std::memcpy(bytes, frame, n);
-    alignas(16) uint32_t c[4];
-    for (uint32_t j = 0; j < kSvcPktChunks; ++j) {
-        std::memcpy(c, bytes + 12 * j, 12);
-        c[3] = tag;
-        put16(dst + j, _mm_load_si128(reinterpret_cast<const __m128i *>(c)), nt);
+    static_assert(kSvcPktChunks == 7 && kSvcSlot == 80, "six 16-byte loads + one 8-byte load per packet");
+    const __m128i keep = _mm_set_epi32(0, -1, -1, -1);
+    const __m128i t = _mm_set_epi32(static_cast<int>(tag), 0, 0, 0);
+    alignas(16) uint8_t b[96];
+    const uint8_t *src = frame;
+    if (len < kSvcSlot) {
+        std::memset(b, 0, sizeof b);
+        if (len) std::memcpy(b, frame, len);
+        src = b;
     }
+    for (uint32_t j = 0; j + 1 < kSvcPktChunks; ++j) {
+        const __m128i v = _mm_loadu_si128(reinterpret_cast<const __m128i *>(src + 12 * j));
+        put16(dst + j, _mm_or_si128(_mm_and_si128(v, keep), t), nt);
+    }
+    // bytes 72-79, then zeros (80-83) and the tag
+    const __m128i last = _mm_loadl_epi64(reinterpret_cast<const __m128i *>(src + 12 * (kSvcPktChunks - 1)));
+    put16(dst + kSvcPktChunks - 1, _mm_or_si128(last, t), nt);
 }
 
 inline void store_chunk(__m128i *dst, uint32_t x, uint32_t y, uint32_t z, uint32_t w, bool nt) {
@@ -1249,6 +1278,9 @@ int nffacl_service_classify_burst(nffacl_service *s, const nffacl_rules *rules, 
                 packet_chunks(wd ? nullptr : frames[i], wd ? 0u : lens ? lens[i] : kSvcSlot, tag,
                               dst + kSvcBurstHdrChunks + kSvcPktChunks * i, s->nt);
             store_chunk(dst + 1, cnt, 0, 0, tag, s->nt);
+            // the consumer reads the packets only once the header carries the
+            // tag: the header chunk goes last (streaming stores: after a fence)
+            if (s->nt) _mm_sfence();
             if (wd) store_chunk(dst, 0, 0, key, tag, s->nt);
             else store_chunk(dst, static_cast<uint32_t>(desc), static_cast<uint32_t>(desc >> 32), key, tag, s->nt);
         },
