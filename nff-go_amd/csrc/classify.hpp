@@ -693,34 +693,18 @@ __device__ __forceinline__ uint32_t prefix_mask(uint32_t L) {
 // 12-byte pieces of the exact flat-form entries (table.hpp): an IPv4 entry
 // is two (the compiler issues dwordx4 + dwordx2), an IPv6 entry four.
 typedef uint32_t u32x3 __attribute__((ext_vector_type(3), aligned(4)));
-typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
-typedef uint32_t u32x2 __attribute__((ext_vector_type(2), aligned(4)));
-#ifndef NFFACL_EXP_R4
-#define NFFACL_EXP_R4 4  // rounds per window of the "4-round" flat-LDS kernels (experiment builds only)
-#endif
-#ifndef NFFACL_EXP_FLAT
-#define NFFACL_EXP_FLAT 0  // flat-walk timing probes, bit mask (experiment builds only; see classify_flat)
-#endif
-#ifndef NFFACL_EXP_ENTLOAD
-#define NFFACL_EXP_ENTLOAD 0  // flat-walk entry-load timing probes (experiment builds only)
-#endif
 
 __device__ __forceinline__ u32x3 ld3(const uint32_t *__restrict__ p) { return *reinterpret_cast<const u32x3 *>(p); }
 
-// Two-stage test of an exact flat-form entry (table.hpp), both families.
-// Stage 1, the entry's first 16 bytes P = {lo, hi, meta, lens}: protocol and
-// ports (acl.go:517-519, 530/548) — at C5 they reject 84 % of the candidates
-// that stage 2's addresses would let through.  Stage 2, the next 8 bytes
-// {src, dst top words, big-endian}: the addresses under the prefix lengths in
-// P.w (acl.go:526-529 / 546-547; IPv6: capped at 32, the rest below).
-__device__ __forceinline__ uint32_t hyb_miss_l4(const u32x4 &P, uint32_t proto, uint32_t ports) {
-    const uint32_t pm = ((proto ^ P.z) & 0xFFu) & (0u - ((P.z >> 8) & 1u));
-    return pm | port_miss(ports, P.x, P.y);
-}
-
-__device__ __forceinline__ uint32_t hyb_miss_l3(uint32_t lens, uint32_t sa, uint32_t da, uint32_t ks, uint32_t kd) {
-    const uint32_t sl = min(lens & 0xFFu, 32u), dl = min((lens >> 8) & 0xFFu, 32u);
-    return ((ks ^ sa) & prefix_mask(sl)) | ((kd ^ da) & prefix_mask(dl));
+// Mismatch bits of an exact entry's first six words (both families): top
+// address words under their prefix lengths (IPv6: capped at 32), protocol,
+// ports — acl.go:526-539 / 546-557 for IPv4 completely, for IPv6 up to the
+// low address words.  ks/kd: big-endian src/dst (top) words.
+__device__ __forceinline__ uint32_t hyb_miss(const u32x3 &A, const u32x3 &B, uint32_t ks, uint32_t kd, uint32_t proto,
+                                             uint32_t ports) {
+    const uint32_t sl = min(B.z & 0xFFu, 32u), dl = min((B.z >> 8) & 0xFFu, 32u);
+    const uint32_t pm = ((proto ^ A.z) & 0xFFu) & (0u - ((A.z >> 8) & 1u));
+    return ((ks ^ A.x) & prefix_mask(sl)) | ((kd ^ A.y) & prefix_mask(dl)) | pm | port_miss(ports, B.x, B.y);
 }
 
 // IPv6 address words 1..3 of an exact entry (C = src1 src2 src3, D = dst1
@@ -821,18 +805,15 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
     // The persistent consumer (DIRS_IN_LDS == false) reads the table with
     // bounds checks: a word outside it reads as 0 and raises the host flag
     // a.oob (reported by nffacl_service_get_stats) instead of faulting.
-    auto inside = [&](const uint32_t *p, uint32_t n) -> bool {
-        if (DIRS_IN_LDS) return true;
-        if (static_cast<uint64_t>(p - a.tab) + n <= a.tab_dwords) return true;
-        __hip_atomic_store(a.oob, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        return false;
-    };
-    auto g3 = [&](const uint32_t *p) -> u32x3 { return inside(p, 3) ? ld3(p) : u32x3{0, 0, 0}; };
-    auto g4 = [&](const uint32_t *p) -> u32x4 {
-        return inside(p, 4) ? *reinterpret_cast<const u32x4a4 *>(p) : u32x4{0, 0, 0, 0};
-    };
-    auto g2 = [&](const uint32_t *p) -> u32x2 {
-        return inside(p, 2) ? *reinterpret_cast<const u32x2 *>(p) : u32x2{0, 0};
+    auto g3 = [&](const uint32_t *p) -> u32x3 {
+        if (!DIRS_IN_LDS) {
+            const uint64_t off = static_cast<uint64_t>(p - a.tab);
+            if (off + 3u > a.tab_dwords) {
+                __hip_atomic_store(a.oob, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                return u32x3{0, 0, 0};
+            }
+        }
+        return ld3(p);
     };
     auto g1 = [&](uint32_t i) -> uint32_t {
         if (!DIRS_IN_LDS && i >= a.tab_dwords) {
@@ -964,10 +945,9 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
         // hold lanes past the wave's candidates (the per-round k < T test
         // stays: with it compiled out the scheduler hoists more loads, and
         // the frames kernels spill at 128 VGPRs).
-        uint32_t owner[RR], oproto[RR];
+        uint32_t owner[RR], idx[RR], oproto[RR];
         bool valid[RR], six[RR];
-        u32x4 P[RR];                 // stage 1: {lo, hi, meta, lens}
-        const uint32_t *ep[RR];      // the candidates' entries (stage 2 reads on)
+        u32x3 A[RR], B[RR], C[RR], D[RR];
         // the rounds' prefix-max scans are independent (only their carries
         // chain): issued together, their DPP steps interleave instead of
         // waiting out each other's data hazards
@@ -997,52 +977,28 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
             // (round 4: one uniform base + a 32-bit byte offset per entry, the
             // saddr load form, -56 static VALU: C5 0.6547 / 0.6527 vs 0.6520 /
             // 0.6491 ms, C3 even; profiles/r4_ab/saddr/ — not kept)
-            ep[j] = (e6 ? E6 : E4) + __umul24(ent, e6 ? kHybEnt6Dwords : kHybEnt4Dwords);
-#if NFFACL_EXP_ENTLOAD == 2  // timing probe: no entry loads (verdicts wrong)
-            const uint32_t z = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(ep[j]));
-            P[j] = u32x4{z >> 3, z | 0xFFFF0000u, z << 4, z & 0xFFFFu};
-#else
-            P[j] = UNCOND || valid[j] ? g4(ep[j]) : u32x4{0, 0, 0, 0};
-#endif
+            const uint32_t *e = (e6 ? E6 : E4) + __umul24(ent, e6 ? kHybEnt6Dwords : kHybEnt4Dwords);
+            if (UNCOND || valid[j]) {
+                A[j] = g3(e);
+                B[j] = g3(e + 3);
+            } else {
+                A[j] = B[j] = u32x3{0, 0, 0};
+            }
+            if (valid[j] && six[j]) {  // (C, D are read only for valid IPv6 candidates)
+                C[j] = g3(e + 6);
+                D[j] = g3(e + 9);
+            }
         }
-        // stage 1: protocol and ports of the owner packet
         bool pass[RR];
-#pragma unroll
-        for (int j = 0; j < RR; ++j) {
-#if NFFACL_EXP_FLAT & 32  // timing probe: 16 extra dependent VALU per round (verdicts right)
-            {
-                uint32_t x = P[j].x;
-#pragma unroll
-                for (int q = 0; q < 16; ++q) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(x) : "v"(lane));
-                valid[j] = valid[j] && x != 0xFFFFFFFFu - 1u - P[j].x + P[j].x;
-            }
-#endif
-            const uint32_t opt = bperm(f.ports, owner[j]);
-            pass[j] = valid[j] && hyb_miss_l4(P[j], oproto[j], opt) == 0u;
-        }
-        // stage 2, for the candidates stage 1 let through: the top address
-        // words (IPv6: all four pieces' worth), every round's loads issued
-        // before any is tested
-        u32x2 Q[RR];
-        u32x3 C[RR], D[RR];
-#pragma unroll
-        for (int j = 0; j < RR; ++j) {
-            Q[j] = u32x2{0, 0};
-            if (pass[j]) {
-                Q[j] = g2(ep[j] + 4);
-                if (six[j]) {
-                    C[j] = g3(ep[j] + 6);
-                    D[j] = g3(ep[j] + 9);
-                }
-            }
-        }
         bool any6 = false;
 #pragma unroll
         for (int j = 0; j < RR; ++j) {
-            if (ballot(pass[j])) {  // whole wave: bpermute reads every lane
-                const uint32_t oks = bperm(ks, owner[j]), okd = bperm(kd, owner[j]);
-                pass[j] = pass[j] && hyb_miss_l3(P[j].w, Q[j].x, Q[j].y, oks, okd) == 0u;
-            }
+            // the owner packet's fields
+            const uint32_t o = owner[j];
+            const uint32_t oks = bperm(ks, o), okd = bperm(kd, o);
+            const uint32_t opt = bperm(f.ports, o);
+            pass[j] = valid[j] && hyb_miss(A[j], B[j], oks, okd, oproto[j], opt) == 0u;
+            idx[j] = A[j].z >> kEntIndexShift;
             any6 |= pass[j] && six[j];
         }
         if (ballot(any6)) {  // IPv6 candidates: address words 1..3 of the owner
@@ -1061,7 +1017,7 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
                         os[q] = bperm(sb[q], owner[j]);
                         ot[q] = bperm(tb[q], owner[j]);
                     }
-                    if (pass[j] && six[j]) pass[j] = hyb_miss6(C[j], D[j], P[j].w, os, ot) == 0u;
+                    if (pass[j] && six[j]) pass[j] = hyb_miss6(C[j], D[j], B[j].z, os, ot) == 0u;
                 }
             }
         }
@@ -1070,22 +1026,20 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
 #pragma unroll
         for (int j = 0; j < RR; ++j)  // rule index << 32 | output code: the minimum carries the winner's output
             if (pass[j]) atomicMin(reinterpret_cast<unsigned long long *>(&W.best[owner[j]]),
-                                   static_cast<unsigned long long>(P[j].z >> kEntIndexShift) << 32 |
-                                       (P[j].w >> kHybOutShift));
+                                   static_cast<unsigned long long>(idx[j]) << 32 | (B[j].z >> kHybOutShift));
         wave_lds_sync();
     };
+    // (a mark carries its window position in 8 bits: at most 256 positions,
+    // R <= 4 — an R = 5 experiment build faulted the GPU on out-of-range
+    // entry numbers in round 4)
+    static_assert(R >= 1 && R <= 4, "window positions are 8-bit fields of the marks");
     using I1 = std::integral_constant<int, 1>;
     using I2 = std::integral_constant<int, 2>;
     using I3 = std::integral_constant<int, (R >= 3 ? 3 : R)>;
-    using I4 = std::integral_constant<int, (R >= 4 ? 4 : R)>;
-    using I5 = std::integral_constant<int, (R >= 5 ? 5 : R)>;
     using IR = std::integral_constant<int, R>;
-    static_assert(R <= 6, "window dispatch covers up to 6 rounds");
-    for (uint32_t win = 0; win < ((NFFACL_EXP_FLAT & 16) ? 0u : T); win += 64 * R) {
+    for (uint32_t win = 0; win < T; win += 64 * R) {
         const uint32_t rem = T - win;  // wave-uniform
         if (rem > 64u * (R - 1)) window(win, IR{});
-        else if (R >= 6 && rem > 256u) window(win, I5{});
-        else if (R >= 5 && rem > 192u) window(win, I4{});
         else if (R >= 3 && rem > 128u) window(win, I3{});
         else if (rem > 64u) window(win, I2{});
         else window(win, I1{});
@@ -1099,12 +1053,11 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
         const uint32_t ew = fam ? kHybEnt6Dwords : kHybEnt4Dwords;
         for (uint32_t i = 0; i < fa.n_resid; ++i) {
             const uint32_t *e = a.tab + fa.off_resid + i * ew;
-            const u32x4 RP = g4(e);
-            const uint32_t ri = RP.z >> kEntIndexShift;
+            const u32x3 RA = g3(e), RB = g3(e + 3);
+            const uint32_t ri = RA.z >> kEntIndexShift;
             const bool want = in_fam && ri < uint32_t(best >> 32);
             if (!ballot(want)) break;  // residual list ascends too
-            const u32x2 RQ = g2(e + 4);
-            bool ok = want && (hyb_miss_l4(RP, f.proto, f.ports) | hyb_miss_l3(RP.w, RQ.x, RQ.y, ks, kd)) == 0u;
+            bool ok = want && hyb_miss(RA, RB, ks, kd, f.proto, f.ports) == 0u;
             if (fam && ballot(ok)) {
                 uint32_t sb[4] = {0, 0, 0, 0}, tb[4] = {0, 0, 0, 0};
 #pragma unroll
@@ -1112,9 +1065,9 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
                     sb[q] = __builtin_bswap32(f.s[q]);
                     tb[q] = __builtin_bswap32(f.t[q]);
                 }
-                if (ok) ok = hyb_miss6(g3(e + 6), g3(e + 9), RP.w, sb, tb) == 0u;
+                if (ok) ok = hyb_miss6(g3(e + 6), g3(e + 9), RB.z, sb, tb) == 0u;
             }
-            best = ok ? (uint64_t(ri) << 32 | (RP.w >> kHybOutShift)) : best;
+            best = ok ? (uint64_t(ri) << 32 | (RB.z >> kHybOutShift)) : best;
         }
     }
     // output numbers below kHybOutEscape travel in the entry; others come from the output array

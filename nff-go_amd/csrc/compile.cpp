@@ -400,10 +400,8 @@ void emit_hyb_entry(const uint32_t *rec, bool v6, uint32_t r, std::vector<uint32
     const uint32_t output = v6 ? rec[19] : rec[7];
     const uint32_t ocode = std::min(output, kHybOutEscape);
     const uint32_t sa = v6 ? rec[0] : rec[0], da = v6 ? rec[8] : rec[2];
-    // stage-1 words (protocol, ports, lengths) first: the walk reads them for
-    // every candidate and the address words only for those they let through
-    blob.insert(blob.end(), {lo, hi, (m[0] & 0xFFu) | exact | (r << kEntIndexShift), sl | dl << 8 | ocode << kHybOutShift,
-                             bswap32(sa), bswap32(da)});
+    blob.insert(blob.end(), {bswap32(sa), bswap32(da), (m[0] & 0xFFu) | exact | (r << kEntIndexShift), lo, hi,
+                             sl | dl << 8 | ocode << kHybOutShift});
     if (v6)
         blob.insert(blob.end(), {bswap32(rec[1]), bswap32(rec[2]), bswap32(rec[3]),
                                  bswap32(rec[9]), bswap32(rec[10]), bswap32(rec[11])});

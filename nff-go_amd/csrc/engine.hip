@@ -92,7 +92,7 @@ __device__ __forceinline__ uint32_t classify_any(const IndexedArgs &a, const Fie
     }
     if (TM == kTabFlatLds || TM == kTabFlatLds4 || TM == kTabFlatLds4U || TM == kTabFlatLdsG) {
         // scratch after the staged directories (stage_dwords: multiple of 4)
-        constexpr int R = TM == kTabFlatLds ? 2 : NFFACL_EXP_R4;
+        constexpr int R = TM == kTabFlatLds ? 2 : 4;
         FlatScratch<R> *W = reinterpret_cast<FlatScratch<R> *>(lds_tab + a.stage_dwords);
         const uint32_t lane = lane_id();
         return classify_flat<NS, R, true, TM == kTabFlatLds4U || TM == kTabFlatLdsG, true, TM == kTabFlatLdsG>(
@@ -510,7 +510,7 @@ static IndexedLaunch indexed_launch(const nffacl_engine *eng, const DevTable *t)
         L.block = tu.block ? static_cast<uint32_t>(tu.block) : 1024u;
         L.per_cu = tu.per_cu ? static_cast<uint32_t>(tu.per_cu) : 1u;
         const size_t image = size_t(t->meta.lds_dwords) * sizeof(uint32_t);
-        const size_t lds4 = image + sizeof(dev::FlatScratch<NFFACL_EXP_R4>) * (L.block / 64);
+        const size_t lds4 = image + sizeof(dev::FlatScratch<4>) * (L.block / 64);
         const int rounds = tu.rounds ? tu.rounds : static_cast<int>(t->meta.flat_rounds);
         const bool r4 = rounds == 4 && lds4 <= kLdsBytes;
         L.tm = r4 ? (t->meta.flat_uncond ? dev::kTabFlatLds4U : dev::kTabFlatLds4) : dev::kTabFlatLds;

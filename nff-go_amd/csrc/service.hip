@@ -75,7 +75,8 @@ struct SvcArgs {
     uint64_t idle_ticks;    // leave after this long without a request (wall clock ticks)
     uint64_t hot_ticks;     // a mailbox answered within this window is read whole every pass
     uint64_t life_ticks;    // leave after this long in any case
-    uint32_t full_poll;     // burst consumer: hot waves read the whole mailbox every pass (NFFACL_TUNE_SVC_FULLPOLL)
+    uint32_t full_poll;     // burst consumer: hot waves read the whole mailbox every pass (default; 0: the
+                            // header, then the packets on a new tag — NFFACL_TUNE_SVC_FULLPOLL=0)
 };
 
 // One 16-byte chunk of host memory, sc0 sc1 (past L1 and L2: host memory
@@ -359,12 +360,14 @@ __global__ void __launch_bounds__(64) k_service(SvcArgs a) {
 
 // The burst consumer: one wave per burst mailbox (service.hpp), lane i
 // classifies packet i of the mailbox's request.  A hot wave (answered within
-// `hot`) polls only the mailbox's two header chunks (32 B) and reads the
-// packets' chunks once, when the header carries a new tag (full_poll: the
-// whole mailbox every pass); an idle wave reads only its bell word.  (Round 4: hot waves used to read the whole 3.6 KB mailbox every
-// pass; 16 of them kept ~45 GB/s of PCIe reads in flight against a ~58 GB/s
-// link and each poll took 4-5 us instead of the 1.2 us of an idle link —
-// tools/pcie_probe.hip, profiles/r4_service/.)  A request is one rule set:
+// `hot`) reads its whole mailbox (3.6 KB, four 1 KiB loads) once per pass and
+// issues the next pass's poll only after answering: a poll issued before the
+// answer is out can never hold the caller's next request, it only loads the
+// PCIe link.  An idle wave reads only its bell word.  (Round 4, C2 rules,
+// 16 / 32 clones: polls issued a pass ahead 55 / 103 Mpps; header-only polls
+// + one read of the packets per request (full_poll = 0,
+// NFFACL_TUNE_SVC_FULLPOLL=0) 56 / 103; whole-mailbox polls issued after
+// the answer 67 / 132 — profiles/r4_service/.)  A request is one rule set:
 // no grouping, the descriptor is wave-uniform.
 __global__ void __launch_bounds__(64) k_service_burst(SvcArgs a) {
     __shared__ FlatScratch<2> W;
@@ -387,10 +390,7 @@ __global__ void __launch_bounds__(64) k_service_burst(SvcArgs a) {
     const uint32_t box = mb * kSvcBurstBoxBytes;
     const uint32_t bell = a.box_bytes + mb * 4u;
     while (true) {
-        // one poll per pass, issued here: a poll issued before the answer is
-        // out can never hold the caller's next request (it waits for the
-        // answer), and a second poll in flight doubles the reads (round 4:
-        // pre-issued polls, 11.6 vs 6.4 us per call at one clone)
+        // one poll per pass, issued here (see above)
         const uint64_t now = wall_clock64();
         if (now - t0 > a.life_ticks) break;
         const bool hot = now - ans_last <= a.hot_ticks;  // wave-uniform
@@ -1033,7 +1033,7 @@ int service_create(int hip_device, uint32_t mailboxes, uint32_t idle_us, bool bu
             release_service(s);
             return NFFACL_ERR_INVALID_ARG;
         }
-        s->args.full_poll = set && v != 0 ? 1u : 0u;
+        s->args.full_poll = !set || v != 0 ? 1u : 0u;
         s->cpus = cpu_budget();
     }
     const void *kern = burst ? reinterpret_cast<const void *>(dev::k_service_burst)

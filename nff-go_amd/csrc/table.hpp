@@ -83,20 +83,17 @@ constexpr uint32_t kMaxIndexedRules = 1u << 23;
 //    on one field or on a 2-D grid of two fields' top bits.
 // A flat-form list entry is EXACT — a candidate needs no second read:
 //   IPv4, 6 dwords (24 B):
-//      [0] lo = sport_min | dport_min << 16   [1] hi = sport_max | dport_max << 16
-//          (IPv4 rules without a port check: 0 / 0xffffffff)
+//      [0] src word, big-endian value   [1] dst word, big-endian value
 //      [2] meta = id | exact << 8 | rule_index << 9          (as inline)
-//      [3] src_len | dst_len << 8 | out << 16
-//      [4] src word, big-endian value   [5] dst word, big-endian value
+//      [3] lo = sport_min | dport_min << 16   [4] hi = sport_max | dport_max << 16
+//          (IPv4 rules without a port check: 0 / 0xffffffff)
+//      [5] src_len | dst_len << 8 | out << 16
 //   IPv6, 12 dwords (48 B): the same six words with the top 32 address bits
 //      and prefix lengths 0..128, then [6..8] src words 1..3, [9..11] dst
 //      words 1..3 (big-endian values).
-// The walk tests in two stages (classify.hpp hyb_miss_l4 / hyb_miss_l3):
-// words 0..3 (one 16-byte load) for every candidate, words 4..5 (and the
-// IPv6 words) only for the candidates whose protocol and ports match.
 // `out` is the OutputNumber when < kHybOutEscape; otherwise it is read from
 // the family's output array (one u32 per rule, in rule order; off_rec4 /
-// off_rec6).
+// off_rec6).  Loads are 12-byte (dwordx3): two per IPv4 entry, four per IPv6.
 // The hybrid forms encode only CIDR masks and id_mask in {0, 0xff} (what
 // the parsers produce); other rule sets compile INDEXED.
 constexpr uint32_t kHybEnt4Dwords = 6;

@@ -249,18 +249,18 @@ def hyb_test(blob, info, offs, v6, F, sel):
     returns (ok, rule index, output code)."""
     ew = 12 if v6 else 6
     e = blob[offs[:, None] + np.arange(ew)[None, :]]
-    lens = e[:, 3]
+    lens = e[:, 5]
     sl, dl = (lens & 0xFF).astype(np.int64), ((lens >> 8) & 0xFF).astype(np.int64)
     m = np.zeros(len(sel), np.uint32)
     for k in range(4 if v6 else 1):
-        rs = e[:, 4] if k == 0 else e[:, 5 + k]
-        rd = e[:, 5] if k == 0 else e[:, 8 + k]
+        rs = e[:, 0] if k == 0 else e[:, 5 + k]
+        rd = e[:, 1] if k == 0 else e[:, 8 + k]
         m |= (bswap(F["s"][k][sel]) ^ rs) & pmask(np.clip(sl - 32 * k, 0, 32))
         m |= (bswap(F["t"][k][sel]) ^ rd) & pmask(np.clip(dl - 32 * k, 0, 32))
     meta = e[:, 2]
     m |= np.where((meta >> 8) & 1 == 1, (F["proto"][sel] ^ meta) & 0xFF, 0).astype(np.uint32)
     sp, dp = F["sp"][sel].astype(np.uint32), F["dp"][sel].astype(np.uint32)
-    lo, hi = e[:, 0], e[:, 1]
+    lo, hi = e[:, 3], e[:, 4]
     ok = (m == 0) & (sp >= (lo & 0xFFFF)) & (sp <= (hi & 0xFFFF)) & (dp >= (lo >> 16)) & (dp <= (hi >> 16))
     return ok, (meta >> 9).astype(np.uint64), (lens >> 16).astype(np.uint32)
 
