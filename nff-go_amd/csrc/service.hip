@@ -402,7 +402,8 @@ __global__ void __launch_bounds__(64) k_service_burst(SvcArgs a) {
         uint64_t cw = 0;  // stop | restart << 32
         if (hot && a.full_poll) {
 #pragma unroll
-            for (uint32_t j = 0; j < kSvcBurstLoads; ++j) body[j] = ld16_host(rs, box + 1024u * j + 16u * lane);
+            for (uint32_t j = 0; j < kSvcBurstLoads; ++j)
+                if (j + 1 < kSvcBurstLoads || lane < kSvcBurstTailLanes) body[j] = ld16_host(rs, box + 1024u * j + 16u * lane);
             hh = body[0];
         } else if (hot) {
             if (lane < kSvcBurstHdrChunks) hh = ld16_host(rs, box + 16u * lane);
@@ -435,7 +436,7 @@ __global__ void __launch_bounds__(64) k_service_burst(SvcArgs a) {
             continue;
         }
         if (!a.full_poll) {
-            const uint32_t nl = ((kSvcBurstHdrChunks + kSvcPktChunks * n) * 16u + 1023u) / 1024u;  // 1 KiB loads
+            const uint32_t nl = ((kSvcBurstHdrChunks + kSvcBurstPktChunks * n) * 16u + 1023u) / 1024u;  // 1 KiB loads
 #pragma unroll
             for (uint32_t j = 0; j < kSvcBurstLoads; ++j)
                 body[j] = j < nl ? ld16_host(rs, box + 1024u * j + 16u * lane) : u32x4{0, 0, 0, 0};
@@ -444,16 +445,16 @@ __global__ void __launch_bounds__(64) k_service_burst(SvcArgs a) {
 #pragma unroll
         for (uint32_t j = 0; j < kSvcBurstLoads; ++j) img[64u * j + lane] = body[j];
         wave_lds_sync();
-        u32x4 c[kSvcPktChunks];
+        u32x4 c[kSvcBurstPktChunks];
 #pragma unroll
-        for (uint32_t j = 0; j < kSvcPktChunks; ++j)
-            c[j] = lane < kSvcBurstMax ? img[kSvcBurstHdrChunks + kSvcPktChunks * lane + j] : u32x4{0, 0, 0, 0};
+        for (uint32_t j = 0; j < kSvcBurstPktChunks; ++j)
+            c[j] = lane < kSvcBurstMax ? img[kSvcBurstHdrChunks + kSvcBurstPktChunks * lane + j] : u32x4{0, 0, 0, 0};
         wave_lds_sync();
         // complete when every chunk of packets 0..n-1 carries the tag
         const bool live = lane < n;
         bool torn = false;
 #pragma unroll
-        for (uint32_t j = 0; j < kSvcPktChunks; ++j) torn = torn || (live && c[j].w != tag);
+        for (uint32_t j = 0; j < kSvcBurstPktChunks; ++j) torn = torn || (live && c[j].w != tag);
         if (ballot(torn)) {  // the packets' stores not all visible yet: the next poll re-reads them
             ++n_torn;
             continue;
@@ -493,12 +494,14 @@ __global__ void __launch_bounds__(64) k_service_burst(SvcArgs a) {
             wave_lds_sync();
             staged_gen = key >> 1;
         }
+        // bytes 0..83 of the packet: the MAC addresses (0-11) were not sent
         uint32_t full[3 * kSvcPktChunks], d[16];
+        full[0] = full[1] = full[2] = 0u;
 #pragma unroll
-        for (uint32_t j = 0; j < kSvcPktChunks; ++j) {
-            full[3 * j + 0] = c[j].x;
-            full[3 * j + 1] = c[j].y;
-            full[3 * j + 2] = c[j].z;
+        for (uint32_t j = 0; j < kSvcBurstPktChunks; ++j) {
+            full[3 * j + 3] = c[j].x;
+            full[3 * j + 4] = c[j].y;
+            full[3 * j + 5] = c[j].z;
         }
 #pragma unroll
         for (int k = 0; k < 16; ++k) d[k] = full[k];
@@ -1181,6 +1184,29 @@ inline void packet_chunks(const uint8_t *frame, uint32_t len, uint32_t tag, __m1
     put16(dst + kSvcPktChunks - 1, _mm_or_si128(last, t), nt);
 }
 
+// One packet as burst-mailbox payload (service.hpp): bytes [12, min(len, 80)),
+// zero after, 12 per chunk with the tag in word 3 — packet_chunks without its
+// first chunk (the MAC addresses).
+inline void burst_chunks(const uint8_t *frame, uint32_t len, uint32_t tag, __m128i *dst, bool nt) {
+    static_assert(kSvcBurstPktChunks == 6 && kSvcSlot == 80, "five 16-byte loads + one 8-byte load per packet");
+    const __m128i keep = _mm_set_epi32(0, -1, -1, -1);
+    const __m128i t = _mm_set_epi32(static_cast<int>(tag), 0, 0, 0);
+    alignas(16) uint8_t b[96];
+    const uint8_t *src = frame;
+    if (len < kSvcSlot) {
+        std::memset(b, 0, sizeof b);
+        if (len) std::memcpy(b, frame, len);
+        src = b;
+    }
+    for (uint32_t j = 0; j + 1 < kSvcBurstPktChunks; ++j) {  // bytes 12 + 12j .. +15
+        const __m128i v = _mm_loadu_si128(reinterpret_cast<const __m128i *>(src + 12 + 12 * j));
+        put16(dst + j, _mm_or_si128(_mm_and_si128(v, keep), t), nt);
+    }
+    // bytes 72-79, then zeros (80-83) and the tag
+    const __m128i last = _mm_loadl_epi64(reinterpret_cast<const __m128i *>(src + 72));
+    put16(dst + kSvcBurstPktChunks - 1, _mm_or_si128(last, t), nt);
+}
+
 inline void store_chunk(__m128i *dst, uint32_t x, uint32_t y, uint32_t z, uint32_t w, bool nt) {
     put16(dst, _mm_set_epi32(static_cast<int>(w), static_cast<int>(z), static_cast<int>(y), static_cast<int>(x)), nt);
 }
@@ -1275,8 +1301,8 @@ int nffacl_service_classify_burst(nffacl_service *s, const nffacl_rules *rules, 
             const bool wd = key == kSvcWithdrawn;
             const uint32_t cnt = wd ? 1u : n;
             for (uint32_t i = 0; i < cnt; ++i)
-                packet_chunks(wd ? nullptr : frames[i], wd ? 0u : lens ? lens[i] : kSvcSlot, tag,
-                              dst + kSvcBurstHdrChunks + kSvcPktChunks * i, s->nt);
+                burst_chunks(wd ? nullptr : frames[i], wd ? 0u : lens ? lens[i] : kSvcSlot, tag,
+                             dst + kSvcBurstHdrChunks + kSvcBurstPktChunks * i, s->nt);
             store_chunk(dst + 1, cnt, 0, 0, tag, s->nt);
             // the consumer reads the packets only once the header carries the
             // tag: the header chunk goes last (streaming stores: after a fence)

@@ -53,15 +53,19 @@ constexpr uint32_t kSvcWithdrawn = 0xFFFFFFFEu;
 // packet.  16-byte chunks as above, each carrying the tag in its last dword:
 //   chunk 0:          {desc address lo, desc address hi, generation << 1 | vlan, tag}
 //   chunk 1:          {packets n (1..kSvcBurstMax), 0, 0, tag}
-//   chunk 2 + 7i + j: packet i bytes [12j, 12j + 12) (as the scalar mailbox)
+//   chunk 2 + 6i + j: packet i bytes [12 + 12j, 24 + 12j) — the scalar
+//                     mailbox's chunks without the MAC addresses (bytes 0-11,
+//                     which no L3/L4 verdict reads): 14 % fewer bytes to poll
 // One consumer wave per mailbox: lane i < n classifies packet i and writes
 // {tag, port} to its own 8-byte response word (kSvcBurstRespWords per
 // mailbox); the caller waits until all n words carry its tag.
 constexpr uint32_t kSvcBurstMax = 32;
 constexpr uint32_t kSvcBurstHdrChunks = 2;
-constexpr uint32_t kSvcBurstChunks = kSvcBurstHdrChunks + kSvcBurstMax * kSvcPktChunks;  // 226
-constexpr uint32_t kSvcBurstBoxBytes = 4096;  // 4 coalesced 1 KiB poll loads (3 616 bytes used)
+constexpr uint32_t kSvcBurstPktChunks = kSvcPktChunks - 1;  // 6
+constexpr uint32_t kSvcBurstChunks = kSvcBurstHdrChunks + kSvcBurstMax * kSvcBurstPktChunks;  // 194
+constexpr uint32_t kSvcBurstBoxBytes = 4096;  // 4 coalesced poll loads (3 104 bytes used)
 constexpr uint32_t kSvcBurstLoads = (kSvcBurstChunks * 16 + 1023) / 1024;
+constexpr uint32_t kSvcBurstTailLanes = kSvcBurstChunks - (kSvcBurstLoads - 1) * 64;  // lanes of the last load
 constexpr uint32_t kSvcBurstRespWords = kSvcBurstMax;  // 256 B: four lines per mailbox
 static_assert(kSvcBurstChunks * 16 <= kSvcBurstBoxBytes, "burst mailbox");
 
