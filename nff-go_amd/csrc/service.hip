@@ -60,6 +60,10 @@
 #include "rules.hpp"
 #include "service.hpp"
 
+#ifndef NFFACL_EXP_SVCSTAT
+#define NFFACL_EXP_SVCSTAT 0  // experiment builds: the burst consumer's poll statistic = answer -> next request
+#endif
+
 namespace nffacl {
 namespace dev {
 
@@ -75,6 +79,8 @@ struct SvcArgs {
     uint64_t idle_ticks;    // leave after this long without a request (wall clock ticks)
     uint64_t hot_ticks;     // a mailbox answered within this window is read whole every pass
     uint64_t life_ticks;    // leave after this long in any case
+    uint32_t idle_naps;     // burst consumer: s_sleep(8) (~0.2 us) naps of an idle wave between bell reads
+                            // (NFFACL_TUNE_SVC_IDLE_NAPS)
     uint32_t full_poll;     // burst consumer: hot waves read the whole mailbox every pass (default; 0: the
                             // header, then the packets on a new tag — NFFACL_TUNE_SVC_FULLPOLL=0)
 };
@@ -387,6 +393,9 @@ __global__ void __launch_bounds__(64) k_service_burst(SvcArgs a) {
     uint32_t w_kind = 0, w_dwords = 0;  // its kind and table size (wave-uniform)
     const uint32_t *tab = nullptr;
     uint64_t n_polls = 0, poll_ticks = 0, n_groups = 0, group_ticks = 0, n_req = 0, n_torn = 0;
+#if NFFACL_EXP_SVCSTAT
+    uint64_t t_ans = 0;
+#endif
     const uint32_t box = mb * kSvcBurstBoxBytes;
     const uint32_t bell = a.box_bytes + mb * 4u;
     while (true) {
@@ -418,10 +427,16 @@ __global__ void __launch_bounds__(64) k_service_burst(SvcArgs a) {
              __builtin_amdgcn_readlane(static_cast<uint32_t>(cw >> 32), 0)) != 0u)
             break;
         const uint64_t t_data = wall_clock64();
+#if !NFFACL_EXP_SVCSTAT
         ++n_polls;
         poll_ticks += t_data - now;
+#endif
         if (tag == done) {
             if (now - last > a.idle_ticks) break;
+            // an idle wave naps between bell reads (its reads share the
+            // link's request slots with the hot waves' polls)
+            if (!hot)
+                for (uint32_t i = 0; i < a.idle_naps; ++i) __builtin_amdgcn_s_sleep(8);
             continue;
         }
         last = now;
@@ -464,6 +479,12 @@ __global__ void __launch_bounds__(64) k_service_burst(SvcArgs a) {
         h0.y = __builtin_amdgcn_readlane(hh.y, 0);
         h0.z = __builtin_amdgcn_readlane(hh.z, 0);
         const uint64_t t_group = wall_clock64();
+#if NFFACL_EXP_SVCSTAT  // experiment: "polls" = answer -> next request seen, per hot wave
+        if (t_ans) {
+            ++n_polls;
+            poll_ticks += t_data - t_ans;
+        }
+#endif
         const uint32_t key = __builtin_amdgcn_readfirstlane(h0.z);
         if (key == kSvcWithdrawn) {  // the caller gave up: answered, no table read
             if (live) __hip_atomic_store(resp + lane, uint64_t(tag) << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -522,6 +543,9 @@ __global__ void __launch_bounds__(64) k_service_burst(SvcArgs a) {
         ++n_groups;
         n_req += n;
         group_ticks += wall_clock64() - t_group;
+#if NFFACL_EXP_SVCSTAT
+        t_ans = wall_clock64();
+#endif
     }
     if (lane == 0) {
         uint64_t *st = a.stats + size_t(blockIdx.x) * kSvcStatWords;
@@ -964,9 +988,12 @@ int service_create(int hip_device, uint32_t mailboxes, uint32_t idle_us, bool bu
     const size_t stat_bytes = size_t(s->waves()) * kSvcStatWords * 8;
     const size_t bytes = box_bytes + bell_bytes + resp_bytes + 64 + stat_bytes;
     hipError_t e = s->mbx ? hipSuccess : hipErrorOutOfMemory;
+    // NFFACL_TUNE_SVC_NODE=0: the caller's default memory policy instead of the device's node
+    const char *node_env = std::getenv("NFFACL_TUNE_SVC_NODE");
+    const bool on_node = !(node_env && node_env[0] == '0' && node_env[1] == 0);
     if (e == hipSuccess)
         e = host_alloc_on_node(reinterpret_cast<void **>(&s->h_mem), bytes, hipHostMallocMapped | hipHostMallocCoherent,
-                               hip_device < device_nodes().count ? device_nodes().node[hip_device] : -1);
+                               on_node && hip_device < device_nodes().count ? device_nodes().node[hip_device] : -1);
     uint8_t *d_mem = nullptr;
     if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void **>(&d_mem), s->h_mem, 0);
     int lo = 0, hi = 0;
@@ -1037,6 +1064,12 @@ int service_create(int hip_device, uint32_t mailboxes, uint32_t idle_us, bool bu
             return NFFACL_ERR_INVALID_ARG;
         }
         s->args.full_poll = !set || v != 0 ? 1u : 0u;
+        if (!env_knob("NFFACL_TUNE_SVC_IDLE_NAPS", 0, 1000, v, set, err)) {
+            set_last_error(err);
+            release_service(s);
+            return NFFACL_ERR_INVALID_ARG;
+        }
+        s->args.idle_naps = set ? static_cast<uint32_t>(v) : 0u;
         s->cpus = cpu_budget();
     }
     const void *kern = burst ? reinterpret_cast<const void *>(dev::k_service_burst)

@@ -14,7 +14,7 @@ step() {  # name, timeout, command...
     return $rc
 }
 cd /tmp && export TMPDIR=/tmp
-B="python3 $R/bench.py --no-cpu-baseline --no-host --extra none --steps 10 --warmup 2 $*"
+B="python3 $R/bench.py --no-cpu-baseline --no-host --no-shapes --extra none --steps 10 --warmup 2 $*"
 step trace 600 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- $B || exit $?
 step fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o run --output-format csv -- $B || exit $?
 step write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o run --output-format csv -- $B || exit $?

@@ -39,8 +39,13 @@ __device__ __forceinline__ u32x4 ld16(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
 // stats: [0] polls, [1] poll ticks, [2] body reads, [3] body ticks.
 // PIPE (full polls only): the next poll is issued before the current one's
 // request is answered, as the service's consumer does.
+// Service-like extras: `ctrl` != null: one system-scope 8-byte load of it per
+// pass (the consumer's stop word); `resp_lanes` lanes answer (one 8-byte
+// system-scope store each, as 32 packets); `work` wall-clock ticks spent
+// between reading a request and answering it (the classification).
 template <bool HDR, bool PIPE>
-__global__ void k_box(const uint8_t *box, uint32_t body_loads, uint64_t *resp, uint32_t rounds, uint64_t *stats) {
+__global__ void k_box(const uint8_t *box, uint32_t body_loads, uint64_t *resp, uint32_t rounds, uint64_t *stats,
+                      const uint64_t *ctrl, uint32_t resp_lanes, uint32_t work) {
     const uint32_t lane = threadIdx.x;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(box), 0, 4096, 0x00020000);
     const uint64_t t0 = wall_clock64();
@@ -66,8 +71,11 @@ __global__ void k_box(const uint8_t *box, uint32_t body_loads, uint64_t *resp, u
 #pragma unroll
         for (uint32_t j = 0; j < 4; ++j) v[j] = nx[j];
         const uint64_t a = ta;
+        uint64_t cw = 0;
+        if (ctrl && lane == 0) cw = __hip_atomic_load(ctrl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         const uint32_t tag = __builtin_amdgcn_readlane(v[0].w, 0);
         const uint32_t last = __builtin_amdgcn_readlane(v[body_loads - 1].w, 63);
+        if (__builtin_amdgcn_readlane(static_cast<uint32_t>(cw), 0) == 0xDEADBEEFu) break;
         __builtin_amdgcn_s_waitcnt(0);  // (the clock read after the data, not hoisted above the wait)
         const uint64_t b = wall_clock64();
         ++np;
@@ -90,8 +98,14 @@ __global__ void k_box(const uint8_t *box, uint32_t body_loads, uint64_t *resp, u
         }
         // the last chunk carries the tag too: torn reads retry
         if (lt == tag) {
+            if (work) {
+                const uint64_t w0 = wall_clock64();
+                while (wall_clock64() - w0 < work) {
+                }
+            }
             done = tag;
-            if (lane == 0) __hip_atomic_store(resp, uint64_t(tag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (lane < resp_lanes)
+                __hip_atomic_store(resp + lane, uint64_t(tag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
         if (!PIPE) issue();
     }
@@ -137,7 +151,7 @@ int main(int argc, char **argv) {
     uint8_t *box;
     uint64_t *resp, *stats;
     CHECK(hipHostMalloc(&box, 4096, hipHostMallocMapped | hipHostMallocCoherent));
-    CHECK(hipHostMalloc(&resp, 64, hipHostMallocMapped | hipHostMallocCoherent));
+    CHECK(hipHostMalloc(&resp, 4096, hipHostMallocMapped | hipHostMallocCoherent));
     CHECK(hipMalloc(&stats, 64));
     const uint32_t rounds = 4000;
     {
@@ -156,46 +170,48 @@ int main(int argc, char **argv) {
             CHECK(hipHostFree(b2));
         }
     }
-    for (int hdr = 0; hdr < 3; ++hdr) {  // 0 full, 1 header, 2 full pipelined
-        for (int nt = 0; nt < 2; ++nt) {
-            for (uint32_t loads : {1u, 4u}) {
-                std::memset(box, 0, 4096);
-                *resp = 0;
-                if (hdr == 1) hipLaunchKernelGGL((k_box<true, false>), dim3(1), dim3(64), 0, 0, box, loads, resp, rounds, stats);
-                else if (hdr == 2) hipLaunchKernelGGL((k_box<false, true>), dim3(1), dim3(64), 0, 0, box, loads, resp, rounds, stats);
-                else hipLaunchKernelGGL((k_box<false, false>), dim3(1), dim3(64), 0, 0, box, loads, resp, rounds, stats);
-                std::vector<double> lat;
-                const uint32_t chunks = loads * 64;
-                for (uint32_t tag = 1; tag <= rounds; ++tag) {
-                    const auto t0 = std::chrono::steady_clock::now();
-                    __m128i *d = reinterpret_cast<__m128i *>(box);
-                    for (uint32_t c = chunks; c-- > 2;) put(d + c, _mm_set_epi32(int(tag), 1, 2, 3), nt);
-                    put(d + 1, _mm_set_epi32(int(tag), 0, 0, 32), nt);
-                    if (nt) _mm_sfence();
-                    put(d, _mm_set_epi32(int(tag), 7, 8, 9), nt);
-                    if (nt) _mm_sfence();
-                    const auto limit = t0 + std::chrono::milliseconds(50);
-                    bool ok = true;
-                    while (__atomic_load_n(resp, __ATOMIC_ACQUIRE) != tag) {
-                        _mm_pause();
-                        if (std::chrono::steady_clock::now() > limit) { ok = false; break; }
-                    }
-                    if (!ok) break;
-                    lat.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
-                }
-                CHECK(hipDeviceSynchronize());
-                uint64_t st[4];
-                CHECK(hipMemcpy(st, stats, 32, hipMemcpyDeviceToHost));
-                std::sort(lat.begin(), lat.end());
-                auto pct = [&](double p) { return lat.empty() ? 0.0 : lat[std::min(lat.size() - 1, size_t(p * lat.size()))]; };
-                std::printf("{\"poll\": \"%s\", \"nt\": %d, \"bytes\": %u, \"answered\": %zu, \"p50_us\": %.2f, \"p99_us\": %.2f, "
-                            "\"hdr_poll_us\": %.3f, \"polls_per_req\": %.2f, \"body_us\": %.3f}\n",
-                            hdr == 1 ? "hdr" : hdr == 2 ? "full_pipe" : "full", nt, loads * 1024, lat.size(), pct(0.5), pct(0.99),
-                            st[0] ? double(st[1]) / st[0] / 100.0 : 0.0, lat.empty() ? 0.0 : double(st[0]) / lat.size(),
-                            st[2] ? double(st[3]) / st[2] / 100.0 : 0.0);
-                std::fflush(stdout);
+    uint64_t *ctrl;
+    CHECK(hipHostMalloc(&ctrl, 64, hipHostMallocMapped | hipHostMallocCoherent));
+    *ctrl = 0;
+    struct V { const char *name; bool use_ctrl; uint32_t lanes; uint32_t work; } vs[] = {
+        {"plain", false, 1, 0}, {"ctrl", true, 1, 0}, {"resp32", false, 32, 0}, {"work1.25us", false, 1, 125},
+        {"service_like", true, 32, 125}};
+    for (const V &v : vs) {
+        const uint32_t loads = 4;
+        std::memset(box, 0, 4096);
+        std::memset(resp, 0, 4096);
+        *resp = 0;
+        hipLaunchKernelGGL((k_box<false, false>), dim3(1), dim3(64), 0, 0, box, loads, resp, rounds, stats,
+                           v.use_ctrl ? ctrl : nullptr, v.lanes, v.work);
+        std::vector<double> lat;
+        for (uint32_t tag = 1; tag <= rounds; ++tag) {
+            const auto t0 = std::chrono::steady_clock::now();
+            __m128i *d = reinterpret_cast<__m128i *>(box);
+            for (uint32_t c = loads * 64; c-- > 2;) put(d + c, _mm_set_epi32(int(tag), 1, 2, 3), false);
+            put(d + 1, _mm_set_epi32(int(tag), 0, 0, 32), false);
+            put(d, _mm_set_epi32(int(tag), 7, 8, 9), false);
+            const auto limit = t0 + std::chrono::milliseconds(50);
+            bool ok = true;
+            const uint32_t want = v.lanes > 1 ? 31 : 0;
+            while (__atomic_load_n(resp + want, __ATOMIC_ACQUIRE) != tag) {
+                _mm_pause();
+                if (std::chrono::steady_clock::now() > limit) { ok = false; break; }
             }
+            if (!ok) break;
+            lat.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
         }
+        *ctrl = 0xDEADBEEFull;
+        CHECK(hipDeviceSynchronize());
+        *ctrl = 0;
+        uint64_t st[4];
+        CHECK(hipMemcpy(st, stats, 32, hipMemcpyDeviceToHost));
+        std::sort(lat.begin(), lat.end());
+        auto pct = [&](double p) { return lat.empty() ? 0.0 : lat[std::min(lat.size() - 1, size_t(p * lat.size()))]; };
+        std::printf("{\"variant\": \"%s\", \"answered\": %zu, \"p50_us\": %.2f, \"p99_us\": %.2f, \"poll_us\": %.3f, "
+                    "\"polls_per_req\": %.2f}\n",
+                    v.name, lat.size(), pct(0.5), pct(0.99), st[0] ? double(st[1]) / st[0] / 100.0 : 0.0,
+                    lat.empty() ? 0.0 : double(st[0]) / lat.size());
+        std::fflush(stdout);
     }
     return 0;
 }
