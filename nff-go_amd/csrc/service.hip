@@ -681,6 +681,10 @@ uint32_t cpu_budget() {
 }  // namespace
 
 struct nffacl_service {
+    // NFFACL_TUNE_SVC_TRACE=1 (experiments): host-side phase times of the
+    // calls, printed to stderr when the service is destroyed
+    bool trace = false;
+    std::atomic<uint64_t> tr_calls{0}, tr_total_ns{0}, tr_post_ns{0}, tr_wait_ns{0}, tr_spins{0};
     int device = 0;
     uint32_t id = 0;  // process-unique: keys the callers' thread-local mailbox choice
     uint32_t n_mb = 0;
@@ -843,6 +847,12 @@ uint32_t my_mailbox(nffacl_service *s) {
 }
 
 void release_service(nffacl_service *s) {
+    if (s->trace && s->tr_calls.load()) {
+        const double c = double(s->tr_calls.load());
+        std::fprintf(stderr, "[nffacl service trace] calls %.0f: total %.3f us, post %.3f us, wait %.3f us, spins %.1f per call\n",
+                     c, s->tr_total_ns.load() / c / 1e3, s->tr_post_ns.load() / c / 1e3, s->tr_wait_ns.load() / c / 1e3,
+                     s->tr_spins.load() / c);
+    }
     if (s->done) (void)hipEventDestroy(s->done);
     if (s->stream) (void)hipStreamDestroy(s->stream);
     if (s->h_mem) (void)hipHostFree(s->h_mem);
@@ -996,6 +1006,9 @@ int service_create(int hip_device, uint32_t mailboxes, uint32_t idle_us, bool bu
                                on_node && hip_device < device_nodes().count ? device_nodes().node[hip_device] : -1);
     uint8_t *d_mem = nullptr;
     if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void **>(&d_mem), s->h_mem, 0);
+    // NFFACL_TUNE_SVC_HOSTPTR=1 (experiment): the kernels use the host pointer itself (unified addressing)
+    const char *hp_env = std::getenv("NFFACL_TUNE_SVC_HOSTPTR");
+    if (e == hipSuccess && hp_env && hp_env[0] == '1') d_mem = s->h_mem;
     int lo = 0, hi = 0;
     if (e == hipSuccess) e = hipDeviceGetStreamPriorityRange(&lo, &hi);
     // its own (highest-priority) stream: kept off the queues of batch work
@@ -1070,6 +1083,12 @@ int service_create(int hip_device, uint32_t mailboxes, uint32_t idle_us, bool bu
             return NFFACL_ERR_INVALID_ARG;
         }
         s->args.idle_naps = set ? static_cast<uint32_t>(v) : 0u;
+        if (!env_knob("NFFACL_TUNE_SVC_TRACE", 0, 1, v, set, err)) {
+            set_last_error(err);
+            release_service(s);
+            return NFFACL_ERR_INVALID_ARG;
+        }
+        s->trace = set && v != 0;
         s->cpus = cpu_budget();
     }
     const void *kern = burst ? reinterpret_cast<const void *>(dev::k_service_burst)
@@ -1113,11 +1132,13 @@ int post_and_wait(nffacl_service *s, MailboxState &m, uint32_t mb, DevTable *t, 
                   Answered answered) {
     for (int attempt = 0;; ++attempt) {
         const uint32_t tag = ++m.seq;
+        const Clock::time_point tp0 = s->trace ? Clock::now() : Clock::time_point{};
         post(tag, key);
         if (s->nt) _mm_sfence();  // the streaming stores are visible before the bell
         __atomic_store_n(&s->h_bell[mb], tag, __ATOMIC_RELEASE);  // idle waves watch the bells
         std::atomic_thread_fence(std::memory_order_seq_cst);      // request visible before `running` is read
         if (!s->running.load(std::memory_order_seq_cst)) kick(s);
+        const Clock::time_point tp1 = s->trace ? Clock::now() : Clock::time_point{};
         // sleep first?  (adaptive: only with more callers than CPUs)
         const bool adaptive = s->sleep_ns < 0 && s->next_mb.load(std::memory_order_relaxed) > s->cpus;
         const uint32_t nap = attempt ? 0u : adaptive ? m.nap : s->sleep_ns > 0 ? static_cast<uint32_t>(s->sleep_ns) : 0u;
@@ -1150,6 +1171,14 @@ int post_and_wait(nffacl_service *s, MailboxState &m, uint32_t mb, DevTable *t, 
                     break;
                 }
             }
+        }
+        if (st == NFFACL_OK && s->trace) {
+            const Clock::time_point tp2 = Clock::now();
+            s->tr_post_ns.fetch_add(uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(tp1 - tp0).count()),
+                                    std::memory_order_relaxed);
+            s->tr_wait_ns.fetch_add(uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(tp2 - tp1).count()),
+                                    std::memory_order_relaxed);
+            s->tr_spins.fetch_add(spins, std::memory_order_relaxed);
         }
         if (st == NFFACL_OK) {
             if (adaptive && attempt == 0) {
@@ -1309,6 +1338,7 @@ int nffacl_service_classify_burst(nffacl_service *s, const nffacl_rules *rules, 
         (flags & ~uint32_t(NFFACL_PARSE_VLAN)) != 0)
         return NFFACL_ERR_INVALID_ARG;
     if (n == 0) return NFFACL_OK;
+    const Clock::time_point tc0 = s->trace ? Clock::now() : Clock::time_point{};
     for (uint32_t i = 0; i < n; ++i)
         if (!frames[i] && (!lens || lens[i])) return NFFACL_ERR_INVALID_ARG;
     auto failed = [s](int st) {
@@ -1357,6 +1387,12 @@ int nffacl_service_classify_burst(nffacl_service *s, const nffacl_rules *rules, 
     if (st != NFFACL_OK) return st;
     for (uint32_t i = 0; i < n; ++i) ports[i] = static_cast<uint32_t>(__atomic_load_n(r + i, __ATOMIC_RELAXED));
     s->requests.fetch_add(n, std::memory_order_relaxed);
+    if (s->trace) {
+        s->tr_calls.fetch_add(1, std::memory_order_relaxed);
+        s->tr_total_ns.fetch_add(
+            uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - tc0).count()),
+            std::memory_order_relaxed);
+    }
     return NFFACL_OK;
 }
 
