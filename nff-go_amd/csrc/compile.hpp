@@ -86,7 +86,7 @@ struct CompileOptions {
     // NFFACL_TUNE_FINE_A / _P: fine 2-D address x port slots of the flat-LDS
     // form (positional slots 4..7), a address bits x p port bits; a = 0: none
     int fine_a = 8;          // 8 x 4 on slots 4-5: C5 0.583 vs 0.626 ms (profiles/r4_ab/fine/)
-    int fine_p = 4;
+    int fine_p = 5;          // 8 x 5: C5 0.5741 / 0.5718 vs 0.5829 / 0.5825 ms in two sweeps (ab_c5_fine_sweep*)
     double fine_gain = 0.5;  // NFFACL_TUNE_FINE_G (1/100): a rule moves below this fraction of its 1-D cover
     int fine_min = 256;      // NFFACL_TUNE_FINE_MIN: fewest moved rules worth a fine slot
     int fine_slots = 3;      // NFFACL_TUNE_FINE_SLOTS: bit k allows fine slot 4 + k (3: dst x dport, src x dport)
