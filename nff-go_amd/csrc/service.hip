@@ -61,7 +61,8 @@
 #include "service.hpp"
 
 #ifndef NFFACL_EXP_SVCSTAT
-#define NFFACL_EXP_SVCSTAT 0  // experiment builds: the burst consumer's poll statistic = answer -> next request
+#define NFFACL_EXP_SVCSTAT 0  // experiment builds (bits): 1 the burst consumer's poll statistic = answer -> next
+                              // request; 2 answers without classifying; 4 the stop word read every 64th pass
 #endif
 
 namespace nffacl {
@@ -419,15 +420,15 @@ __global__ void __launch_bounds__(64) k_service_burst(SvcArgs a) {
         } else if (lane == 0) {
             bl = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(bell), 0, 17);
         }
-        if (lane == 0) cw = __hip_atomic_load(reinterpret_cast<uint64_t *>(a.ctrl), __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_SYSTEM);
+        if (lane == 0 && (!(NFFACL_EXP_SVCSTAT & 4) || (n_polls & 63u) == 0u))  // (experiment 4: every 64th pass)
+            cw = __hip_atomic_load(reinterpret_cast<uint64_t *>(a.ctrl), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         const uint32_t tag = hot ? static_cast<uint32_t>(__builtin_amdgcn_readlane(hh.w, 0))
                                  : static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(bl));
         if ((__builtin_amdgcn_readlane(static_cast<uint32_t>(cw), 0) |
              __builtin_amdgcn_readlane(static_cast<uint32_t>(cw >> 32), 0)) != 0u)
             break;
         const uint64_t t_data = wall_clock64();
-#if !NFFACL_EXP_SVCSTAT
+#if !(NFFACL_EXP_SVCSTAT & 1)
         ++n_polls;
         poll_ticks += t_data - now;
 #endif
@@ -479,7 +480,7 @@ __global__ void __launch_bounds__(64) k_service_burst(SvcArgs a) {
         h0.y = __builtin_amdgcn_readlane(hh.y, 0);
         h0.z = __builtin_amdgcn_readlane(hh.z, 0);
         const uint64_t t_group = wall_clock64();
-#if NFFACL_EXP_SVCSTAT  // experiment: "polls" = answer -> next request seen, per hot wave
+#if NFFACL_EXP_SVCSTAT & 1  // experiment: "polls" = answer -> next request seen, per hot wave
         if (t_ans) {
             ++n_polls;
             poll_ticks += t_data - t_ans;
@@ -536,7 +537,11 @@ __global__ void __launch_bounds__(64) k_service_burst(SvcArgs a) {
                 hi = k + 1 == j ? full[j] : hi;
             }
         }, key & 1u ? uint32_t(NFFACL_PARSE_VLAN) : 0u);
+#if NFFACL_EXP_SVCSTAT & 2  // experiment: answer without classifying (verdicts wrong)
+        const uint32_t port = f.proto;
+#else
         const uint32_t port = svc_classify(wd, tab, f, W, lane, a.ctrl + 2, staged);
+#endif
         if (live) __hip_atomic_store(resp + lane, uint64_t(tag) << 32 | port, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         done = tag;
         ans_last = now;
