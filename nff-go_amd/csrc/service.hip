@@ -1379,7 +1379,11 @@ int nffacl_service_classify_burst(nffacl_service *s, const nffacl_rules *rules, 
             else store_chunk(dst, static_cast<uint32_t>(desc), static_cast<uint32_t>(desc >> 32), key, tag, s->nt);
         },
         [&](uint32_t tag) {
-            for (uint32_t i = n; i-- > 0;)  // (the words arrive in any order)
+            // spin on one word, then check all (the words arrive in any order)
+            // (round 4: 16 clones 68.9 vs 66.4 Mpps checking all 32 words every spin,
+            // profiles/r4_service/trace/spin1_*)
+            if (static_cast<uint32_t>(__atomic_load_n(r + n - 1, __ATOMIC_ACQUIRE) >> 32) != tag) return false;
+            for (uint32_t i = n; i-- > 0;)
                 if (static_cast<uint32_t>(__atomic_load_n(r + i, __ATOMIC_ACQUIRE) >> 32) != tag) return false;
             return true;
         });
