@@ -43,10 +43,13 @@ def _ptrs(slots, n):
     return nffacl.Batcher.frame_pointers(slots, np.arange(n, dtype=np.uint64) * 80, np.full(n, 80, np.uint32))
 
 
-@pytest.mark.parametrize("cfg", ["c2", "c3", "c5"])
-def test_bursts_vs_oracle(torch_cuda, cfg):
+@pytest.mark.parametrize("cfg,full_poll", [("c2", "1"), ("c3", "1"), ("c5", "1"), ("c2", "0"), ("c5", "0")])
+def test_bursts_vs_oracle(torch_cuda, monkeypatch, cfg, full_poll):
     """C2 (INDEXED, LDS-staged), C3 / C5 (HYBRID flat, directories from
-    global memory): bursts of 1..32 with ragged lengths == the oracle."""
+    global memory): bursts of 1..32 with ragged lengths == the oracle, with
+    the consumer reading whole mailboxes every pass (default) or the header
+    first and the packets on a new tag (NFFACL_TUNE_SVC_FULLPOLL=0)."""
+    monkeypatch.setenv("NFFACL_TUNE_SVC_FULLPOLL", full_poll)
     g = synth.gen_rules(synth.SPECS[cfg], synth.RULE_SEEDS[cfg])
     rules = nffacl.L3Rules.parse_text(g.text)
     n = 4096 if cfg != "c5" else 2048
