@@ -219,21 +219,25 @@ __global__ void __launch_bounds__(64) k_service(SvcArgs a) {
     uint32_t nbell = 0;
     uint64_t ncw = 0, nt = t0;
     bool nhot = true;
+    // (the stop word first and by every lane — one coalesced request — so
+    // that no read of the pass waits behind another; round 4, as in
+    // k_service_burst)
     auto issue = [&]() {
         nt = wall_clock64();
         nhot = ballot(has_mb && nt - lane_last <= a.hot_ticks) != 0u;  // wave-uniform
-#pragma unroll
-        for (uint32_t j = 0; j < kLoads; ++j) nx[j] = u32x4{0, 0, 0, 0};
-        nbell = 0;
+        ncw = __hip_atomic_load(reinterpret_cast<uint64_t *>(a.ctrl), __ATOMIC_RELAXED,
+                                __HIP_MEMORY_SCOPE_SYSTEM);  // stop | restart << 32
+        // the bells by every pass (4 bytes a lane, hot or not: a register
+        // loaded on one path and zeroed on the other made the compiler wait
+        // for the loads issued before it)
+        nbell = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(bell), 0, 17);
         if (nhot) {
 #pragma unroll
             for (uint32_t j = 0; j < kLoads; ++j) nx[j] = ld16_host(rs, wave_box + 1024u * j + 16u * lane);
-        } else if (has_mb) {
-            nbell = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(bell), 0, 17);
+        } else {
+#pragma unroll
+            for (uint32_t j = 0; j < kLoads; ++j) nx[j] = u32x4{0, 0, 0, 0};
         }
-        ncw = 0;  // stop | restart << 32
-        if (lane == 0) ncw = __hip_atomic_load(reinterpret_cast<uint64_t *>(a.ctrl), __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_SYSTEM);
     };
     issue();
     while (true) {
@@ -404,24 +408,34 @@ __global__ void __launch_bounds__(64) k_service_burst(SvcArgs a) {
         const uint64_t now = wall_clock64();
         if (now - t0 > a.life_ticks) break;
         const bool hot = now - ans_last <= a.hot_ticks;  // wave-uniform
-        u32x4 hh = u32x4{0, 0, 0, 0};  // lane 0 chunk 0, lane 1 chunk 1
+        // Every read of the pass is issued before the first wait: the stop
+        // word (all lanes: one coalesced request), then the whole mailbox
+        // (all lanes, all four loads: the last KiB past a full request is
+        // read and ignored), or the header / the bell.  (Round 4: with the
+        // tail load under a lane mask and the stop word read by lane 0 after
+        // it, the compiler waited for the first three loads before issuing
+        // them — two PCIe round trips per pass.)
+        const uint64_t cw = (NFFACL_EXP_SVCSTAT & 4) && (n_polls & 63u) != 0u  // (experiment 4: every 64th pass)
+                                ? 0ull
+                                : __hip_atomic_load(reinterpret_cast<uint64_t *>(a.ctrl), __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_SYSTEM);  // stop | restart << 32
         u32x4 body[kSvcBurstLoads];
-#pragma unroll
-        for (uint32_t j = 0; j < kSvcBurstLoads; ++j) body[j] = u32x4{0, 0, 0, 0};
+        u32x4 hh;  // lane 0 chunk 0, lane 1 chunk 1
         uint32_t bl = 0;
-        uint64_t cw = 0;  // stop | restart << 32
         if (hot && a.full_poll) {
 #pragma unroll
-            for (uint32_t j = 0; j < kSvcBurstLoads; ++j)
-                if (j + 1 < kSvcBurstLoads || lane < kSvcBurstTailLanes) body[j] = ld16_host(rs, box + 1024u * j + 16u * lane);
+            for (uint32_t j = 0; j < kSvcBurstLoads; ++j) body[j] = ld16_host(rs, box + 1024u * j + 16u * lane);
             hh = body[0];
-        } else if (hot) {
-            if (lane < kSvcBurstHdrChunks) hh = ld16_host(rs, box + 16u * lane);
-        } else if (lane == 0) {
-            bl = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(bell), 0, 17);
+        } else {
+#pragma unroll
+            for (uint32_t j = 0; j < kSvcBurstLoads; ++j) body[j] = u32x4{0, 0, 0, 0};
+            hh = u32x4{0, 0, 0, 0};
+            if (hot) {
+                if (lane < kSvcBurstHdrChunks) hh = ld16_host(rs, box + 16u * lane);
+            } else if (lane == 0) {
+                bl = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(bell), 0, 17);
+            }
         }
-        if (lane == 0 && (!(NFFACL_EXP_SVCSTAT & 4) || (n_polls & 63u) == 0u))  // (experiment 4: every 64th pass)
-            cw = __hip_atomic_load(reinterpret_cast<uint64_t *>(a.ctrl), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         const uint32_t tag = hot ? static_cast<uint32_t>(__builtin_amdgcn_readlane(hh.w, 0))
                                  : static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(bl));
         if ((__builtin_amdgcn_readlane(static_cast<uint32_t>(cw), 0) |
@@ -451,6 +465,21 @@ __global__ void __launch_bounds__(64) k_service_burst(SvcArgs a) {
             ++n_torn;  // raced the host's stores: the next poll has it
             continue;
         }
+#if NFFACL_EXP_SVCSTAT & 8  // experiment: answer at once (no packet read, transposition or classification)
+        if (lane < n) __hip_atomic_store(resp + lane, uint64_t(tag) << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        done = tag;
+        ans_last = now;
+        ++n_groups;
+        n_req += n;
+#if NFFACL_EXP_SVCSTAT & 1
+        if (t_ans) {
+            ++n_polls;
+            poll_ticks += t_data - t_ans;
+        }
+        t_ans = wall_clock64();
+#endif
+        continue;
+#endif
         if (!a.full_poll) {
             const uint32_t nl = ((kSvcBurstHdrChunks + kSvcBurstPktChunks * n) * 16u + 1023u) / 1024u;  // 1 KiB loads
 #pragma unroll
