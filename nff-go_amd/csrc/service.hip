@@ -219,25 +219,24 @@ __global__ void __launch_bounds__(64) k_service(SvcArgs a) {
     uint32_t nbell = 0;
     uint64_t ncw = 0, nt = t0;
     bool nhot = true;
-    // (the stop word first and by every lane — one coalesced request — so
-    // that no read of the pass waits behind another; round 4, as in
-    // k_service_burst)
+    // (round 4: the burst consumer's order — stop word first by every lane,
+    // bells unconditionally — ran 5.20 / 5.35 vs 5.86 / 5.63 Mpps at 32
+    // threads here, profiles/r4_service/scalar_poll_order/: not kept)
     auto issue = [&]() {
         nt = wall_clock64();
         nhot = ballot(has_mb && nt - lane_last <= a.hot_ticks) != 0u;  // wave-uniform
-        ncw = __hip_atomic_load(reinterpret_cast<uint64_t *>(a.ctrl), __ATOMIC_RELAXED,
-                                __HIP_MEMORY_SCOPE_SYSTEM);  // stop | restart << 32
-        // the bells by every pass (4 bytes a lane, hot or not: a register
-        // loaded on one path and zeroed on the other made the compiler wait
-        // for the loads issued before it)
-        nbell = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(bell), 0, 17);
+#pragma unroll
+        for (uint32_t j = 0; j < kLoads; ++j) nx[j] = u32x4{0, 0, 0, 0};
+        nbell = 0;
         if (nhot) {
 #pragma unroll
             for (uint32_t j = 0; j < kLoads; ++j) nx[j] = ld16_host(rs, wave_box + 1024u * j + 16u * lane);
-        } else {
-#pragma unroll
-            for (uint32_t j = 0; j < kLoads; ++j) nx[j] = u32x4{0, 0, 0, 0};
+        } else if (has_mb) {
+            nbell = __builtin_amdgcn_raw_buffer_load_b32(rs, static_cast<int>(bell), 0, 17);
         }
+        ncw = 0;  // stop | restart << 32
+        if (lane == 0) ncw = __hip_atomic_load(reinterpret_cast<uint64_t *>(a.ctrl), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_SYSTEM);
     };
     issue();
     while (true) {

@@ -3,7 +3,7 @@
 # (NFFACL_EXP_SVCSTAT builds: 3 = gap statistic + no classification,
 # 5 = gap statistic + stop word read every 64th pass).  usage: gpu_r4w.sh TAG
 R="$GRAFT_REPO_ROOT"; T=$1; OUT="$R/gpurun_out/$T"; mkdir -p "$OUT"; cd "$R"
-for v in svc3 svc5; do
+for v in ${VARIANTS:-svc3 svc5}; do
   NFFACL_LIB=$R/nff-go_amd/build_exp/$v.so NFFACL_BENCH_SHAPES="burst:1:32:1.0,burst:16:32:1.5" \
     timeout -k 10 300 python bench.py --extra none --no-cpu-baseline --no-host --steps 5 --warmup 2 \
       > "$OUT/$v.json" 2> "$OUT/$v.err"
