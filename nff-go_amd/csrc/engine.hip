@@ -519,6 +519,12 @@ static IndexedLaunch indexed_launch(const nffacl_engine *eng, const DevTable *t)
             L.lds_bytes = lds4;
         }
         L.lds_bytes = r4 ? lds4 : image + sizeof(dev::FlatScratch<2>) * (L.block / 64);
+        // (round 4: 2 workgroups per CU — one resident at a time, so that one
+        // that starts late on a CU held by a resident consumer takes a
+        // smaller share — ran C5 0.5810 / 0.5829 vs 0.5816 / 0.5736 ms alone
+        // in two sweeps and +37 % instead of +81 % beside busy consumers; 4
+        // per CU +18 %: profiles/r4_ab/grid/, r4_service/svc_overlap_*.  Kept
+        // at one; NFFACL_TUNE_PER_CU=2-4 for GPUs shared with consumers.)
         return L;
     }
     if (t->meta.algo == NFFACL_ALGO_HYBRID) {
