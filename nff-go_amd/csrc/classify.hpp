@@ -934,7 +934,16 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
             if (ln[s] != 0u && so < win + 64u * RR && so + ln[s] > win) {
                 const uint32_t pos = so > win ? so - win : 0u;
                 W.mark[pos] = (lane << 19 | static_cast<uint32_t>(s) << 16 | pos << 8 | (f.proto & 0xFFu)) + 1u;
-                W.delta[pos] = ((st[s] - so) << 1) | (v6 ? 1u : 0u);
+                if (DIRS_IN_LDS) {
+                    // byte offset (from a.tab) of the list's "candidate 0"
+                    // entry, wrapping mod 2^32, IPv6 in bit 0: the round's
+                    // entry address is then one multiply-shift-add away
+                    const uint32_t w = v6 ? kHybEnt6Dwords : kHybEnt4Dwords;
+                    const uint32_t fb = v6 ? a.f6.off_ent_base : a.f4.off_ent_base;
+                    W.delta[pos] = ((fb + (st[s] - so) * w) << 2) | (v6 ? 1u : 0u);
+                } else {
+                    W.delta[pos] = ((st[s] - so) << 1) | (v6 ? 1u : 0u);
+                }
             }
             so += ln[s];
         }
@@ -977,7 +986,18 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
             // (round 4: one uniform base + a 32-bit byte offset per entry, the
             // saddr load form, -56 static VALU: C5 0.6547 / 0.6527 vs 0.6520 /
             // 0.6491 ms, C3 even; profiles/r4_ab/saddr/ — not kept)
-            const uint32_t *e = (e6 ? E6 : E4) + __umul24(ent, e6 ? kHybEnt6Dwords : kHybEnt4Dwords);
+            // staged walks: entry byte offset = delta + k * 24 (IPv4) / 48
+            // (IPv6), no family base select (round 4: C5 0.5915 / 0.5936 vs
+            // 0.6004 / 0.5984 ms, C3 0.4001 / 0.4058 vs 0.4084 / 0.4053;
+            // profiles/r4_ab/bdelta/); the consumer's walk keeps entry numbers
+            const uint32_t *e;
+            if (DIRS_IN_LDS) {
+                const uint32_t off = !UNCOND || valid[j] ? (dp & ~3u) + (__umul24(k, 4u * kHybEnt4Dwords) << (dp & 1u))
+                                                         : (a.f4.off_ent_base << 2);
+                e = reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(a.tab) + off);
+            } else {
+                e = (e6 ? E6 : E4) + __umul24(ent, e6 ? kHybEnt6Dwords : kHybEnt4Dwords);
+            }
             if (UNCOND || valid[j]) {
                 A[j] = g3(e);
                 B[j] = g3(e + 3);
