@@ -8,13 +8,17 @@ path) over the whole per-GPU batch of synthetic 64-byte slots already
 resident in HBM.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c1|c3|c4|c5|l2]
-                  [--extra c3,c5|none] [--algo auto|linear|indexed|hybrid]
+                  [--extra c1,c3,c5|none] [--algo auto|linear|indexed|hybrid]
 
 At N = 1 the same process then measures the other single-GPU BASELINE.json
-configs named by --extra (default C3: 10 k rules on IMIX frames, C5: 100 k
-rules with port ranges — the "LDS rule-table tiling stress") and reports them
-under "configs", each with its own metric, roofline and CPU baseline; `value`
-stays the C2 headline.  (`--config l2` measures the L2 ACL kernel, SURVEY.md
+configs named by --extra (default C1: examples/firewall's firewall.conf, C3:
+10 k rules on IMIX frames, C5: 100 k rules with port ranges — the "LDS
+rule-table tiling stress") and reports them under "configs", each with its
+own metric, roofline and CPU baseline; `value` stays the C2 headline.
+
+Key order of the one JSON line: the contract's keys, "configs", the compact
+"call_shapes", the PCIe-inclusive rate, and last a "summary" of every headline
+figure, so that a reader who keeps only the line's tail still has them all.  (`--config l2` measures the L2 ACL kernel, SURVEY.md
 §8f row 4 — not a BASELINE.json config.)
 
 N > 1 runs under torch.distributed.run (one rank per GPU, RCCL): rank 0
@@ -338,7 +342,6 @@ def run_config(cfg: str, args, rank: int, world: int, local: int, dev, nd, headl
             "traffic_source": pmc_traffic(cfg, algo_name, n)[1],
             "kernel_ms_mean": round(float(kms.mean()), 5), "kernel_ms_min": round(float(spread.min()), 5),
             "kernel_ms_p50": round(float(np.median(spread)), 5), "kernel_ms_max": round(float(spread.max()), 5),
-            "kernel_ms_all": [round(float(x), 4) for x in spread],
             "timing": args.timing,
         },
         "bit_exact_sample": bit_exact,
@@ -454,13 +457,49 @@ def call_shapes(cfg: str, text: str, gen, cpu_mpps, local: int):
     return res
 
 
+def compact_shapes(res: dict) -> dict:
+    """One config's call-shape record as it goes into the JSON line: per
+    shape the rate, latency, exactness and same-CPU ratio (the consumer's
+    counters stay out of the line)."""
+    out = {k: res[k] for k in ("cpu_same_cpus_mpps", "pinned_numa_node", "bit_exact") if k in res}
+    for name, v in res.items():
+        if isinstance(v, dict):
+            out[name] = {k: v[k] for k in ("mpps", "lat_us_p50", "lat_us_p99", "wrong", "errors", "timeouts",
+                                           "vs_cpu_same_cpus", "error") if k in v}
+    return out
+
+
+def summary(out: dict, ok: bool, cfg: str) -> dict:
+    """Every headline figure of the line in one small block (emitted last)."""
+    def leg(r):
+        rf = r.get("roofline", {})
+        cb = r.get("cpu_baseline") or {}
+        return {"gpps": round(r["value"] / 1e3, 2), "ms": r["ms_per_step"], "frac": rf.get("frac"),
+                "exact": r.get("bit_exact_sample"), "cpu16_mpps": cb.get("value")}
+    s = {cfg: leg(out)}
+    for c, r in (out.get("configs") or {}).items():
+        s[c] = leg(r)
+    for k in ("host_inclusive_mpps", "host_inclusive_bit_exact_sample"):
+        if k in out:
+            s[k] = out[k]
+    for c, r in (out.get("call_shapes") or {}).items():
+        b = r.get("burst32_16_clones") or {}
+        b32 = r.get("burst32_32_clones") or {}
+        sc = r.get("scalar_32_threads") or {}
+        s[f"shapes_{c}"] = {"burst16_mpps": b.get("mpps"), "burst16_vs_cpu": b.get("vs_cpu_same_cpus"),
+                            "burst32_mpps": b32.get("mpps"), "scalar32_mpps": sc.get("mpps"),
+                            "scalar32_vs_cpu": sc.get("vs_cpu_same_cpus"), "exact": r.get("bit_exact")}
+    s["all_bit_exact"] = bool(ok)
+    return s
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "l2"])
-    ap.add_argument("--extra", default="c3,c5",
+    ap.add_argument("--extra", default="c1,c3,c5",
                     help="N=1: further configs measured in the same process (comma list, or 'none')")
     ap.add_argument("--algo", default="auto", choices=["auto", "linear", "indexed", "hybrid"])
     ap.add_argument("--packets", type=int, default=1 << 24, help="packets per GPU")
@@ -503,6 +542,7 @@ def main():
     }
     ok = rec["bit_exact_sample"]
     eng, n, got, idx = st["eng"], st["n"], st["got"], st["idx"]
+    host = {}
 
     # ---- N>1: root-scattered curve (SURVEY.md §8e curve 2; not `value`) ----
     # rank 0's resident batch goes out with one dist.scatter (RCCL: the
@@ -550,10 +590,11 @@ def main():
             t = time.perf_counter()
             hp, _ = eng.classify_host(pinned, 64, m, out=hout, permit=False)
             best = min(best, time.perf_counter() - t)
-        out["host_inclusive_mpps"] = round(m / best / 1e6, 1)
-        out["host_inclusive"] = {"packets": m, "gbps_in": round(m * 64 / best / 1e9, 1),
-                                 "input": "pinned host 64 B slots", "output": "pinned host u32 verdicts"}
-        out["host_inclusive_bit_exact_sample"] = bool((hp[idx[idx < m]] == got[idx[idx < m]]).all())
+        host = {"host_inclusive": {"packets": m, "gbps_in": round(m * 64 / best / 1e9, 1),
+                                   "input": "pinned host 64 B slots", "output": "pinned host u32 verdicts"},
+                "host_inclusive_mpps": round(m / best / 1e6, 1),
+                "host_inclusive_bit_exact_sample": bool((hp[idx[idx < m]] == got[idx[idx < m]]).all())}
+        ok = ok and host["host_inclusive_bit_exact_sample"]
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cb, cports = cpu_baseline_for(cfg, st, args.cpu_seconds)
@@ -593,9 +634,11 @@ def main():
         torch.cuda.empty_cache()
 
     if shapes:
-        out["call_shapes"] = shapes
+        out["call_shapes"] = {c: compact_shapes(v) for c, v in shapes.items()}
+    out.update(host)
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        out["summary"] = summary(out, ok, cfg)
+        print(json.dumps(out, separators=(",", ":")), flush=True)
     if world > 1:
         dist.destroy_process_group()
     return 0 if ok else 1

@@ -32,6 +32,7 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <unordered_map>
 
 #include "compile.hpp"
 #include "devutil.hpp"
@@ -41,6 +42,13 @@ using namespace nffacl;
 using Clock = std::chrono::steady_clock;
 
 namespace {
+
+// Tickets this thread has submitted and not collected, per batcher id (the
+// back-pressure bound in submit_impl).
+thread_local std::unordered_map<uint64_t, int64_t> t_own_tickets;
+std::atomic<uint64_t> g_batcher_ids{1};
+constexpr std::chrono::milliseconds kSubmitForeignBound{30000};
+
 
 // Mapped (device-addressable) and coherent (fine-grained): the GPU reads the
 // slots the CPU just wrote and the CPU reads the verdicts, with no cache
@@ -203,6 +211,7 @@ int create_impl(nffacl_engine *eng, bool own, uint32_t stride, uint32_t max_batc
                 uint32_t nbuf, nffacl_batcher **out) {
     nffacl_batcher *b = new (std::nothrow) nffacl_batcher();
     if (!b) return NFFACL_ERR_NOMEM;
+    b->id = g_batcher_ids.fetch_add(1, std::memory_order_relaxed);
     b->eng = eng;
     b->own_eng = own;
     b->stride = stride;
@@ -281,7 +290,7 @@ int submit_impl(nffacl_batcher *b, DevTable *table, const uint8_t *const *frames
     std::unique_lock<std::mutex> lk(b->mu);
     BatchBuf *x = nullptr;
     uint32_t off = 0, burst = 0;
-    Clock::time_point give_up{};  // set at the first back-pressure wait
+    Clock::time_point first_wait{};  // set at the first back-pressure wait
     while (true) {
         if (b->stop) return NFFACL_ERR_INVALID_ARG;
         BatchBuf &cur = b->bufs[b->open_idx];
@@ -296,17 +305,25 @@ int submit_impl(nffacl_batcher *b, DevTable *table, const uint8_t *const *frames
             cur.readers.store(0, std::memory_order_relaxed);
             cur.written.store(0, std::memory_order_relaxed);
         } else if (cur.state != BatchBuf::OPEN) {
-            // every buffer busy: back-pressure.  Bounded: buffers whose
-            // batches are done stay busy until their tickets are collected,
-            // and when the tickets are this caller's own (submitted, not yet
-            // waited for) no amount of waiting frees one.
+            // every buffer busy: back-pressure.  Buffers whose batches are
+            // done stay busy until their tickets are collected; when some of
+            // those tickets are this caller's own (submitted, not yet waited
+            // for) no amount of waiting may free one, so that wait is bounded
+            // by submit_bound.  A caller holding no ticket waits for the
+            // other threads' batches (a GPU shared with resident consumers,
+            // a first launch) up to kSubmitForeignBound.
             const auto now = Clock::now();
-            if (give_up == Clock::time_point{}) give_up = now + b->submit_bound;
+            if (first_wait == Clock::time_point{}) first_wait = now;
+            const auto own = t_own_tickets.find(b->id);
+            const bool self = own != t_own_tickets.end() && own->second > 0;
+            const auto give_up = first_wait + (self ? std::chrono::duration_cast<std::chrono::milliseconds>(b->submit_bound)
+                                                    : std::max(b->submit_bound, kSubmitForeignBound));
             if (now >= give_up) {
-                set_last_error("batcher submit: every buffer holds bursts not yet waited for");
+                set_last_error(self ? "batcher submit: every buffer holds bursts not yet waited for (this thread's own)"
+                                    : "batcher submit: no buffer freed within the bound");
                 return NFFACL_ERR_TIMEOUT;
             }
-            b->cv_free.wait_until(lk, give_up);
+            b->cv_free.wait_until(lk, std::min(give_up, now + std::chrono::milliseconds(50)));
             continue;
         }
         if (cur.count > 0 && cur.table != table) {  // another rule set: the next batch
@@ -338,6 +355,7 @@ int submit_impl(nffacl_batcher *b, DevTable *table, const uint8_t *const *frames
         if (len < b->stride) std::memset(dst + len, 0, b->stride - len);
     }
     x->written.fetch_add(n, std::memory_order_release);
+    ++t_own_tickets[b->id];
     return NFFACL_OK;
 }
 
@@ -384,6 +402,10 @@ int wait_impl(nffacl_batcher *b, const nffacl_ticket *t, uint32_t *ports, uint64
     if (x.seq.load(std::memory_order_acquire) != t->seq) return NFFACL_ERR_INVALID_ARG;
     const int st = x.status.load(std::memory_order_relaxed);
     if (ports && st == NFFACL_OK) std::memcpy(ports, x.h_port + t->off, size_t(t->n) * 4);
+    {
+        auto own = t_own_tickets.find(b->id);  // (collected on another thread than its submit: no entry)
+        if (own != t_own_tickets.end() && own->second > 0 && --own->second == 0) t_own_tickets.erase(own);
+    }
     if (x.readers.fetch_sub(1, std::memory_order_acq_rel) == 1) {  // the batch's last burst
         std::lock_guard<std::mutex> g(b->mu);
         if (x.state == BatchBuf::DONE) free_buffer(b, x);  // else the completer frees it once it marks it DONE

@@ -81,6 +81,7 @@ struct nffacl_batcher {
     // longest back-pressure wait of a submit before NFFACL_ERR_TIMEOUT
     // (NFFACL_TUNE_BATCH_SUBMIT_MS, tests)
     std::chrono::milliseconds submit_bound{1000};
+    uint64_t id = 0;  // process-unique (this thread's own tickets, batcher.cpp)
     uint32_t nbuf = 0;
     std::unique_ptr<nffacl::BatchBuf[]> bufs;
 

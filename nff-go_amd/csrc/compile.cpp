@@ -960,7 +960,29 @@ void build_hybrid(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vec
     // address bits x p port bits) and their directories come off the budget.
     DimBuild fine[2][4];
     bool any_fine = false;
+    // does a directory's every group fit the offsets of form f (8: u8, 16: u16, 0: plain)?
+    auto dir_fits = [](const std::vector<uint32_t> &dir, int f) {
+        if (f == 0) return true;
+        const uint32_t gs = f == 8 ? kDir8GroupShift : kDir16GroupShift;
+        const uint32_t lim = f == 8 ? 0xFFu : 0xFFFFu;
+        for (size_t t = 0; t < dir.size(); ++t)
+            if (dir[t] - dir[(t >> gs) << gs] > lim) return false;
+        return true;
+    };
+    // the fine grids' directory bytes in form f (their shapes are fixed: only the form changes)
+    auto fine_bytes_in = [&](int f) {
+        size_t b = 0;
+        for (int q = 0; q < 2; ++q)
+            for (int k = 0; k < 4; ++k)
+                if (!fine[q][k].rules.empty()) b += size_t(dir_form_bytes(double(fine[q][k].dir.size() - 1), f)) + 16;
+        return b;
+    };
+    // the plan before any rule moved to a grid: restored if the directories
+    // ever degrade to the plain form, where the grids would not fit the budget
+    FamilyPlan plan_1d[2];
     if (flat && lds_dirs && !tuned && opt.fine_a > 0 && !opt.coarse) {
+        plan_1d[0] = plan[0];
+        plan_1d[1] = plan[1];
         const uint32_t fa = static_cast<uint32_t>(opt.fine_a), fp = static_cast<uint32_t>(opt.fine_p);
         static const uint32_t f1s[4] = {kFDst, kFSrc, kFDst, kFSrc}, f2s[4] = {kFDport, kFDport, kFSport, kFSport};
         const uint32_t allowed = static_cast<uint32_t>(opt.fine_slots);  // bit k: positional slot 4 + k
@@ -994,6 +1016,35 @@ void build_hybrid(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vec
                 std::sort(moved[k].begin(), moved[k].end());
                 g[k].rules = moved[k];
                 g[k].fill(pl.rr);
+                // A grid whose lists overflow the current form's offsets
+                // sheds the rules that touch an overflowing group of buckets
+                // (they stay in their 1-D slots): in the wider form its
+                // directory would outgrow the bytes taken off the budget.
+                // Left with fewer than fine_min rules, it is not built.
+                for (int it = 0; it < 8 && !dir_fits(g[k].dir, fmt); ++it) {
+                    const uint32_t gs = fmt == 8 ? kDir8GroupShift : kDir16GroupShift;
+                    const uint32_t lim = fmt == 8 ? 0xFFu : 0xFFFFu;
+                    const std::vector<uint32_t> &dir = g[k].dir;
+                    std::vector<char> hot((dir.size() >> gs) + 1, 0);
+                    for (size_t t = 0; t < dir.size(); ++t)
+                        if (dir[t] - dir[(t >> gs) << gs] > lim) hot[t >> gs] = 1;
+                    std::vector<uint32_t> keep;
+                    for (uint32_t r : g[k].rules) {
+                        uint64_t l1, h1, l2, h2;
+                        g[k].span(pl.rr[r], l1, h1, l2, h2);
+                        bool touch = false;
+                        for (uint64_t t1 = l1; t1 <= h1 && !touch; ++t1)
+                            for (uint64_t t2 = l2; t2 <= h2 && !touch; ++t2)
+                                touch = hot[((t1 << g[k].b2) | t2) >> gs] != 0;
+                        if (!touch) keep.push_back(r);
+                    }
+                    g[k].rules.swap(keep);
+                    g[k].fill(pl.rr);
+                }
+                if (!dir_fits(g[k].dir, fmt) || g[k].rules.size() < size_t(opt.fine_min)) {
+                    g[k].rules.clear();
+                    continue;
+                }
                 DimBuild &fd = fine[f][k];
                 fd.kind = field_kind(g[k].f1, f == 1);
                 fd.key_bits = 32;
@@ -1080,31 +1131,28 @@ void build_hybrid(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vec
     const int nd = static_cast<int>(ext.size());
     // a group whose lists overflow its offsets: the next wider form, re-sized for the same budget
     auto form_fits = [&](int f) {
-        if (f == 0) return true;
-        const uint32_t gs = f == 8 ? kDir8GroupShift : kDir16GroupShift;
-        const uint32_t lim = f == 8 ? 0xFFu : 0xFFFFu;
-        for (int i = 0; i < nd; ++i) {
-            const std::vector<uint32_t> &dir = ext[i]->dir;
-            for (size_t t = 0; t < dir.size(); ++t)
-                if (dir[t] - dir[(t >> gs) << gs] > lim) return false;
-        }
+        for (int i = 0; i < nd; ++i)
+            if (!dir_fits(ext[i]->dir, f)) return false;
         return true;
     };
     auto fine_fits = [&](int f) {
-        if (f == 0) return true;
-        const uint32_t gs = f == 8 ? kDir8GroupShift : kDir16GroupShift;
-        const uint32_t lim = f == 8 ? 0xFFu : 0xFFFFu;
         for (int q = 0; q < 2; ++q)
-            for (int k = 0; k < 4; ++k) {
-                const std::vector<uint32_t> &dir = fine[q][k].dir;
-                for (size_t t = 0; t < dir.size(); ++t)
-                    if (dir[t] - dir[(t >> gs) << gs] > lim) return false;
-            }
+            for (int k = 0; k < 4; ++k)
+                if (!dir_fits(fine[q][k].dir, f)) return false;
         return true;
     };
     while (!form_fits(fmt) || !fine_fits(fmt)) {
         fmt = fmt == 8 && want16 ? 16 : 0;
-        size_and_fill(ext.data(), wext.data(), budget, fmt, nd);
+        if (any_fine && fmt == 0) {  // plain directories: no room for the grids, their rules go back
+            plan[0] = plan_1d[0];
+            plan[1] = plan_1d[1];
+            for (auto &ff : fine)
+                for (DimBuild &fd : ff) fd = DimBuild{};
+            any_fine = false;
+        }
+        // the 1-D slots re-sized for what the grids leave of the budget in the new form
+        const size_t fb = any_fine ? fine_bytes_in(fmt) : 0;
+        size_and_fill(ext.data(), wext.data(), budget > fb ? budget - fb : 1024, fmt, nd);
     }
     const bool dir16 = fmt != 0;
     out.dir8 = fmt == 8 ? 1u : 0u;

@@ -514,11 +514,11 @@ static IndexedLaunch indexed_launch(const nffacl_engine *eng, const DevTable *t)
         const int rounds = tu.rounds ? tu.rounds : static_cast<int>(t->meta.flat_rounds);
         const bool r4 = rounds == 4 && lds4 <= kLdsBytes;
         L.tm = r4 ? (t->meta.flat_uncond ? dev::kTabFlatLds4U : dev::kTabFlatLds4) : dev::kTabFlatLds;
-        if (t->meta.slots_g) {  // generalized slots: the generic kernel (4 rounds)
-            L.tm = dev::kTabFlatLdsG;
-            L.lds_bytes = lds4;
-        }
         L.lds_bytes = r4 ? lds4 : image + sizeof(dev::FlatScratch<2>) * (L.block / 64);
+        if (t->meta.slots_g) {  // generalized slots: the generic kernel, always 4 rounds (its scratch)
+            L.tm = dev::kTabFlatLdsG;
+            L.lds_bytes = lds4;  // > kLdsBytes is refused by the launch check below
+        }
         // (round 4: 2 workgroups per CU — one resident at a time, so that one
         // that starts late on a CU held by a resident consumer takes a
         // smaller share — ran C5 0.5810 / 0.5829 vs 0.5816 / 0.5736 ms alone
@@ -693,6 +693,10 @@ int launch_slots(nffacl_engine *eng, DevTable *t, const uint8_t *d_slots, uint32
         dev::IndexedArgs a = indexed_args(t);
         a.flags = flags;
         const IndexedLaunch L = indexed_launch(eng, t);
+        if (L.lds_bytes > kLdsBytes) {  // (a generalized-slot table with a directory image too large for its scratch)
+            set_last_error("compiled table's LDS image and scratch exceed the CU's LDS");
+            return NFFACL_ERR_INVALID_ARG;
+        }
         const uint32_t grid = grid_for(eng, n, L.block, L.per_cu);
         // long flat walks (kTabFlatLds4U, C5) default to mode 5, the next
         // batch's packets in flight: 0.6278 / 0.6312 vs 0.6340 / 0.6328 ms
@@ -728,6 +732,10 @@ int launch_frames(nffacl_engine *eng, DevTable *t, const uint8_t *d_frames,
         dev::IndexedArgs a = indexed_args(t);
         a.flags = flags;
         const IndexedLaunch L = indexed_launch(eng, t);
+        if (L.lds_bytes > kLdsBytes) {  // (a generalized-slot table with a directory image too large for its scratch)
+            set_last_error("compiled table's LDS image and scratch exceed the CU's LDS");
+            return NFFACL_ERR_INVALID_ARG;
+        }
         const uint32_t grid = grid_for(eng, n, L.block, L.per_cu);
         dispatch_indexed(L.ns, L.tm, [&](auto nsc, auto tmc) {
             launch_frames_tm<decltype(nsc)::value, decltype(tmc)::value>(L, grid, stream, d_frames, d_desc, n, a,

@@ -1443,13 +1443,20 @@ int nffacl_service_pause(nffacl_service *s, int paused) {
     {
         std::lock_guard<std::mutex> g(s->mu);
         if (s->stop) return NFFACL_ERR_INVALID_ARG;
-        s->paused.store(false, std::memory_order_release);
     }
-    // the consumer of the pause has left once `running` drops; then clear the stop word and re-arm
+    // The consumer of the pause has left once `running` drops (still paused,
+    // the armer launches none meanwhile); then clear the stop word, unpause
+    // and re-arm.  A resume that gives up leaves the service consistently
+    // paused (stop word set, `paused` true) for a later resume to finish.
     const auto limit = Clock::now() + std::chrono::seconds(2);
     while (s->running.load(std::memory_order_seq_cst) && Clock::now() < limit) std::this_thread::yield();
     if (s->running.load(std::memory_order_seq_cst)) return NFFACL_ERR_TIMEOUT;
     __atomic_store_n(s->h_ctrl, 0u, __ATOMIC_RELEASE);
+    {
+        std::lock_guard<std::mutex> g(s->mu);
+        if (s->stop) return NFFACL_ERR_INVALID_ARG;
+        s->paused.store(false, std::memory_order_release);
+    }
     kick(s);
     return NFFACL_OK;
 }

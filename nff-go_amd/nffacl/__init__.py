@@ -467,7 +467,19 @@ class Batcher:
         ptrs = (base + np.asarray(offsets, np.uint64)).astype(np.uint64)
         return ptrs, np.ascontiguousarray(lens, np.uint32)
 
+    @staticmethod
+    def _burst_arrays(ptrs, lens):
+        """uint64 pointers and uint32 lengths as contiguous arrays the caller
+        keeps bound for the C call (a converted temporary's .ctypes.data
+        would point at freed memory)."""
+        pa = np.ascontiguousarray(ptrs, np.uint64)
+        la = None if lens is None else np.ascontiguousarray(lens, np.uint32)
+        if la is not None and len(la) != len(pa):
+            raise ValueError(f"{len(la)} lengths for {len(pa)} frames")
+        return pa, la
+
     def classify(self, ptrs: np.ndarray, lens: np.ndarray | None, rules: "L3Rules | None" = None) -> np.ndarray:
+        ptrs, lens = self._burst_arrays(ptrs, lens)
         n = len(ptrs)
         ports = np.zeros(n, np.uint32)
         lp = None if lens is None else lens.ctypes.data
@@ -481,6 +493,7 @@ class Batcher:
 
     def submit(self, ptrs: np.ndarray, lens: np.ndarray | None, rules: "L3Rules | None" = None) -> Ticket:
         t = Ticket()
+        ptrs, lens = self._burst_arrays(ptrs, lens)
         lp = None if lens is None else lens.ctypes.data
         if rules is None:
             st = _batcher_submit(self._h, ptrs.ctypes.data, lp, len(ptrs), ctypes.byref(t))
@@ -581,9 +594,15 @@ class Service:
         ptrs = np.ascontiguousarray(ptrs, np.uint64)
         n = len(ptrs)
         ports = np.zeros(n, np.uint32)
-        lp = None if lens is None else np.ascontiguousarray(lens, np.uint32).ctypes.data
+        # the converted lengths stay bound to a local for the call (a
+        # temporary's .ctypes.data would point at freed memory)
+        la = None if lens is None else np.ascontiguousarray(lens, np.uint32)
+        if la is not None and len(la) != n:
+            raise ValueError(f"classify_burst: {len(la)} lengths for {n} frames")
+        lp = None if la is None or n == 0 else la.ctypes.data
         st = _service_classify_burst(self._h, rules.handle, ptrs.ctypes.data if n else None, lp, n, flags,
                                      ports.ctypes.data if n else None)
+        del la
         if st != OK and (st != ERR_TIMEOUT or _raise_timeout):
             _raise(st, "nffacl_service_classify_burst")
         return ports

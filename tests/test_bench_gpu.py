@@ -1,6 +1,6 @@
 """bench.py end to end on the GPU (-m gpu), at reduced sizes.
 
-* N = 1: the headline line plus the same-process C3 / C5 records, every
+* N = 1: the headline line plus the same-process C1 / C3 / C5 records, every
   record bit-exact against the oracle sample and carrying its own metric,
   roofline and CPU baseline.
 * N = 2 rehearsed on ONE GPU (NFFACL_BENCH_ONE_GPU=1, gloo — RCCL refuses two
@@ -42,7 +42,10 @@ def test_bench_n1_with_extra_configs(gpu_available):
     d = _json_line(r.stdout)
     assert d["metric"].startswith("Mpackets/s device-resident L3 ACL classify, 64B pkts @1k rules")
     assert d["bit_exact_sample"] and d["cpu_baseline"]["bit_exact_vs_gpu"]
-    assert set(d["configs"]) == {"c3", "c5"}
+    assert set(d["configs"]) == {"c1", "c3", "c5"}
+    assert list(d)[-1] == "summary" and d["summary"]["all_bit_exact"]
+    assert {"c2", "c1", "c3", "c5"} <= set(d["summary"])
+    assert d["configs"]["c1"]["config"]["rules_ip4"] == 4 and d["configs"]["c1"]["config"]["rules_ip6"] == 1
     for c, rec in d["configs"].items():
         assert "@1k rules" not in rec["metric"], rec["metric"]  # labelled per config
         assert rec["bit_exact_sample"] and rec["cpu_baseline"]["bit_exact_vs_gpu"], c

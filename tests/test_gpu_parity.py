@@ -552,15 +552,18 @@ def test_full_size_c3_hybrid(torch_cuda):
     np.testing.assert_array_equal(outs[nffacl.ALGO_AUTO].cpu().numpy().view(np.uint32)[idx], want)
 
 
-@pytest.mark.parametrize("coarse,dir8", [("1", "1"), ("0", "0")])
-def test_c5_flat_lds_layout_options(torch_cuda, monkeypatch, coarse, dir8):
+@pytest.mark.parametrize("coarse,dir8,rounds", [("1", "1", None), ("0", "0", None), ("1", "1", "2")])
+def test_c5_flat_lds_layout_options(torch_cuda, monkeypatch, coarse, dir8, rounds):
     """The flat-LDS layout options besides the default (u8 directories, no
     coarse slots): coarse address slots (five generalized slots: the NS = 5
     kernels) and u16 directories, on 64-byte slots and IMIX frames, against
-    the oracle."""
+    the oracle.  rounds "2" (ADVICE round 4, medium): generalized slots with
+    NFFACL_TUNE_ROUNDS=2 still launch their 4-round kernel with its scratch."""
     torch = torch_cuda
     monkeypatch.setenv("NFFACL_TUNE_COARSE", coarse)
     monkeypatch.setenv("NFFACL_TUNE_DIR8", dir8)
+    if rounds:
+        monkeypatch.setenv("NFFACL_TUNE_ROUNDS", rounds)
     g = synth.gen_rules(synth.SPECS["c5"], synth.RULE_SEEDS["c5"])
     rules, (a4, a6) = _rules_and_arrays(g.text)
     n = (1 << 16) + 3
@@ -576,6 +579,36 @@ def test_c5_flat_lds_layout_options(torch_cuda, monkeypatch, coarse, dir8):
         torch.cuda.synchronize()
         np.testing.assert_array_equal(port.cpu().numpy().view(np.uint32),
                                       oracle.classify_frames(frames, desc, a4, a6, threads=THREADS))
+
+
+@pytest.mark.parametrize("case", ["grid_overflow", "dir_overflow"])
+def test_c5_fine_grids_when_offsets_overflow_gpu(torch_cuda, case):
+    """ADVICE round 4 (high), on the GPU: C5 plus 300 rules that overflow a
+    fine grid's / a 1-D slot's u8 offsets (tests/test_index_compile.py
+    test_hybrid_fine_grids_when_offsets_overflow) compile to a table that
+    fits the LDS and classify exactly as the oracle, packets aimed at the
+    added rules included."""
+    torch = torch_cuda
+    g = synth.gen_rules(synth.SPECS["c5"], synth.RULE_SEEDS["c5"])
+    line = ("ANY 33.128.0.0/9 TCP ANY 8192:9000 Accept" if case == "grid_overflow"
+            else "ANY 44.55.66.77/32 UDP 1000:2000 ANY Reject")
+    text = g.text + (line + "\n") * 300
+    rules, (a4, a6) = _rules_and_arrays(text)
+    n = (1 << 16) + 9
+    slots = synth.gen_slots(g, n, 41)
+    for i in range(0, n, 37):
+        pk = slots[i * 64:(i + 1) * 64]
+        pk[12:14] = (0x08, 0x00)
+        pk[14] = 0x45
+        pk[23] = 6 if case == "grid_overflow" else 17
+        pk[30:34] = (33, 200, 1, 2) if case == "grid_overflow" else (44, 55, 66, 77)
+        pk[34:38] = (0x05, 0xDC, 0x21, 0x98)
+    with nffacl.Engine(rules, algo=nffacl.ALGO_HYBRID) as eng:
+        p, b = classify(torch, eng, slots, 64, n)
+        want = oracle.classify_slots(slots, 64, n, a4, a6, threads=THREADS)
+        np.testing.assert_array_equal(p, want)
+        np.testing.assert_array_equal(b, permit_bits(want))
+        assert (want[::37] != 0).any()
 
 
 @pytest.mark.parametrize("flat", [0, 1, 2])

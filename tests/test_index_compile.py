@@ -542,3 +542,42 @@ def test_hybrid_fine_slots_and_param_block(monkeypatch, cfg, env):
         assert fine and all(d.kind2 != KIND_NONE for d in fine)
         if cfg == "c5" and not env:
             assert info.fam[0].n_slots == 6
+
+
+def _c5_plus(extra_lines):
+    g = synth.gen_rules(synth.SPECS["c5"], synth.RULE_SEEDS["c5"])
+    return g, g.text + "".join(line + "\n" for line in extra_lines)
+
+
+@pytest.mark.parametrize("case", ["grid_overflow", "dir_overflow"])
+def test_hybrid_fine_grids_when_offsets_overflow(case):
+    """fine 2-D grids take their directory bytes off
+    the LDS budget in the u8 form.  A grid whose lists overflow the u8
+    offsets sheds the rules of its overflowing groups (they stay in their
+    1-D slots), and when a 1-D slot overflows them the directories re-size
+    for the wider form with the grids' bytes in that form taken off the
+    budget: the image always fits kHybLdsDirMaxBytes and the walk still
+    gives the oracle's first match.  grid_overflow: 300 rules (dst /9, dport
+    8192-9000) that the dst x dport grid would put into one bucket;
+    dir_overflow: 300 copies of one dst /32 rule (one 1-D bucket of 300
+    entries).  Both end in the u16 form beside C5's own grids."""
+    if case == "grid_overflow":
+        extra = ["ANY 33.128.0.0/9 TCP ANY 8192:9000 Accept"] * 300
+    else:
+        extra = ["ANY 44.55.66.77/32 UDP 1000:2000 ANY Reject"] * 300
+    g, text = _c5_plus(extra)
+    n = 1 << 12
+    slots = synth.gen_slots(g, n, synth.PACKET_SEEDS["c5"] + 11)
+    # a few packets aimed at the added rules (IPv4 TCP, dst 33.200.1.2 / 44.55.66.77)
+    for i in range(0, n, 97):
+        pk = slots[i * 64:(i + 1) * 64]
+        pk[12:14] = (0x08, 0x00)
+        pk[14] = 0x45
+        pk[23] = 6 if case == "grid_overflow" else 17
+        pk[30:34] = (33, 200, 1, 2) if case == "grid_overflow" else (44, 55, 66, 77)
+        pk[34:38] = (0x05, 0xDC, 0x21, 0x98)  # sport 1500, dport 8600
+    info = check_hybrid(text, slots, n)
+    assert info.lds_dwords * 4 <= 135 * 1024
+    fine = [info.fam[0].dims[k] for k in range(4, info.fam[0].n_slots) if info.fam[0].dims[k].n_rules]
+    assert fine and all(d.max_list < 300 for d in fine)  # the C5 rules' own grids stay, without the hot bucket
+    assert info.fam[0].dims[0].dir8 == 0 and info.fam[0].dims[0].off_dir16 != 0  # u16 form

@@ -141,6 +141,13 @@ def test_scalar_call_on_burst_service_and_vlan(torch_cuda, golden):
         with pytest.raises(nffacl.NFError):  # > 32 packets
             s.classify_burst(rules, np.tile(ptrs, 2), np.tile(lens, 2))
         assert len(s.classify_burst(rules, ptrs[:0], lens[:0])) == 0
+        # lengths given as int64 / a list are converted
+        # into an array that stays alive for the call (not a freed temporary)
+        want = _want(g.text, slots, 32)
+        for ln in (lens.astype(np.int64), [int(x) for x in lens]):
+            np.testing.assert_array_equal(s.classify_burst(rules, ptrs, ln), want)
+        with pytest.raises(ValueError):
+            s.classify_burst(rules, ptrs, lens[:5])
 
 
 @pytest.mark.parametrize("burst", [False, True])

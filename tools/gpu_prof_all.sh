@@ -1,6 +1,6 @@
 #!/bin/bash
-# Round 4 profiles: tools/gpu_prof.sh (kernel trace + HBM / SQ / TCC / TA
-# counter passes) for C5, C3 and C2, then their summaries.  usage: gpu_prof_r4.sh TAG
+# Profiles of every config: tools/gpu_prof.sh (kernel trace + HBM / SQ / TCC / TA
+# counter passes) for C5, C3 and C2, then their summaries.  usage: gpu_prof_all.sh TAG
 R="$GRAFT_REPO_ROOT"; T=$1; cd "$R"
 for c in c5 c3 c2; do
   bash tools/gpu_prof.sh "${T}_$c" --config $c || { echo "prof $c failed"; exit 1; }
