@@ -62,7 +62,7 @@
 extern "C" {
 #endif
 
-#define NFFACL_ABI_VERSION 5
+#define NFFACL_ABI_VERSION 6
 
 /* Only the entry points below are exported from libnffacl.so (built with
  * -fvisibility=hidden). */
@@ -162,10 +162,23 @@ NFFACL_API int nffacl_rules_get6(const nffacl_rules *rules, size_t i, nffacl_rul
  * the rule set it was given.  A rule set must outlive the calls using it. */
 NFFACL_API int nffacl_rules_prepare(const nffacl_rules *rules, int hip_device);
 
-/* The HIP device on the calling thread's NUMA node (the GPU a flow-function
- * clone pinned to that node should use; device 0 when none matches), or
- * NFFACL_ERR_NO_DEVICE.  Replaces the binding's former hard-wired GPU 0. */
+/* The HIP device the calling thread (a flow-function clone) should use, or
+ * NFFACL_ERR_NO_DEVICE: ABI 6 spreads the clones of a NUMA node over ALL of
+ * that node's GPUs — the device is nffacl_pick_device() of the thread's CPU
+ * (its rank among its node's CPUs, modulo the node's device count; every
+ * device when none is on the node).  Stable per thread: its first call
+ * decides.  nff-go pins every clone to a core (flow/scheduler.go:283-289,
+ * internal/low/low.go:654-666), so the clones of a 2-socket, 8-GPU node land
+ * on all 8 GPUs (ABI 5 gave every clone the node's first GPU).  Replaces the
+ * binding's former hard-wired GPU 0. */
 NFFACL_API int nffacl_local_device(void);
+
+/* The device map behind nffacl_local_device, on any topology: CPU `cpu`
+ * (cpu_node[c] = NUMA node of CPU c, -1 unknown; n_cpus entries) gets device
+ * local[rank % |local|], where local = the devices d with dev_node[d] equal
+ * to the CPU's node (all devices when none) and rank = the number of CPUs
+ * below `cpu` on its node.  NFFACL_ERR_INVALID_ARG on bad arguments. */
+NFFACL_API int nffacl_pick_device(int cpu, const int *cpu_node, int n_cpus, const int *dev_node, int n_devs);
 
 /* The NUMA node of a HIP device's PCIe attachment (>= 0), or a negative
  * status (NFFACL_ERR_INVALID_ARG, NFFACL_ERR_NO_DEVICE; NFFACL_ERR_HIP when
@@ -509,6 +522,32 @@ NFFACL_API int nffacl_l2_classify_frames_device(nffacl_l2engine *eng, const uint
  * request).  h_port / h_permit (one byte per packet) may be NULL. */
 NFFACL_API int nffacl_l2_classify_host(nffacl_l2engine *eng, const uint8_t *h_slots, uint32_t stride,
                                        uint64_t n, uint32_t *h_port, uint8_t *h_permit);
+
+/* ---- device group: one process, several GPUs (ABI 6) -------------------
+ * The reference's multi-core deployment is ONE process whose core-pinned
+ * clones share one *L3Rules (flow/scheduler.go:283-289, packet/acl.go:
+ * 495-506); a group lets such a host spread one batch over several GPUs
+ * without a process per GPU.  nffacl_group_create opens one RCCL
+ * communicator per device (ncclCommInitAll), compiles `rules` once on the
+ * host, uploads the table to hip_devices[0] (the root) and ncclBroadcasts
+ * it to the others over xGMI.  The group owns its tables (the rule set may
+ * be freed afterwards); a rule reload is a new group.  Devices must be
+ * distinct.  NFFACL_ERR_NO_DEVICE without HIP devices. */
+typedef struct nffacl_group nffacl_group;
+NFFACL_API int nffacl_group_create(const int *hip_devices, int n, const nffacl_rules *rules, nffacl_group **out);
+NFFACL_API int nffacl_group_size(const nffacl_group *g);
+/* L3ACLPort / L3ACLPermit of n packets resident on the ROOT device (slots as
+ * nffacl_classify_device; d_port / d_permit_bits on the root too, either may
+ * be NULL but not both): 64-aligned shards go to the group's devices by
+ * ncclSend/ncclRecv (the root keeps the first), every device classifies its
+ * shard, and the verdicts (ports, permit words) come back by ncclSend/
+ * ncclRecv into the root's arrays.  Enqueued on `stream` (a root-device
+ * hipStream_t; NULL = default) and the group's own per-device streams:
+ * returns at once; the verdicts are complete when `stream` is.  Calls on one
+ * group are serialised (they share its communicators). */
+NFFACL_API int nffacl_group_classify_device(nffacl_group *g, const uint8_t *d_slots, uint32_t stride, uint64_t n,
+                                            uint32_t *d_port, uint64_t *d_permit_bits, void *stream);
+NFFACL_API void nffacl_group_destroy(nffacl_group *g);
 
 /* ---- misc ------------------------------------------------------------- */
 NFFACL_API const char *nffacl_strerror(int status);

@@ -346,6 +346,7 @@ struct IndexedArgs {
     uint32_t stage_dwords;  // leading dwords staged in LDS (multiple of 4)
     uint32_t flags;         // NFFACL_PARSE_*
     uint32_t dir8;          // HYBRID: two-level directories carry u8 offsets (SplitTab::bounds)
+    uint32_t dir16;         // HYBRID: two-level directories (u16 offsets, or u8 with dir8); 0 = plain u32
     uint32_t generic;       // HYBRID flat forms: slots key on SlotArgs::f1/f2 (else slot s on field s)
     uint32_t live;          // positional flat forms: bit s set iff slot s lists rules in some family
     uint32_t off_params;    // flat-LDS positional forms: dword offset (in the LDS image) of the slot
@@ -381,6 +382,9 @@ enum TableMode : int {
     kTabFlatLds4U = 8, // the same, entry loads of every non-empty round issued
                        // without a per-lane branch (tables with many candidates
                        // per packet: CompiledTable::flat_uncond)
+    kTabFlatLdsP = 11, // flat-LDS, positional slots, pipelined walk (classify_flat_pipe,
+                       // round 5): family-split candidate streams, one pass's
+                       // IPv6 round and IPv4 windows of 4 + 3 rounds in flight together
     kTabFlatLdsG = 10, // flat-LDS over generalized slots (CompiledTable::slots_g:
                        // the coarse / SLOTS2D layout experiments), 4 rounds,
                        // branch-free loads — a kernel of its own, so that the
@@ -408,7 +412,7 @@ struct LdsTab {
     static constexpr bool kFreeLoads = true;  // out-of-range LDS reads return 0, never fault
     __device__ __forceinline__ uint32_t ld(uint32_t i) const { return lds_tab[i]; }
     __device__ __forceinline__ void bounds(uint32_t dir, uint32_t, uint32_t t, uint32_t &lo, uint32_t &hi,
-                                           bool = false) const {
+                                           uint32_t = 0) const {
         bounds32(*this, dir, t, lo, hi);
     }
     __device__ __forceinline__ u32x4 ld4(uint32_t i) const {
@@ -421,7 +425,7 @@ struct GlobalTab {
     const uint32_t *__restrict__ p;
     __device__ __forceinline__ uint32_t ld(uint32_t i) const { return p[i]; }
     __device__ __forceinline__ void bounds(uint32_t dir, uint32_t, uint32_t t, uint32_t &lo, uint32_t &hi,
-                                           bool = false) const {
+                                           uint32_t = 0) const {
         bounds32(*this, dir, t, lo, hi);
     }
     __device__ __forceinline__ u32x4 ld4(uint32_t i) const {
@@ -429,6 +433,22 @@ struct GlobalTab {
         return *reinterpret_cast<const u32x4 *>(p + i);
     }
 };
+// List bounds of bucket t from its group's base b and 4-bit counts
+// (w1:w0, bucket 16g + i in bits 4i..4i+3): lo = b + the counts before t,
+// hi = lo + count(t).  The counts before t are the top 4 (t & 15) bits of
+// x << (64 - 4 (t & 15)), summed bytewise (each byte <= 60) by one v_sad_u8.
+__device__ __forceinline__ void nib_bounds(uint32_t b, uint32_t w0, uint32_t w1, uint32_t t, uint32_t &lo,
+                                           uint32_t &hi) {
+    const uint64_t x = uint64_t(w1) << 32 | w0;
+    const uint32_t j4 = (t & 15u) * 4u;
+    const uint64_t p = (x << (63u - j4)) << 1;  // counts of buckets 0..j-1 in the top bits (j = 0: none)
+    const uint32_t pl = static_cast<uint32_t>(p), ph = static_cast<uint32_t>(p >> 32);
+    constexpr uint32_t M = 0x0F0F0F0Fu;
+    const uint32_t bytes = (pl & M) + ((pl >> 4) & M) + (ph & M) + ((ph >> 4) & M);
+    lo = b + __builtin_amdgcn_sad_u8(bytes, 0u, 0u);
+    hi = lo + (static_cast<uint32_t>(x >> j4) & 15u);
+}
+
 // HYBRID lane form: directories (ld) staged in LDS, entries (ld4) global.
 // IN_LDS = false reads the same directory image from global memory (the
 // persistent scalar-call consumer, service.hip, which stages nothing).
@@ -444,9 +464,15 @@ struct DirTab {
     // two-level directory (table.hpp): dir[t] = base[t >> 6] + dir16[t], or
     // with dir8 (wave-uniform) base[t >> 4] + dir8[t]
     __device__ __forceinline__ void bounds(uint32_t dir, uint32_t dir16, uint32_t t, uint32_t &lo, uint32_t &hi,
-                                           bool dir8 = false) const {
+                                           uint32_t dir8 = 0) const {
         if (dir16 == 0u) {
             bounds32(*this, dir, t, lo, hi);
+            return;
+        }
+        if (dir8 == 2u) {  // 4-bit counts (table.hpp kDir4GroupShift)
+            const uint32_t g = t >> kDir4GroupShift;
+            const uint32_t b = ld(dir + g);
+            nib_bounds(b, ld(dir16 + 2u * g), ld(dir16 + 2u * g + 1u), t, lo, hi);
             return;
         }
         if (dir8) {
@@ -589,7 +615,7 @@ __device__ __forceinline__ uint32_t classify_indexed(const T &tab, const Indexed
         const uint32_t base = par(s4.off_ent, s6.off_ent);
         const uint32_t t = key[s] >> shift;  // < n_buckets for any key: both reads in range
         uint32_t lo, hi;
-        tab.bounds(dir, C::kLds ? 0u : fam_sel(v6, s4.off_dir16, s6.off_dir16), t, lo, hi, a.dir8 != 0u);
+        tab.bounds(dir, C::kLds ? 0u : fam_sel(v6, s4.off_dir16, s6.off_dir16), t, lo, hi, a.dir8);
         c[s] = C::of(base + times_ew(lo, v6));
         // (a select of the bound, not of the cursor: otherwise the compiler
         // sank the hi read into a branch, two LDS round trips instead of one)
@@ -882,7 +908,7 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
                 t = ((addr >> shift) << bits2) | (port >> shift2);
             }
             uint32_t hi;
-            DirTab<DIRS_IN_LDS>{a.tab, a.tab_dwords}.bounds(dir, dir16, t, st[s], hi, a.dir8 != 0u);
+            DirTab<DIRS_IN_LDS>{a.tab, a.tab_dwords}.bounds(dir, dir16, t, st[s], hi, a.dir8);
             ln[s] = mine ? hi - st[s] : 0u;
         }
     } else {
@@ -895,7 +921,7 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
                            (pick(fam_sel(v6, s4.f2, s6.f2)) >> (fam_sel(v6, s4.shift2, s6.shift2)));
         if (LDS_DIRS) {
             uint32_t hi;
-            DirTab<DIRS_IN_LDS>{a.tab, a.tab_dwords}.bounds(dir, fam_sel(v6, s4.off_dir16, s6.off_dir16), t, st[s], hi, a.dir8 != 0u);
+            DirTab<DIRS_IN_LDS>{a.tab, a.tab_dwords}.bounds(dir, fam_sel(v6, s4.off_dir16, s6.off_dir16), t, st[s], hi, a.dir8);
             ln[s] = mine ? hi - st[s] : 0u;
         } else {
             // generalized slots: a family's unused slots (f1 == kFZero) read nothing
@@ -1097,6 +1123,320 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
     if (ballot(rd)) {
         const uint32_t r = static_cast<uint32_t>(best >> 32);
         if (rd) out = g1(fam_sel(v6, a.f4.off_cold, a.f6.off_cold) + r);
+        settle(out);
+    }
+    return out;
+}
+
+// ---- FLAT, pipelined (round 5): family-split windows, a batch's rounds in flight together ----
+//
+// classify_flat (above) runs a batch's candidates window by window: marks,
+// scans, entry loads of 4 rounds, then their tests, and only then the next
+// window — C5 (6.5 candidates per packet, 7 rounds) waits out two dependent
+// entry round trips per batch, and every round carries the IPv6 machinery
+// (12-dword entries, a per-round ballot and stage for address words 1..3)
+// although IPv6 candidates are ~7 % of the total.  Here:
+//  * the candidates are laid out per family: the IPv4 packets' lists form one
+//    stream, the IPv6 packets' another, each with its own exclusive scan;
+//  * a pass marks, locates and issues the loads of up to one IPv6 round and
+//    IPv4 windows of 4 and 3 rounds — the window scratch (marks, deltas) is
+//    free again once a window's candidates are located, so the LDS footprint
+//    is classify_flat's — and tests them only once the loads behind them are
+//    in flight (IPv6 round and first window issued, IPv6 round tested, second
+//    window issued, both windows tested): about one exposed entry round trip
+//    per batch (C5: 390 IPv4 + 27 IPv6 candidates per batch, one pass);
+//  * IPv4 rounds hold 6-dword entries and test them with no IPv6 branch; the
+//    IPv6 round tests all of its lanes' address words 1..3 at once;
+//  * directory lookups are straight-line over every slot (the form is a
+//    wave-uniform table property), so their LDS reads overlap.
+// Semantics are classify_flat's: the minimum (rule index << 32 | output code)
+// over all candidates that pass the full rule test is the first match
+// (acl.go:522-565), residual entries after.  Positional slots, directories
+// and parameter block staged in LDS (flat-LDS tables).
+
+// List bounds of this packet in every positional slot (directories in LDS).
+template <int NS>
+__device__ __forceinline__ void flat_bounds_lds(const IndexedArgs &a, const Fields &f, uint32_t (&st)[NS],
+                                                uint32_t (&ln)[NS]) {
+    const bool v6 = f.is6;
+    const bool mine = f.is4 || f.is6;
+    const uint32_t ks = __builtin_bswap32(f.s[0]), kd = __builtin_bswap32(f.t[0]);
+    const uint32_t sport = f.ports & 0xFFFFu, dport = f.ports >> 16;
+    const uint32_t half = v6 ? 16u : 0u;
+    // every slot's parameters first (broadcast ds_read_b128 each), then the
+    // bucket reads: no slot waits for another's LDS round trip
+    u32x4 P[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+        P[s] = *(lds_u32x4 *)(uintptr_t)(lds_base() + 4u * (a.off_params + kFlatParamDwords * s));
+    uint32_t t[NS], dir[NS], d16[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        const uint32_t shift = __builtin_amdgcn_ubfe(P[s].x, half, 16);
+        dir[s] = __builtin_amdgcn_ubfe(P[s].y, half, 16);
+        d16[s] = __builtin_amdgcn_ubfe(P[s].z, half, 16);
+        if (s < 4) {  // 1-D: [dst, src, dport, sport]
+            const uint32_t key = s == kFDst ? kd : s == kFSrc ? ks : s == kFDport ? dport : sport;
+            t[s] = key >> shift;
+        } else {      // fine 2-D grids: [dst x dport, src x dport, dst x sport, src x sport]
+            const uint32_t fine = __builtin_amdgcn_ubfe(P[s].w, half, 16);
+            const uint32_t addr = (s & 1) ? ks : kd, port = s < 6 ? dport : sport;
+            t[s] = ((addr >> shift) << (fine & 0xFFu)) | (port >> (fine >> 8));
+        }
+    }
+    auto lds2 = [](uint32_t dw, uint32_t &x, uint32_t &y) {  // one ds_read2_b32 (or b64 when aligned)
+        x = lds_tab[dw];
+        y = lds_tab[dw + 1];
+    };
+    uint32_t lo[NS], hi[NS];
+    if (a.dir8 == 2u) {  // two-level, 4-bit counts (table.hpp kDir4GroupShift)
+        uint32_t b[NS], w0[NS], w1[NS];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            const uint32_t g = t[s] >> kDir4GroupShift;
+            b[s] = lds_tab[dir[s] + g];
+            lds2(d16[s] + 2u * g, w0[s], w1[s]);  // one ds_read_b64 (8-byte aligned pair)
+        }
+#pragma unroll
+        for (int s = 0; s < NS; ++s) nib_bounds(b[s], w0[s], w1[s], t[s], lo[s], hi[s]);
+    } else if (a.dir8) {  // two-level, u8 offsets (table.hpp kDir8GroupShift)
+        uint32_t b0[NS], b1[NS], w0[NS], w1[NS];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            lds2(dir[s] + (t[s] >> kDir8GroupShift), b0[s], b1[s]);
+            lds2(d16[s] + (t[s] >> 2), w0[s], w1[s]);
+        }
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            const uint32_t x = __builtin_amdgcn_alignbit(w1[s], w0[s], (t[s] & 3u) * 8u);
+            lo[s] = b0[s] + (x & 0xFFu);
+            hi[s] = (((t[s] + 1u) & ((1u << kDir8GroupShift) - 1u)) == 0u ? b1[s] : b0[s]) + ((x >> 8) & 0xFFu);
+        }
+    } else if (a.dir16) {  // two-level, u16 offsets
+        uint32_t b0[NS], b1[NS], w0[NS], w1[NS];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            lds2(dir[s] + (t[s] >> kDir16GroupShift), b0[s], b1[s]);
+            lds2(d16[s] + (t[s] >> 1), w0[s], w1[s]);
+        }
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            const bool odd = (t[s] & 1u) != 0u;
+            lo[s] = b0[s] + (odd ? w0[s] >> 16 : w0[s] & 0xFFFFu);
+            hi[s] = (((t[s] + 1u) >> kDir16GroupShift) != (t[s] >> kDir16GroupShift) ? b1[s] : b0[s]) +
+                    (odd ? w1[s] & 0xFFFFu : w0[s] >> 16);
+        }
+    } else {  // plain u32
+#pragma unroll
+        for (int s = 0; s < NS; ++s) lds2(dir[s] + t[s], lo[s], hi[s]);
+    }
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        st[s] = lo[s];
+        ln[s] = mine ? hi[s] - lo[s] : 0u;
+    }
+}
+
+// `prefetch()` is called once, in the first pass, after the tests of its
+// IPv6 round and first IPv4 window: the kernel issues the next batch's packet
+// loads there (load mode 6) — younger than every entry load of the pass, so
+// no test waits for them (vmcnt counts in order), and into registers the
+// first window's entries have just freed.
+template <int NS, class PF>
+__device__ __forceinline__ uint32_t classify_flat_pipe(const IndexedArgs &a, const Fields &f, FlatScratch<4> &W,
+                                                       uint32_t lane, PF &&prefetch) {
+    const bool v6 = f.is6;
+    const uint32_t ks = __builtin_bswap32(f.s[0]), kd = __builtin_bswap32(f.t[0]);
+    // list bounds, family streams: recomputed by every pass (a second pass
+    // is rare: > 7 IPv4 rounds or > 1 IPv6 round in a batch), so that they
+    // are dead while a pass's entry loads are in flight
+    uint32_t st[NS], ln[NS], off = 0, T4 = 0, T6 = 0;
+    auto streams = [&]() {
+        flat_bounds_lds<NS>(a, f, st, ln);
+        uint32_t total = 0;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) total += ln[s];
+        const uint32_t t4 = v6 ? 0u : total, t6 = v6 ? total : 0u;
+        const uint32_t i4 = wave_incl_sum(t4), i6 = wave_incl_sum(t6);
+        T4 = __builtin_amdgcn_readlane(i4, 63);
+        T6 = __builtin_amdgcn_readlane(i6, 63);
+        off = v6 ? i6 - t6 : i4 - t4;  // this packet's first candidate in its family's stream
+    };
+    W.best[lane] = ~0ull;
+    const uint8_t *tab8 = reinterpret_cast<const uint8_t *>(a.tab);
+    // Mark the lists of family `fam6` overlapping the window [w, w + 64 RR):
+    // mark[pos] = (owner lane << 19 | slot << 16 | pos << 8 | owner's protocol)
+    // + 1 at the list's first position in the window, delta[pos] = byte
+    // offset (from a.tab, mod 2^32) of the list's "candidate 0" entry.
+    auto mark = [&](bool fam6, uint32_t w, auto rr) {
+        constexpr int RR = decltype(rr)::value;
+        wave_lds_sync();  // (the previous window's mark and delta reads come first)
+#pragma unroll
+        for (int j = 0; j < RR; ++j) W.mark[64 * j + lane] = 0u;
+        wave_lds_sync();
+        if (v6 == fam6) {
+            const uint32_t ew = fam6 ? kHybEnt6Dwords : kHybEnt4Dwords;
+            const uint32_t fb = fam6 ? a.f6.off_ent_base : a.f4.off_ent_base;
+            uint32_t so = off;
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                if (ln[s] != 0u && so < w + 64u * RR && so + ln[s] > w) {
+                    const uint32_t pos = so > w ? so - w : 0u;
+                    W.mark[pos] = (lane << 19 | static_cast<uint32_t>(s) << 16 | pos << 8 | (f.proto & 0xFFu)) + 1u;
+                    W.delta[pos] = (fb + (st[s] - so) * ew) << 2;
+                }
+                so += ln[s];
+            }
+        }
+        wave_lds_sync();
+    };
+    // Locate the RR rounds of a marked window and issue their entry loads
+    // (lanes past the stream load the table's first bytes, untested).
+    // mk[j] = the candidate's mark - 1 (owner, protocol), k = stream number.
+    auto locate = [&](uint32_t w, uint32_t T, auto six, auto rr, uint32_t (&mk)[4], u32x3 (&A)[4], u32x3 (&B)[4],
+                      u32x3 &C, u32x3 &D) {
+        constexpr bool SIX = decltype(six)::value;
+        constexpr uint32_t ent_bytes = 4u * (SIX ? kHybEnt6Dwords : kHybEnt4Dwords);
+        constexpr int RR = decltype(rr)::value;
+        static_assert(!SIX || RR == 1, "IPv6 rounds: one per pass");
+        uint32_t scan[RR];
+#pragma unroll
+        for (int j = 0; j < RR; ++j) scan[j] = wave_incl_max(W.mark[64 * j + lane]);
+        uint32_t carry = 0;
+#pragma unroll
+        for (int j = 0; j < RR; ++j) {
+            const uint32_t m = max(scan[j], carry);
+            if (j + 1 < RR) carry = __builtin_amdgcn_readlane(m, 63);
+            mk[j] = m - 1u;
+            const uint32_t k = w + 64u * j + lane;
+            const uint32_t dp = W.delta[(mk[j] >> 8) & 0xFFu];
+            const uint32_t o = k < T ? dp + __umul24(k, ent_bytes) : 0u;
+            const uint32_t *e = reinterpret_cast<const uint32_t *>(tab8 + o);
+            A[j] = ld3(e);
+            B[j] = ld3(e + 3);
+            if constexpr (SIX) {
+                C = ld3(e + 6);
+                D = ld3(e + 9);
+            }
+        }
+    };
+    // Test round j of a window: the owner packet's fields by ds_bpermute;
+    // a passing candidate posts (rule index << 32 | output code) to the
+    // owner's LDS minimum.
+    auto post = [&](bool pass, uint32_t o, const u32x3 &A, const u32x3 &B) {
+        if (pass)
+            atomicMin(reinterpret_cast<unsigned long long *>(&W.best[o]),
+                      static_cast<unsigned long long>(A.z >> kEntIndexShift) << 32 | (B.z >> kHybOutShift));
+    };
+    auto test4 = [&](uint32_t w, auto rr, const uint32_t (&mk)[4], const u32x3 (&A)[4], const u32x3 (&B)[4]) {
+        constexpr int RR = decltype(rr)::value;
+#pragma unroll
+        for (int j = 0; j < RR; ++j) {
+            const uint32_t o = mk[j] >> 19;
+            const uint32_t oks = bperm(ks, o), okd = bperm(kd, o), opt = bperm(f.ports, o);
+            const bool valid = w + 64u * j + lane < T4;
+            const bool pass = valid & (hyb_miss(A[j], B[j], oks, okd, mk[j] & 0xFFu, opt) == 0u);
+            post(pass, o, A[j], B[j]);
+        }
+    };
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
+    using I4 = std::integral_constant<int, 4>;
+    // One pass: up to one IPv6 round from w6 and IPv4 windows of R0 (<= 4)
+    // and R1 (<= 3) rounds from w4 and w4 + 256.
+    auto pass = [&](uint32_t w4, uint32_t w6, bool do6, auto r0, auto r1) {
+        constexpr int R0 = decltype(r0)::value, R1 = decltype(r1)::value;
+        uint32_t mk6[4], mkA[4], mkB[4];
+        u32x3 A6[4], B6[4], C6, D6, AA[4], BA[4], AB[4], BB[4], cd;
+        if (do6) {
+            mark(true, w6, I1{});
+            locate(w6, T6, std::true_type{}, I1{}, mk6, A6, B6, C6, D6);
+        }
+        if constexpr (R0 > 0) {
+            mark(false, w4, r0);
+            locate(w4, T4, std::false_type{}, r0, mkA, AA, BA, cd, cd);
+        }
+        if (do6) {  // the IPv6 round: every lane's address words 1..3 against its owner's
+            const uint32_t o = mk6[0] >> 19;
+            const uint32_t oks = bperm(ks, o), okd = bperm(kd, o), opt = bperm(f.ports, o);
+            uint32_t os[4] = {0, 0, 0, 0}, ot[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int q = 1; q < 4; ++q) {
+                os[q] = bperm(__builtin_bswap32(f.s[q]), o);
+                ot[q] = bperm(__builtin_bswap32(f.t[q]), o);
+            }
+            const bool valid = w6 + lane < T6;
+            // (one combined mismatch word: no short-circuit branch)
+            const uint32_t miss6 = hyb_miss(A6[0], B6[0], oks, okd, mk6[0] & 0xFFu, opt) |
+                                   hyb_miss6(C6, D6, B6[0].z, os, ot);
+            const bool pass6 = valid && miss6 == 0u;
+            post(pass6, o, A6[0], B6[0]);
+        }
+        if constexpr (R1 > 0) {
+            mark(false, w4 + 256u, r1);
+            locate(w4 + 256u, T4, std::false_type{}, r1, mkB, AB, BB, cd, cd);
+        }
+        if constexpr (R0 > 0) test4(w4, r0, mkA, AA, BA);
+        if (w4 == 0u) prefetch();  // (the first pass)
+        if constexpr (R1 > 0) test4(w4 + 256u, r1, mkB, AB, BB);
+    };
+    using I0 = std::integral_constant<int, 0>;
+    uint32_t w4 = 0, w6 = 0;
+    while (true) {
+        streams();
+        if (w4 >= T4 && w6 >= T6) {
+            if (w4 == 0u && w6 == 0u) prefetch();  // a batch without candidates runs no pass
+            break;
+        }
+        const uint32_t rem4 = T4 > w4 ? T4 - w4 : 0u;  // wave-uniform
+        const bool do6 = w6 < T6;
+        const uint32_t r = (rem4 + 63u) / 64u;  // IPv4 rounds left: 0..7 in this pass (more: next pass)
+        if (r >= 7) pass(w4, w6, do6, I4{}, I3{});
+        else if (r == 6) pass(w4, w6, do6, I4{}, I2{});
+        else if (r == 5) pass(w4, w6, do6, I4{}, I1{});
+        else if (r == 4) pass(w4, w6, do6, I4{}, I0{});
+        else if (r == 3) pass(w4, w6, do6, I3{}, I0{});
+        else if (r == 2) pass(w4, w6, do6, I2{}, I0{});
+        else if (r == 1) pass(w4, w6, do6, I1{}, I0{});
+        else pass(w4, w6, do6, I0{}, I0{});
+        wave_lds_sync();
+        w4 += 448u;
+        w6 += 64u;
+        if (w4 >= T4 && w6 >= T6) break;
+    }
+    uint64_t best = W.best[lane];  // ~0 or rule index << 32 | output code
+    // rules with no selective key: wave-uniform scan in rule order per family
+#pragma unroll
+    for (int fam = 0; fam < 2; ++fam) {
+        const FamArgs &fa = fam ? a.f6 : a.f4;
+        const bool in_fam = fam ? f.is6 : f.is4;
+        const uint32_t ew = fam ? kHybEnt6Dwords : kHybEnt4Dwords;
+        for (uint32_t i = 0; i < fa.n_resid; ++i) {
+            const uint32_t *e = a.tab + fa.off_resid + i * ew;
+            const u32x3 RA = ld3(e), RB = ld3(e + 3);
+            const uint32_t ri = RA.z >> kEntIndexShift;
+            const bool want = in_fam && ri < uint32_t(best >> 32);
+            if (!ballot(want)) break;  // residual list ascends too
+            bool ok = want && hyb_miss(RA, RB, ks, kd, f.proto, f.ports) == 0u;
+            if (fam && ballot(ok)) {
+                uint32_t sb[4] = {0, 0, 0, 0}, tb[4] = {0, 0, 0, 0};
+#pragma unroll
+                for (int q = 1; q < 4; ++q) {
+                    sb[q] = __builtin_bswap32(f.s[q]);
+                    tb[q] = __builtin_bswap32(f.t[q]);
+                }
+                if (ok) ok = hyb_miss6(ld3(e + 6), ld3(e + 9), RB.z, sb, tb) == 0u;
+            }
+            best = ok ? (uint64_t(ri) << 32 | (RB.z >> kHybOutShift)) : best;
+        }
+    }
+    const bool hit = best != ~0ull;
+    uint32_t out = hit ? static_cast<uint32_t>(best) : 0u;
+    const bool rd = hit && out == kHybOutEscape;
+    if (ballot(rd)) {
+        const uint32_t r = static_cast<uint32_t>(best >> 32);
+        if (rd) out = a.tab[fam_sel(v6, a.f4.off_cold, a.f6.off_cold) + r];
         settle(out);
     }
     return out;

@@ -425,6 +425,7 @@ uint64_t entries_at(const DimBuild &d, uint32_t rb) {
 // LDS bytes of a directory of nb buckets in form fmt: 0 plain u32, 16 two-level
 // u16 (groups of 64), 8 two-level u8 (groups of 16).
 double dir_form_bytes(double nb, int fmt) {
+    if (fmt == 4) return 0.5 * (nb + 16) + 8 + 4.0 * (std::floor(nb / (1u << kDir4GroupShift)) + 2);
     if (fmt == 8) return 1.0 * (nb + 8) + 4.0 * (std::floor(nb / (1u << kDir8GroupShift)) + 2);
     if (fmt == 16) return 2.0 * (nb + 4) + 4.0 * (std::floor(nb / (1u << kDir16GroupShift)) + 2);
     return 4.0 * (nb + 1);
@@ -432,6 +433,29 @@ double dir_form_bytes(double nb, int fmt) {
 
 // LDS directories start at `per_rule` buckets per rule (then narrow to the budget).
 thread_local size_t g_dir_per_rule = 4;  // CompileOptions::dir_per_rule of this thread's compile (compile_table)
+thread_local double g_dir_sbias = 0.0;   // CompileOptions::dir_sbias / 100
+
+// Size-biased mean list length of a slot at radix b: sum(len^2) / sum(len),
+// the list a key drawn like the rules' own keys lands in (traffic that
+// matches rules), where the uniform-key mean (entries / buckets) is the list
+// of a random key.
+double size_biased_at(const DimBuild &d, uint32_t b) {
+    const uint32_t shift = d.key_bits - b;
+    const size_t nb = size_t(1) << b;
+    std::vector<int32_t> diff(nb + 1, 0);
+    for (const KeyRange &r : d.ranges) {
+        ++diff[r.lo >> shift];
+        --diff[size_t(r.hi >> shift) + 1];
+    }
+    double s1 = 0, s2 = 0;
+    int64_t c = 0;
+    for (size_t t = 0; t < nb; ++t) {
+        c += diff[t];
+        s1 += double(c);
+        s2 += double(c) * double(c);
+    }
+    return s1 > 0 ? s2 / s1 : 0.0;
+}
 
 void size_directories(DimBuild *const *all, const double *weight, int nd, size_t budget, int fmt) {
     std::vector<uint32_t> rb(nd);
@@ -445,7 +469,10 @@ void size_directories(DimBuild *const *all, const double *weight, int nd, size_t
         if (d.rules.empty()) { rb[i] = 1; continue; }
         rb[i] = std::max(1u, std::min(pick_rb(d.rules.size(), d.key_bits, g_dir_per_rule), d.max_rb));
         mean[i].assign(rb[i] + 1, 0.0);
-        for (uint32_t b = 1; b <= rb[i]; ++b) mean[i][b] = double(entries_at(d, b)) / double(1u << b);
+        for (uint32_t b = 1; b <= rb[i]; ++b) {
+            mean[i][b] = double(entries_at(d, b)) / double(1u << b);
+            if (g_dir_sbias > 0) mean[i][b] = (1.0 - g_dir_sbias) * mean[i][b] + g_dir_sbias * size_biased_at(d, b);
+        }
     }
     double total = 0;
     for (int i = 0; i < nd; ++i) total += bytes(i, rb[i]);
@@ -963,6 +990,11 @@ void build_hybrid(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vec
     // does a directory's every group fit the offsets of form f (8: u8, 16: u16, 0: plain)?
     auto dir_fits = [](const std::vector<uint32_t> &dir, int f) {
         if (f == 0) return true;
+        if (f == 4) {  // 4-bit counts: every list <= 15 entries
+            for (size_t t = 0; t + 1 < dir.size(); ++t)
+                if (dir[t + 1] - dir[t] > 15u) return false;
+            return true;
+        }
         const uint32_t gs = f == 8 ? kDir8GroupShift : kDir16GroupShift;
         const uint32_t lim = f == 8 ? 0xFFu : 0xFFFFu;
         for (size_t t = 0; t < dir.size(); ++t)
@@ -977,6 +1009,18 @@ void build_hybrid(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vec
                 if (!fine[q][k].rules.empty()) b += size_t(dir_form_bytes(double(fine[q][k].dir.size() - 1), f)) + 16;
         return b;
     };
+    // 4-bit-count directories (flat-LDS positional forms): 1.67x the buckets
+    // of the u8 form per LDS byte, so budget-bound slots get finer radixes
+    // (C5: the address slots' longer prefixes collide in fewer buckets) at
+    // a few more VALU per lookup; taken when the expected candidates drop
+    if (flat && lds_dirs && fmt == 8 && opt.dir4 && !opt.coarse) {
+        const double e8 = size_and_fill(all, weight, budget, 8);
+        const double e4 = size_and_fill(all, weight, budget, 4);
+        bool ok = e4 < 0.97 * e8;
+        for (int i = 0; ok && i < 8; ++i) ok = dir_fits(all[i]->dir, 4);
+        if (ok) fmt = 4;
+        else size_and_fill(all, weight, budget, fmt);
+    }
     // the plan before any rule moved to a grid: restored if the directories
     // ever degrade to the plain form, where the grids would not fit the budget
     FamilyPlan plan_1d[2];
@@ -1022,12 +1066,18 @@ void build_hybrid(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vec
                 // directory would outgrow the bytes taken off the budget.
                 // Left with fewer than fine_min rules, it is not built.
                 for (int it = 0; it < 8 && !dir_fits(g[k].dir, fmt); ++it) {
-                    const uint32_t gs = fmt == 8 ? kDir8GroupShift : kDir16GroupShift;
+                    // (4-bit counts: the overflowing buckets themselves, gs 0)
+                    const uint32_t gs = fmt == 4 ? 0u : fmt == 8 ? kDir8GroupShift : kDir16GroupShift;
                     const uint32_t lim = fmt == 8 ? 0xFFu : 0xFFFFu;
                     const std::vector<uint32_t> &dir = g[k].dir;
                     std::vector<char> hot((dir.size() >> gs) + 1, 0);
-                    for (size_t t = 0; t < dir.size(); ++t)
-                        if (dir[t] - dir[(t >> gs) << gs] > lim) hot[t >> gs] = 1;
+                    for (size_t t = 0; t < dir.size(); ++t) {
+                        if (fmt == 4) {
+                            if (t + 1 < dir.size() && dir[t + 1] - dir[t] > 15u) hot[t] = 1;
+                        } else if (dir[t] - dir[(t >> gs) << gs] > lim) {
+                            hot[t >> gs] = 1;
+                        }
+                    }
                     std::vector<uint32_t> keep;
                     for (uint32_t r : g[k].rules) {
                         uint64_t l1, h1, l2, h2;
@@ -1058,6 +1108,49 @@ void build_hybrid(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vec
                 fd.ents = g[k].ents;
                 fd.max_list = g[k].max_list;
                 fine_bytes += size_t(dir_form_bytes(double(g[k].n_buckets()), fmt)) + 16;
+                any_fine = true;
+            }
+            // Coarse address grids (slots 6 / 7 when no fine grid uses them):
+            // a dst / src rule whose prefix spans >= 2^cgrid buckets of its
+            // 1-D slot is replicated that many times; in a grid on the same
+            // address with radix rb - cgrid (no port bits) it is a candidate
+            // for exactly the same packets with 2^cgrid times fewer copies.
+            for (int c = 0; opt.cgrid > 0 && c < 2; ++c) {
+                const int k = 2 + c;  // positional slot 6 (dst) / 7 (src)
+                if (((allowed >> k) & 1u) || !fine[f][k].rules.empty()) continue;
+                const DimBuild &db = pl.dims[c];
+                if (db.rb < uint32_t(opt.cgrid) + 6u) continue;
+                const uint32_t wide = 1u << opt.cgrid;
+                std::vector<uint32_t> mv;
+                for (size_t i = 0; i < db.rules.size(); ++i) {
+                    const uint32_t r = db.rules[i];
+                    if (!gone[r] && (db.ranges[i].hi >> db.shift) - (db.ranges[i].lo >> db.shift) + 1 >= wide)
+                        mv.push_back(r);
+                }
+                if (mv.size() < size_t(opt.fine_min)) continue;
+                std::sort(mv.begin(), mv.end());
+                GSlot gc;
+                gc.f1 = c == 0 ? kFDst : kFSrc;
+                gc.b1 = db.rb - uint32_t(opt.cgrid);
+                gc.f2 = kFSport;
+                gc.b2 = 0;
+                gc.rules = mv;
+                gc.fill(pl.rr);
+                if (!dir_fits(gc.dir, fmt)) continue;
+                for (uint32_t r : mv) gone[r] = 1;
+                DimBuild &fd = fine[f][k];
+                fd.kind = field_kind(gc.f1, f == 1);
+                fd.key_bits = 32;
+                fd.rb = gc.b1;
+                fd.shift = 32 - gc.b1;
+                fd.kind2 = field_kind(gc.f2, f == 1);
+                fd.bits2 = 0;
+                fd.shift2 = 16;
+                fd.rules = gc.rules;
+                fd.dir = gc.dir;
+                fd.ents = gc.ents;
+                fd.max_list = gc.max_list;
+                fine_bytes += size_t(dir_form_bytes(double(gc.n_buckets()), fmt)) + 16;
                 any_fine = true;
             }
             for (int d = 0; d < 4; ++d) {  // the moved rules leave their 1-D slots
@@ -1142,7 +1235,7 @@ void build_hybrid(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vec
         return true;
     };
     while (!form_fits(fmt) || !fine_fits(fmt)) {
-        fmt = fmt == 8 && want16 ? 16 : 0;
+        fmt = fmt == 4 ? 8 : fmt == 8 && want16 ? 16 : 0;
         if (any_fine && fmt == 0) {  // plain directories: no room for the grids, their rules go back
             plan[0] = plan_1d[0];
             plan[1] = plan_1d[1];
@@ -1155,7 +1248,7 @@ void build_hybrid(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vec
         size_and_fill(ext.data(), wext.data(), budget > fb ? budget - fb : 1024, fmt, nd);
     }
     const bool dir16 = fmt != 0;
-    out.dir8 = fmt == 8 ? 1u : 0u;
+    out.dir8 = fmt == 8 ? 1u : fmt == 4 ? 2u : 0u;
     // slot order per family: positional [dst, src, dport, sport] (empty ones
     // included), or compacted (non-empty slots only, coarse ones last)
     std::vector<DimBuild *> order[2];
@@ -1202,12 +1295,25 @@ void build_hybrid(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vec
                 continue;
             }
             const size_t nb = dir.size() - 1;
-            const uint32_t gs = out.dir8 ? kDir8GroupShift : kDir16GroupShift;
+            const uint32_t gs = out.dir8 == 2 ? kDir4GroupShift : out.dir8 ? kDir8GroupShift : kDir16GroupShift;
             const size_t groups = (nb >> gs) + 2;  // base[g + 1] stays readable
             for (size_t g = 0; g < groups; ++g) blob.push_back(dir[std::min(g << gs, nb)]);
             dir_words[f][k] = static_cast<uint32_t>(groups);
+            if (out.dir8 == 2 && blob.size() % 2) blob.push_back(0);  // counts: 8-byte aligned dword pairs
             di.off_dir16 = static_cast<uint32_t>(blob.size());
             di.dir8 = out.dir8;
+            if (out.dir8 == 2) {  // 4-bit counts, 8 per dword; group g = dwords 2g, 2g + 1
+                const size_t words = 2 * ((nb >> kDir4GroupShift) + 2);
+                for (size_t w = 0; w < words; ++w) {
+                    uint32_t x = 0;
+                    for (size_t i = 0; i < 8; ++i) {
+                        const size_t t = 8 * w + i;
+                        if (t < nb) x |= (dir[t + 1] - dir[t]) << (4 * i);
+                    }
+                    blob.push_back(x);
+                }
+                continue;
+            }
             auto rel = [&](size_t t) -> uint32_t { return t <= nb ? dir[t] - dir[(t >> gs) << gs] : 0u; };
             if (out.dir8) {
                 const size_t words = (nb + 4) / 4 + 1;  // dword (t >> 2) + 1 stays readable
@@ -1322,6 +1428,8 @@ bool CompileOptions::from_env(CompileOptions &o, std::string &err) {
     if (set) o.dir_bytes = size_t(v) * 1024;
     if (!env_knob("NFFACL_TUNE_DIR16", 0, 1, v, set, err)) return false;
     if (set) o.dir16 = v != 0;
+    if (!env_knob("NFFACL_TUNE_DIR4", 0, 1, v, set, err)) return false;
+    if (set) o.dir4 = v != 0;
     if (!env_knob("NFFACL_TUNE_DIR8", 0, 1, v, set, err)) return false;
     if (set) o.dir8 = v != 0;
     if (!env_knob("NFFACL_TUNE_COARSE", 0, 1, v, set, err)) return false;
@@ -1344,6 +1452,10 @@ bool CompileOptions::from_env(CompileOptions &o, std::string &err) {
     if (set) o.fine_slots = static_cast<int>(v);
     if (!env_knob("NFFACL_TUNE_DIR_PER_RULE", 1, 64, v, set, err)) return false;
     if (set) o.dir_per_rule = static_cast<int>(v);
+    if (!env_knob("NFFACL_TUNE_CGRID", 0, 12, v, set, err)) return false;
+    if (set) o.cgrid = static_cast<int>(v);
+    if (!env_knob("NFFACL_TUNE_DIR_SB", 0, 100, v, set, err)) return false;
+    if (set) o.dir_sbias = static_cast<int>(v);
     return true;
 }
 
@@ -1356,6 +1468,7 @@ bool compile_table(const nffacl_rules &rules, int algo, const CompileOptions &op
     }
     out = CompiledTable{};
     g_dir_per_rule = static_cast<size_t>(opt.dir_per_rule);
+    g_dir_sbias = double(opt.dir_sbias) / 100.0;
     std::vector<uint32_t> rec4, rec6;
     rec4.reserve(rules.ip4.size() * kRec4Dwords);
     rec6.reserve(rules.ip6.size() * kRec6Dwords);

@@ -23,7 +23,8 @@ struct DimInfo {
                              // 2-level directory's group bases base[n_buckets / 64 + 2])
     uint32_t off_dir16 = 0;  // 0, or dword offset of the u16 offsets dir16[n_buckets + 1]:
                              // dir[t] = base[t >> 6] + dir16[t]
-    uint32_t dir8 = 0;       // 1: off_dir16 holds u8 offsets instead, dir[t] = base[t >> 4] + dir8[t]
+    uint32_t dir8 = 0;       // 1: off_dir16 holds u8 offsets instead, dir[t] = base[t >> 4] + dir8[t];
+                             // 2: 4-bit bucket counts, dir[t] = base[t >> 4] + sum(cnt[16 (t >> 4) .. t - 1])
     uint32_t off_ent = 0;    // dword offset of the bucket entries (inline rule entries)
     uint32_t n_rules = 0;    // rules assigned to this dimension
     uint64_t n_ent = 0;      // bucket entries (with replication)
@@ -82,6 +83,8 @@ struct CompileOptions {
     double slot_cost = 0.1; // NFFACL_TUNE_SLOT_COST (1/100): expected candidates per packet a slot must save
     bool dir16 = true;      // NFFACL_TUNE_DIR16: two-level u16 LDS directories allowed
     bool dir8 = true;       // NFFACL_TUNE_DIR8: two-level u8 LDS directories allowed (HYBRID)
+    bool dir4 = true;       // NFFACL_TUNE_DIR4: two-level 4-bit-count LDS directories allowed (flat-LDS
+                            // positional forms, when they buy finer radixes: table.hpp kDir4GroupShift)
     int uncond = -1;        // NFFACL_TUNE_UNCOND: flat-LDS branch-free entry loads (-1 = policy)
     // NFFACL_TUNE_FINE_A / _P: fine 2-D address x port slots of the flat-LDS
     // form (positional slots 4..7), a address bits x p port bits; a = 0: none
@@ -90,6 +93,11 @@ struct CompileOptions {
     double fine_gain = 0.5;  // NFFACL_TUNE_FINE_G (1/100): a rule moves below this fraction of its 1-D cover
     int fine_min = 256;      // NFFACL_TUNE_FINE_MIN: fewest moved rules worth a fine slot
     int fine_slots = 3;      // NFFACL_TUNE_FINE_SLOTS: bit k allows fine slot 4 + k (3: dst x dport, src x dport)
+    int cgrid = 0;           // NFFACL_TUNE_CGRID: coarse address grids on free positional slots 6 / 7: the
+                             // dst / src slot's rules replicated into >= 2^cgrid buckets move to a grid of
+                             // radix rb - cgrid (same candidates, far fewer copies: a smaller, L2-resident table)
+    int dir_sbias = 0;       // NFFACL_TUNE_DIR_SB (percent): weight of the size-biased list length (the lists
+                             // traffic that matches rules lands in) beside the uniform-key mean in the radix sizing
     int dir_per_rule = 16;   // NFFACL_TUNE_DIR_PER_RULE: LDS directory buckets per rule before the budget cut
                              // (C3 0.4005 vs 0.4122 ms at 4: profiles/r4_ab/fine/ab_c3_dir_per_rule.json)
     bool coarse = false;    // NFFACL_TUNE_COARSE: flat-LDS coarse address slots for short prefixes

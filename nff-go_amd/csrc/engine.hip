@@ -82,8 +82,15 @@ k_linear_frames(const uint8_t *__restrict__ frames, const uint64_t *__restrict__
 }
 
 
-template <int NS, int TM>
-__device__ __forceinline__ uint32_t classify_any(const IndexedArgs &a, const Fields &f) {
+// `pf`: the next batch's packet loads (load mode 6); the pipelined walk
+// issues them itself, after its first window's tests; other walks up front.
+template <int NS, int TM, class PF>
+__device__ __forceinline__ uint32_t classify_any(const IndexedArgs &a, const Fields &f, PF &&pf) {
+    if constexpr (TM == kTabFlatLdsP) {
+        FlatScratch<4> *W = reinterpret_cast<FlatScratch<4> *>(lds_tab + a.stage_dwords);
+        return classify_flat_pipe<NS>(a, f, W[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)], lane_id(), pf);
+    }
+    pf();
     if (TM == kTabFlat || TM == kTabFlat4) {
         constexpr int R = TM == kTabFlat4 ? 4 : 2;
         FlatScratch<R> *W = reinterpret_cast<FlatScratch<R> *>(lds_tab);
@@ -123,8 +130,9 @@ k_indexed_slots(const uint8_t *__restrict__ slots, uint32_t stride, uint64_t n, 
     const uint32_t wpb = blockDim.x >> 6;
     const uint64_t wave0 = uint64_t(blockIdx.x) * wpb + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t step = uint64_t(gridDim.x) * wpb * 64;
-    constexpr bool RS = MODE == 4 || MODE == 5;  // lane-contiguous loads + permlane row swaps
+    constexpr bool RS = MODE == 4 || MODE == 5 || MODE == 6;  // lane-contiguous loads + permlane row swaps
     constexpr bool RSPF = MODE == 5;             // RS + the next batch's loads in flight (16 VGPRs)
+    constexpr bool RSIN = MODE == 6;             // RS + the next batch's loads issued by the walk (pf below)
     constexpr bool COAL = MODE != 0 && !RS;      // lane-contiguous loads + quad DPP transpose
     constexpr bool NT = MODE >= 2;
     constexpr bool PF = MODE == 3;  // coalesced + next-batch register prefetch
@@ -134,7 +142,7 @@ k_indexed_slots(const uint8_t *__restrict__ slots, uint32_t stride, uint64_t n, 
     u32x4 nv[4];
     if (!COAL && !RS && base < n) load16(slots + (base + lane < n ? base + lane : 0) * stride, d);
     if (PF && base + 64 <= n) load_coal<NT>(slots + base * 64, lane, nv);
-    if (RSPF && base + 64 <= n) load_rowswap<NT>(slots + base * 64, lane, nv);
+    if ((RSPF || RSIN) && base + 64 <= n) load_rowswap<NT>(slots + base * 64, lane, nv);
     for (; base < n; base += step) {
         const uint64_t idx = base + mine;
         const bool live = idx < n;
@@ -143,15 +151,19 @@ k_indexed_slots(const uint8_t *__restrict__ slots, uint32_t stride, uint64_t n, 
         if (RS) {
             if (base + 64 <= n) {
                 u32x4 cv[4];
-                if (RSPF) {
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) cv[j] = nv[j];
-                    const uint64_t nb = base + step;
-                    if (nb + 64 <= n) load_rowswap<NT>(slots + nb * 64, lane, nv);
+                if (RSIN) {  // this batch's loads were issued during the previous batch
+                    rowswap_batch(nv, cur);
                 } else {
-                    load_rowswap<NT>(slots + base * 64, lane, cv);
+                    if (RSPF) {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) cv[j] = nv[j];
+                        const uint64_t nb = base + step;
+                        if (nb + 64 <= n) load_rowswap<NT>(slots + nb * 64, lane, nv);
+                    } else {
+                        load_rowswap<NT>(slots + base * 64, lane, cv);
+                    }
+                    rowswap_batch(cv, cur);
                 }
-                rowswap_batch(cv, cur);
             } else {
                 load16(pkt, cur);
             }
@@ -182,11 +194,17 @@ k_indexed_slots(const uint8_t *__restrict__ slots, uint32_t stride, uint64_t n, 
         // it is VALU-bound, the select chain cost it 2.6 % (round 1), and
         // taking every option port from registers (no far read at all at
         // stride 64) 9 % (round 3, profiles/r3_ab/regports/)
-        constexpr bool REG = TM == kTabFlatLds || TM == kTabFlatLds4 || TM == kTabFlatLds4U || TM == kTabFlatLdsG;
+        constexpr bool REG = TM == kTabFlatLds || TM == kTabFlatLds4 || TM == kTabFlatLds4U || TM == kTabFlatLdsG ||
+                             TM == kTabFlatLdsP;
         parse_fields<REG, TM == kTabLdsNP>(cur, live, f, [&](uint32_t k, uint32_t &lo, uint32_t &hi) {
             far_dwords(pkt, stride, k, lo, hi);
         }, a.flags);
-        const uint32_t res = classify_any<NS, TM>(a, f);
+        const uint32_t res = classify_any<NS, TM>(a, f, [&] {
+            if (RSIN) {
+                const uint64_t nb = base + step;
+                if (nb + 64 <= n) load_rowswap<NT>(slots + nb * 64, lane, nv);
+            }
+        });
         if (live && port_out) port_out[idx] = res;
         if (permit_out) {
             // permit bit p belongs to packet p: fetch packet `lane`'s verdict from the lane holding it
@@ -229,7 +247,7 @@ k_indexed_frames(const uint8_t *__restrict__ frames, const uint64_t *__restrict_
         parse_fields<true, TM == kTabLdsNP>(d, live, f, [&](uint32_t k, uint32_t &lo, uint32_t &hi) {
             far_dwords(pkt, len, k, lo, hi);
         }, a.flags);
-        const uint32_t res = classify_any<NS, TM>(a, f);
+        const uint32_t res = classify_any<NS, TM>(a, f, [] {});
         store_verdicts(b, lane, live, res, port_out, permit_out);
     };
     // Software pipeline.  Always: the next batch's descriptors load while this
@@ -298,7 +316,7 @@ bool Tune::from_env(Tune &t, std::string &err) {
     t = Tune{};
     long v = 0;
     bool set = false;
-    if (!env_knob("NFFACL_TUNE_COAL", 0, 5, v, set, err)) return false;
+    if (!env_knob("NFFACL_TUNE_COAL", 0, 6, v, set, err)) return false;
     if (set) t.coal = static_cast<int>(v);
     t.coal_set = set;
     if (!env_knob("NFFACL_TUNE_BLOCK", 64, 1024, v, set, err)) return false;
@@ -317,6 +335,8 @@ bool Tune::from_env(Tune &t, std::string &err) {
     if (set) t.rounds = static_cast<int>(v);
     if (!env_knob("NFFACL_TUNE_LDS", 0, 1, v, set, err)) return false;
     if (set) t.lds = static_cast<int>(v);
+    if (!env_knob("NFFACL_TUNE_PIPE", 0, 1, v, set, err)) return false;
+    if (set) t.pipe = static_cast<int>(v);
     if (!env_knob("NFFACL_TUNE_HOST_DMA", 0, 1, v, set, err)) return false;
     if (set) t.host_dma = static_cast<int>(v);
     if (!env_knob("NFFACL_TUNE_HOST_BUFS", 2, nffacl_engine::kHostBufs, v, set, err)) return false;
@@ -369,7 +389,8 @@ static SvcDesc service_desc(const CompiledTable &m) {
 // Tables uploaded so far (DevTable::gen of the latest).
 static std::atomic<uint32_t> g_table_epoch{0};
 
-int compile_upload(const nffacl_rules &rules, int algo, const CompileOptions &copt, TableHome &home, DevTable &t) {
+int compile_words(const nffacl_rules &rules, int algo, const CompileOptions &copt, DevTable &t,
+                  std::vector<uint32_t> &words) {
     std::string err;
     if (!compile_table(rules, algo, copt, t.meta, err)) {
         set_last_error("compile: " + err);
@@ -377,19 +398,30 @@ int compile_upload(const nffacl_rules &rules, int algo, const CompileOptions &co
     }
     const SvcDesc d = service_desc(t.meta);
     t.svc_kind = d.kind;
-    std::vector<uint32_t> words(t.meta.blob);
+    words = t.meta.blob;
     words.resize(words.size() + kSvcDescDwords);
     std::memcpy(words.data() + t.meta.blob.size(), &d, sizeof d);
-    const hipError_t e = t.upload(&home, words.data(), words.size());
-    if (e != hipSuccess) {
-        set_last_error(std::string("table upload: ") + hipGetErrorString(e));
-        return e == hipErrorOutOfMemory ? NFFACL_ERR_NOMEM : NFFACL_ERR_HIP;
-    }
+    return NFFACL_OK;
+}
+
+void table_resident(DevTable &t) {
     t.bytes = t.meta.blob.size() * sizeof(uint32_t);  // reported size: the table itself
     t.d_desc = t.d_blob + t.meta.blob.size();
     // the generation is drawn after the upload has completed (service.hip:
     // a consumer launched after the counter passed it sees the table)
     t.gen = g_table_epoch.fetch_add(1, std::memory_order_seq_cst) + 1;
+}
+
+int compile_upload(const nffacl_rules &rules, int algo, const CompileOptions &copt, TableHome &home, DevTable &t) {
+    std::vector<uint32_t> words;
+    const int st = compile_words(rules, algo, copt, t, words);
+    if (st != NFFACL_OK) return st;
+    const hipError_t e = t.upload(&home, words.data(), words.size());
+    if (e != hipSuccess) {
+        set_last_error(std::string("table upload: ") + hipGetErrorString(e));
+        return e == hipErrorOutOfMemory ? NFFACL_ERR_NOMEM : NFFACL_ERR_HIP;
+    }
+    table_resident(t);
     return NFFACL_OK;
 }
 
@@ -428,6 +460,7 @@ static dev::IndexedArgs indexed_args(const DevTable *t) {
     const bool hyb = t->meta.algo == NFFACL_ALGO_HYBRID;
     a.stage_dwords = hyb ? t->meta.lds_dwords : static_cast<uint32_t>(t->meta.blob.size());
     a.dir8 = hyb ? t->meta.dir8 : 0u;
+    a.dir16 = hyb && (t->meta.idx4.dims[0].off_dir16 | t->meta.idx6.dims[0].off_dir16) != 0 ? 1u : 0u;
     a.generic = t->meta.slots_g ? 1u : 0u;
     auto fam = [&](const FamilyIndex &fi, uint32_t off_cold, dev::FamArgs &fa) {
         for (uint32_t k = 0; k < kMaxSlots; ++k) {
@@ -518,6 +551,10 @@ static IndexedLaunch indexed_launch(const nffacl_engine *eng, const DevTable *t)
         if (t->meta.slots_g) {  // generalized slots: the generic kernel, always 4 rounds (its scratch)
             L.tm = dev::kTabFlatLdsG;
             L.lds_bytes = lds4;  // > kLdsBytes is refused by the launch check below
+        } else if (tu.pipe && t->meta.flat_uncond && lds4 <= kLdsBytes && !tu.rounds) {
+            // the pipelined walk (its scratch: FlatScratch<4>)
+            L.tm = dev::kTabFlatLdsP;
+            L.lds_bytes = lds4;
         }
         // (round 4: 2 workgroups per CU — one resident at a time, so that one
         // that starts late on a CU held by a resident consumer takes a
@@ -569,8 +606,11 @@ template <int NS, int TM>
 static hipError_t allow_lds_modes() {
     hipError_t e = allow_lds(dev::k_indexed_slots<NS, TM, 0>);
     if (e == hipSuccess) e = allow_lds(dev::k_indexed_slots<NS, TM, 4>);
-    if (TM == dev::kTabFlatLds || TM == dev::kTabFlatLds4 || TM == dev::kTabFlatLds4U || TM == dev::kTabFlatLdsG)
+    if (TM == dev::kTabFlatLds || TM == dev::kTabFlatLds4 || TM == dev::kTabFlatLds4U || TM == dev::kTabFlatLdsG ||
+        TM == dev::kTabFlatLdsP)
         if (e == hipSuccess) e = allow_lds(dev::k_indexed_slots<NS, TM, 5>);
+    if constexpr (TM == dev::kTabFlatLdsP)
+        if (e == hipSuccess) e = allow_lds(dev::k_indexed_slots<NS, TM, 6>);
     if (TM == dev::kTabLds) {
         if (e == hipSuccess) e = allow_lds(dev::k_indexed_slots<NS, dev::kTabLds, 1>);
         if (e == hipSuccess) e = allow_lds(dev::k_indexed_slots<NS, dev::kTabLds, 2>);
@@ -583,6 +623,11 @@ static hipError_t allow_lds_modes() {
 // Calls f(integral_constant<NS>, integral_constant<TM>) for the runtime pair.
 template <class F>
 static void dispatch_indexed(int ns, int tm, F &&f) {
+#ifdef NFFACL_PROBE_NS  // register / ISA probe builds only (make probe): one slot count, two flat walks
+    (void)ns;
+    if (tm == dev::kTabFlatLdsP) f(std::integral_constant<int, NFFACL_PROBE_NS>{}, std::integral_constant<int, dev::kTabFlatLdsP>{});
+    else f(std::integral_constant<int, NFFACL_PROBE_NS>{}, std::integral_constant<int, dev::kTabFlatLds4U>{});
+#else
     auto with_ns = [&](auto nsc) {
         switch (tm) {
         case dev::kTabLds: f(nsc, std::integral_constant<int, dev::kTabLds>{}); break;
@@ -594,6 +639,7 @@ static void dispatch_indexed(int ns, int tm, F &&f) {
         case dev::kTabFlatLds4: f(nsc, std::integral_constant<int, dev::kTabFlatLds4>{}); break;
         case dev::kTabFlatLds4U: f(nsc, std::integral_constant<int, dev::kTabFlatLds4U>{}); break;
         case dev::kTabFlatLdsG: f(nsc, std::integral_constant<int, dev::kTabFlatLdsG>{}); break;
+        case dev::kTabFlatLdsP: f(nsc, std::integral_constant<int, dev::kTabFlatLdsP>{}); break;
         default: f(nsc, std::integral_constant<int, dev::kTabGlobal>{}); break;
         }
     };
@@ -605,6 +651,7 @@ static void dispatch_indexed(int ns, int tm, F &&f) {
         case dev::kTabFlatLds4: f(nsc, std::integral_constant<int, dev::kTabFlatLds4>{}); break;
         case dev::kTabFlatLds4U: f(nsc, std::integral_constant<int, dev::kTabFlatLds4U>{}); break;
         case dev::kTabFlatLdsG: f(nsc, std::integral_constant<int, dev::kTabFlatLdsG>{}); break;
+        case dev::kTabFlatLdsP: f(nsc, std::integral_constant<int, dev::kTabFlatLdsP>{}); break;
         default: f(nsc, std::integral_constant<int, dev::kTabFlat4>{}); break;
         }
     };
@@ -615,6 +662,7 @@ static void dispatch_indexed(int ns, int tm, F &&f) {
     else if (ns == 6) with_ns_flat(std::integral_constant<int, 6>{});
     else if (ns == 7) with_ns_flat(std::integral_constant<int, 7>{});
     else with_ns_flat(std::integral_constant<int, 8>{});
+#endif
 }
 
 int prepare_kernels() {
@@ -623,9 +671,9 @@ int prepare_kernels() {
     std::call_once(once, [] {
         for (int ns = 2; ns <= int(kMaxSlots); ++ns)
             for (int tm : {int(dev::kTabLds), int(dev::kTabLdsNP), int(dev::kTabSplit), int(dev::kTabFlatLds), int(dev::kTabFlatLds4),
-                           int(dev::kTabFlatLds4U), int(dev::kTabFlatLdsG)}) {
+                           int(dev::kTabFlatLds4U), int(dev::kTabFlatLdsG), int(dev::kTabFlatLdsP)}) {
                 if (ns > 4 && tm != dev::kTabFlatLds && tm != dev::kTabFlatLds4 && tm != dev::kTabFlatLds4U &&
-                    tm != dev::kTabFlatLdsG)
+                    tm != dev::kTabFlatLdsG && tm != dev::kTabFlatLdsP)
                     continue;  // flat walks only
                 dispatch_indexed(ns, tm, [&](auto nsc, auto tmc) {
                     const hipError_t e = allow_lds_modes<decltype(nsc)::value, decltype(tmc)::value>();
@@ -647,7 +695,13 @@ static void launch_slots_tm(int mode, const IndexedLaunch &L, uint32_t grid, hip
     const dim3 g(grid), b(L.block);
     const size_t lds = TM == dev::kTabGlobal ? 0 : L.lds_bytes;
     if constexpr (TM == dev::kTabFlatLds || TM == dev::kTabFlatLds4 || TM == dev::kTabFlatLds4U ||
-                  TM == dev::kTabFlatLdsG) {  // load modes 0, 4, 5
+                  TM == dev::kTabFlatLdsG || TM == dev::kTabFlatLdsP) {  // load modes 0, 4, 5
+        if constexpr (TM == dev::kTabFlatLdsP) {  // mode 6: the walk issues the next batch's loads
+            if (mode == 6) {
+                hipLaunchKernelGGL((dev::k_indexed_slots<NS, TM, 6>), g, b, lds, stream, d_slots, stride, n, a, d_port, d_permit);
+                return;
+            }
+        }
         if (mode == 0)
             hipLaunchKernelGGL((dev::k_indexed_slots<NS, TM, 0>), g, b, lds, stream, d_slots, stride, n, a, d_port, d_permit);
         else if (mode == 5)
@@ -702,7 +756,11 @@ int launch_slots(nffacl_engine *eng, DevTable *t, const uint8_t *d_slots, uint32
         // batch's packets in flight: 0.6278 / 0.6312 vs 0.6340 / 0.6328 ms
         // (profiles/r3_ab/c5_mode5/); everything else to mode 4
         int mode = stride == 64 ? eng->tune.coal : 0;
-        if (stride == 64 && !eng->tune.coal_set && (L.tm == dev::kTabFlatLds4U || L.tm == dev::kTabFlatLdsG)) mode = 5;
+        if (stride == 64 && !eng->tune.coal_set && (L.tm == dev::kTabFlatLds4U || L.tm == dev::kTabFlatLdsG))
+            mode = 5;
+        // (the pipelined walk: load mode 4 — mode 6, the next batch's loads
+        // issued from inside the walk, spilled and ran 0.64 vs 0.53 ms on C5:
+        // NFFACL_TUNE_COAL=6, profiles/r5_ab/)
         dispatch_indexed(L.ns, L.tm, [&](auto nsc, auto tmc) {
             launch_slots_tm<decltype(nsc)::value, decltype(tmc)::value>(mode, L, grid, stream, d_slots, stride, n, a,
                                                                       d_port, d_permit);

@@ -8,6 +8,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "compile.hpp"
 #include "tables.hpp"
@@ -37,6 +38,7 @@ struct Tune {
     int per_cu = 0;  // NFFACL_TUNE_PER_CU: workgroups per CU (0 = kernel default)
     int rounds = 0;  // NFFACL_TUNE_ROUNDS: flat walks, loads in flight (0 = compiled, 2 or 4)
     int lds = 1;     // NFFACL_TUNE_LDS: 0 keeps INDEXED tables in global memory
+    int pipe = 1;    // NFFACL_TUNE_PIPE: flat-LDS positional tables take the pipelined walk (classify_flat_pipe)
     // nffacl_classify_host (capi.cpp): pinned input read by the kernel over
     // PCIe (0) or DMA'd to HBM first (1); buffers = streams in flight (2..4);
     // packets per chunk, log2
@@ -55,6 +57,12 @@ int engine_shell(int hip_device, nffacl_engine **out);
 // Compile `rules` with `algo` / `copt`, upload blob + service descriptor
 // through `home` (whose device is current), fill `t`.
 int compile_upload(const nffacl_rules &rules, int algo, const CompileOptions &copt, TableHome &home, DevTable &t);
+// The device image of a compiled table (blob + service descriptor) in
+// `words`, its metadata in `t`; table_resident() completes `t` once its
+// d_blob holds the words (the group's RCCL broadcast, group.cpp).
+int compile_words(const nffacl_rules &rules, int algo, const CompileOptions &copt, DevTable &t,
+                  std::vector<uint32_t> &words);
+void table_resident(DevTable &t);
 // Generation of the latest completed table upload.
 uint32_t table_epoch();
 

@@ -108,7 +108,7 @@ struct CheckedTab {
         return 0u;
     }
     __device__ __forceinline__ void bounds(uint32_t dir, uint32_t, uint32_t t, uint32_t &lo, uint32_t &hi,
-                                           bool = false) const {
+                                           uint32_t = 0) const {
         lo = ld(dir + t);
         hi = ld(dir + t + 1);
     }
@@ -960,15 +960,7 @@ hipError_t host_alloc_on_node(void **p, size_t bytes, unsigned flags, int node) 
 
 extern "C" {
 
-int nffacl_local_device(void) {
-    const DeviceNodes &dn = device_nodes();
-    if (dn.count <= 0) return NFFACL_ERR_NO_DEVICE;
-    unsigned cpu = 0, node = 0;
-    if (getcpu(&cpu, &node) != 0) return 0;
-    for (int d = 0; d < dn.count; ++d)
-        if (dn.node[d] == static_cast<int>(node)) return d;
-    return 0;
-}
+// nffacl_local_device: group.cpp (it spreads a node's callers over the node's devices)
 
 int nffacl_device_numa_node(int hip_device) {
     const DeviceNodes &dn = device_nodes();

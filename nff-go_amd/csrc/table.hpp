@@ -125,6 +125,13 @@ constexpr uint32_t kDir16GroupShift = 6;
 // the u16 form in the same LDS) when every group's lists hold <= 255 entries;
 // else the u16 form, else plain u32.  C5: 11.0 -> ~8.5 candidates per packet.
 constexpr uint32_t kDir8GroupShift = 4;
+// 4-bit form (round 5): one u32 base per group of 16 buckets + a 4-bit count
+// per bucket (0.75 B per bucket: 1.67x the buckets of the u8 form in the
+// same LDS).  dir[t] = base[t >> 4] + the counts of the group's buckets
+// before t, dir[t + 1] = dir[t] + cnt[t]; the counts of group g are the
+// dword pair 2g, 2g + 1 of the count array (8-byte aligned), low nibble
+// first.  Every bucket list must hold <= 15 entries.
+constexpr uint32_t kDir4GroupShift = 4;
 // Largest table staged whole in LDS (gfx950: 160 KiB per CU, 1 KiB headroom).
 constexpr size_t kLdsTableBytes = 159 * 1024;
 

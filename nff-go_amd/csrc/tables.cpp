@@ -92,6 +92,14 @@ hipError_t DeviceBlob::note_use(hipStream_t s) {
 }
 
 hipError_t DeviceBlob::upload(TableHome *h, const uint32_t *words, size_t n_words) {
+    hipError_t e = alloc(h, n_words);
+    if (e != hipSuccess) return e;
+    e = hipMemcpyAsync(d_blob, words, bytes, hipMemcpyHostToDevice, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    return e;
+}
+
+hipError_t DeviceBlob::alloc(TableHome *h, size_t n_words) {
     home = h;
     bytes = n_words * sizeof(uint32_t);
     void *p = nullptr;
@@ -104,9 +112,7 @@ hipError_t DeviceBlob::upload(TableHome *h, const uint32_t *words, size_t n_word
     }
     if (e != hipSuccess) return e;
     d_blob = static_cast<uint32_t *>(p);
-    e = hipMemcpyAsync(d_blob, words, bytes, hipMemcpyHostToDevice, h->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
-    return e;
+    return hipSuccess;
 }
 
 DeviceBlob::~DeviceBlob() {

@@ -63,6 +63,8 @@ struct DeviceBlob {
     // Allocate + upload `words` on home->stream (synchronous w.r.t. that
     // stream only); the blob is usable by any stream when this returns.
     hipError_t upload(TableHome *h, const uint32_t *words, size_t n_words);
+    // Allocate only (the words arrive by other means: group.cpp's broadcast).
+    hipError_t alloc(TableHome *h, size_t n_words);
 
     DeviceBlob() = default;
     DeviceBlob(const DeviceBlob &) = delete;

@@ -151,6 +151,11 @@ class ServiceStats(ctypes.Structure):
 
 _rules_prepare = _sig("nffacl_rules_prepare", _i, _vp, _i)
 _local_device = _sig("nffacl_local_device", _i)
+_pick_device = _sig("nffacl_pick_device", _i, _i, _vp, _i, _vp, _i)
+_group_create = _sig("nffacl_group_create", _i, _vp, _i, _vp, _pp)
+_group_size = _sig("nffacl_group_size", _i, _vp)
+_group_classify = _sig("nffacl_group_classify_device", _i, _vp, _vp, _u32, ctypes.c_uint64, _vp, _vp, _vp)
+_group_destroy = _sig("nffacl_group_destroy", None, _vp)
 _device_numa_node = _sig("nffacl_device_numa_node", _i, _i)
 _service_create = _sig("nffacl_service_create", _i, _i, _u32, _u32, _pp)
 _service_classify = _sig("nffacl_service_classify", _i, _vp, _vp, _vp, _u32, _u32, ctypes.POINTER(_u32))
@@ -184,7 +189,8 @@ EXPORTED_SYMBOLS = [
     "nffacl_batcher_wait_timeout", "nffacl_local_device", "nffacl_device_numa_node",
     "nffacl_rules_prepare", "nffacl_service_create", "nffacl_service_classify", "nffacl_service_get_stats",
     "nffacl_service_destroy", "nffacl_service_create_burst", "nffacl_service_classify_burst",
-    "nffacl_service_pause",
+    "nffacl_service_pause", "nffacl_pick_device", "nffacl_group_create", "nffacl_group_size",
+    "nffacl_group_classify_device", "nffacl_group_destroy",
 ]
 
 
@@ -193,8 +199,57 @@ def abi_version() -> int:
 
 
 def local_device() -> int:
-    """nffacl_local_device: the HIP device on the calling thread's NUMA node."""
+    """nffacl_local_device: the HIP device of the calling thread (its CPU's
+    rank on its NUMA node modulo the node's GPUs; stable per thread)."""
     return _local_device()
+
+
+def pick_device(cpu: int, cpu_node, dev_node) -> int:
+    """nffacl_pick_device: the device map behind local_device() on any
+    topology (cpu_node[c] / dev_node[d] = NUMA nodes, -1 unknown)."""
+    cn = np.ascontiguousarray(cpu_node, np.int32)
+    dn = np.ascontiguousarray(dev_node, np.int32)
+    return _pick_device(cpu, cn.ctypes.data if len(cn) else None, len(cn), dn.ctypes.data if len(dn) else None,
+                        len(dn))
+
+
+class Group:
+    """nffacl_group: one rule set on several GPUs of this process (RCCL
+    broadcast of the table; scatter of a root-resident batch, gather of the
+    verdicts).  The reference's clones-in-one-process deployment
+    (flow/scheduler.go:283-289) on a multi-GPU node."""
+
+    def __init__(self, devices, rules: L3Rules):
+        devs = np.ascontiguousarray(devices, np.int32)
+        h = ctypes.c_void_p()
+        st = _group_create(devs.ctypes.data if len(devs) else None, len(devs), rules.handle, ctypes.byref(h))
+        if st != OK:
+            _raise(st, "nffacl_group_create")
+        self._h = h
+
+    def size(self) -> int:
+        return _group_size(self._h)
+
+    def classify_device(self, d_slots, stride: int, n: int, port=None, permit=None, stream=None):
+        """Root-device tensors (torch) or raw device addresses."""
+        s = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
+        st = _group_classify(self._h, _ptr(d_slots), stride, n, _ptr(port), _ptr(permit), s)
+        if st != OK:
+            _raise(st, "nffacl_group_classify_device")
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _group_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
 
 
 def device_numa_node(device: int) -> int:

@@ -39,7 +39,8 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert nffacl.abi_version() == 5  # 3: generalized slots in nffacl_table_info; 5: burst service
+    # 3: generalized slots in nffacl_table_info; 5: burst service; 6: device groups, nffacl_pick_device
+    assert nffacl.abi_version() == 6
 
 
 def test_exports_are_c_linkage_only():
@@ -79,3 +80,45 @@ def test_device_numa_node(gpu_available):
     assert nffacl.device_numa_node(0) >= 0 or nffacl.device_numa_node(0) == nffacl.ERR_HIP
     assert nffacl.device_numa_node(-1) == nffacl.ERR_INVALID_ARG
     assert nffacl.device_numa_node(4096) == nffacl.ERR_INVALID_ARG
+
+
+def test_pick_device_spreads_a_node_over_its_gpus():
+    """a synthetic 2-socket host (256 CPUs, SMT
+    siblings numbered +128, node 0 = CPUs 0-63 and 128-191) with 8 GPUs, 4 on
+    each node: every node's clones spread evenly over that node's 4 GPUs, by
+    the CPU's rank among the node's CPUs (nffacl_local_device's map)."""
+    cpu_node = [0] * 64 + [1] * 64 + [0] * 64 + [1] * 64
+    dev_node = [0, 0, 0, 0, 1, 1, 1, 1]
+    got = [nffacl.pick_device(c, cpu_node, dev_node) for c in range(256)]
+    assert got[:8] == [0, 1, 2, 3, 0, 1, 2, 3]
+    assert got[64:72] == [4, 5, 6, 7, 4, 5, 6, 7]
+    assert got[128] == 0 and got[129] == 1 and got[192] == 4  # SMT siblings continue the node's rank
+    for node, devs in ((0, {0, 1, 2, 3}), (1, {4, 5, 6, 7})):
+        mine = [got[c] for c in range(256) if cpu_node[c] == node]
+        assert set(mine) == devs
+        counts = [mine.count(d) for d in sorted(devs)]
+        assert max(counts) - min(counts) <= 1  # even spread: 32 clones per GPU
+    # GPUs interleaved over the nodes (dev_node 0,1,0,1,...)
+    inter = [0, 1] * 4
+    assert [nffacl.pick_device(c, cpu_node, inter) for c in range(4)] == [0, 2, 4, 6]
+    assert [nffacl.pick_device(c, cpu_node, inter) for c in range(64, 68)] == [1, 3, 5, 7]
+    # no device on the CPU's node, or unknown nodes: every device, by CPU number
+    assert [nffacl.pick_device(c, cpu_node, [-1] * 8) for c in range(10)] == [c % 8 for c in range(10)]
+    assert nffacl.pick_device(3, [], [0, 0]) == 1  # unknown CPU map
+    assert nffacl.pick_device(0, cpu_node, []) < 0  # no devices: NFFACL_ERR_INVALID_ARG
+
+
+def test_group_without_device_reports_no_device():
+    """nffacl_group_create without a HIP device: NFFACL_ERR_NO_DEVICE (the
+    group itself runs in tests/test_group.py on the GPU); bad arguments are
+    rejected before any device is touched."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a HIP device is visible")
+    rules = nffacl.L3Rules.parse_text("ANY ANY TCP ANY 80 Accept\n")
+    with pytest.raises(nffacl.NFError) as e:
+        nffacl.Group([0], rules)
+    assert e.value.status == nffacl.ERR_NO_DEVICE
+    with pytest.raises(nffacl.NFError) as e:
+        nffacl.Group([], rules)
+    assert e.value.status == nffacl.ERR_INVALID_ARG

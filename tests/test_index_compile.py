@@ -110,6 +110,14 @@ def dir_values(blob, di):
     if di.off_dir16 == 0:
         return blob[di.off_dir:di.off_dir + nb + 1].astype(np.int64)
     t = np.arange(nb + 1)
+    if di.dir8 == 2:  # 4-bit counts per bucket, a base per 16 buckets (table.hpp kDir4GroupShift)
+        tb = np.arange(nb)
+        cnt = (blob[di.off_dir16 + (tb >> 3)].astype(np.int64) >> (4 * (tb & 7))) & 0xF
+        out = np.zeros(nb + 1, np.int64)
+        for g in range((nb + 15) // 16):
+            seg = cnt[16 * g:16 * g + 16]
+            out[16 * g:16 * g + len(seg) + 1] = int(blob[di.off_dir + g]) + np.concatenate([[0], np.cumsum(seg)])
+        return out
     if di.dir8:
         base = blob[di.off_dir + (t >> 4)].astype(np.int64)
         w = blob[di.off_dir16 + (t >> 2)].astype(np.int64)
@@ -421,7 +429,11 @@ def test_hybrid_policy_c5_flat(monkeypatch):
     info = check_hybrid(g.text, slots, n)
     assert 0 < info.lds_dwords * 4 <= 135 * 1024 and info.fam[0].entry_dwords == 6
     assert info.fam[0].dims[3].n_rules == 0  # sparse source-port slot folded away
+    assert info.fam[0].dims[0].dir8 == 2  # 4-bit-count two-level directories (round 5)
+    monkeypatch.setenv("NFFACL_TUNE_DIR4", "0")
+    info = check_hybrid(g.text, slots, n)
     assert info.fam[0].dims[0].dir8 == 1  # u8 two-level directories
+    monkeypatch.delenv("NFFACL_TUNE_DIR4")
     monkeypatch.setenv("NFFACL_TUNE_FLAT", "1")
     info = check_hybrid(g.text, slots, n)
     assert info.lds_dwords == 0 and info.fam[0].entry_dwords == 6
