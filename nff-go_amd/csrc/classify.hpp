@@ -1242,6 +1242,15 @@ __device__ __forceinline__ void flat_bounds_lds(const IndexedArgs &a, const Fiel
 // loads there (load mode 6) — younger than every entry load of the pass, so
 // no test waits for them (vmcnt counts in order), and into registers the
 // first window's entries have just freed.
+// Timing probes (experiment builds only: make EXTRA=-DNFFACL_EXP_PIPE=k;
+// verdicts wrong by design): 1 entry loads from one line (no gather
+// traffic), 2 no candidate tests, 3 no marks / scans (every candidate owned
+// by lane 0, entries from its stream number), 4 no directory lookups (one
+// candidate per slot per packet).
+#ifndef NFFACL_EXP_PIPE
+#define NFFACL_EXP_PIPE 0
+#endif
+
 template <int NS, class PF>
 __device__ __forceinline__ uint32_t classify_flat_pipe(const IndexedArgs &a, const Fields &f, FlatScratch<4> &W,
                                                        uint32_t lane, PF &&prefetch) {
@@ -1252,7 +1261,15 @@ __device__ __forceinline__ uint32_t classify_flat_pipe(const IndexedArgs &a, con
     // are dead while a pass's entry loads are in flight
     uint32_t st[NS], ln[NS], off = 0, T4 = 0, T6 = 0;
     auto streams = [&]() {
-        flat_bounds_lds<NS>(a, f, st, ln);
+        if (NFFACL_EXP_PIPE == 4) {
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                st[s] = (f.t[0] >> (4 * s)) & 1023u;
+                ln[s] = f.is4 || f.is6 ? 1u : 0u;
+            }
+        } else {
+            flat_bounds_lds<NS>(a, f, st, ln);
+        }
         uint32_t total = 0;
 #pragma unroll
         for (int s = 0; s < NS; ++s) total += ln[s];
@@ -1270,6 +1287,7 @@ __device__ __forceinline__ uint32_t classify_flat_pipe(const IndexedArgs &a, con
     // offset (from a.tab, mod 2^32) of the list's "candidate 0" entry.
     auto mark = [&](bool fam6, uint32_t w, auto rr) {
         constexpr int RR = decltype(rr)::value;
+        if (NFFACL_EXP_PIPE == 3) return;
         wave_lds_sync();  // (the previous window's mark and delta reads come first)
 #pragma unroll
         for (int j = 0; j < RR; ++j) W.mark[64 * j + lane] = 0u;
@@ -1301,7 +1319,7 @@ __device__ __forceinline__ uint32_t classify_flat_pipe(const IndexedArgs &a, con
         static_assert(!SIX || RR == 1, "IPv6 rounds: one per pass");
         uint32_t scan[RR];
 #pragma unroll
-        for (int j = 0; j < RR; ++j) scan[j] = wave_incl_max(W.mark[64 * j + lane]);
+        for (int j = 0; j < RR; ++j) scan[j] = NFFACL_EXP_PIPE == 3 ? 1u : wave_incl_max(W.mark[64 * j + lane]);
         uint32_t carry = 0;
 #pragma unroll
         for (int j = 0; j < RR; ++j) {
@@ -1310,7 +1328,12 @@ __device__ __forceinline__ uint32_t classify_flat_pipe(const IndexedArgs &a, con
             mk[j] = m - 1u;
             const uint32_t k = w + 64u * j + lane;
             const uint32_t dp = W.delta[(mk[j] >> 8) & 0xFFu];
-            const uint32_t o = k < T ? dp + __umul24(k, ent_bytes) : 0u;
+            uint32_t o = k < T ? dp + __umul24(k, ent_bytes) : 0u;
+            if (NFFACL_EXP_PIPE == 1) o = 4u * a.f4.off_ent_base;
+            if (NFFACL_EXP_PIPE == 3) {
+                mk[j] = 0u;
+                o = 4u * a.f4.off_ent_base + __umul24(k & 4095u, ent_bytes);
+            }
             const uint32_t *e = reinterpret_cast<const uint32_t *>(tab8 + o);
             A[j] = ld3(e);
             B[j] = ld3(e + 3);
@@ -1324,6 +1347,10 @@ __device__ __forceinline__ uint32_t classify_flat_pipe(const IndexedArgs &a, con
     // a passing candidate posts (rule index << 32 | output code) to the
     // owner's LDS minimum.
     auto post = [&](bool pass, uint32_t o, const u32x3 &A, const u32x3 &B) {
+        if (NFFACL_EXP_PIPE == 2) {  // keep the loads alive without testing: one cheap use
+            if ((A.x ^ B.z) == 0x5A5A5A5Au) W.best[lane] = 0u;
+            return;
+        }
         if (pass)
             atomicMin(reinterpret_cast<unsigned long long *>(&W.best[o]),
                       static_cast<unsigned long long>(A.z >> kEntIndexShift) << 32 | (B.z >> kHybOutShift));

@@ -1116,8 +1116,12 @@ void build_hybrid(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vec
             // address with radix rb - cgrid (no port bits) it is a candidate
             // for exactly the same packets with 2^cgrid times fewer copies.
             for (int c = 0; opt.cgrid > 0 && c < 2; ++c) {
-                const int k = 2 + c;  // positional slot 6 (dst) / 7 (src)
-                if (((allowed >> k) & 1u) || !fine[f][k].rules.empty()) continue;
+                // the first positional grid slot (4..7) on this address that no fine grid takes
+                const uint32_t field = c == 0 ? kFDst : kFSrc;
+                int k = -1;
+                for (int q = 0; q < 4 && k < 0; ++q)
+                    if (f1s[q] == field && !((allowed >> q) & 1u) && fine[f][q].rules.empty()) k = q;
+                if (k < 0) continue;
                 const DimBuild &db = pl.dims[c];
                 if (db.rb < uint32_t(opt.cgrid) + 6u) continue;
                 const uint32_t wide = 1u << opt.cgrid;
@@ -1130,9 +1134,9 @@ void build_hybrid(const std::vector<uint32_t> &rec4, uint32_t n4, const std::vec
                 if (mv.size() < size_t(opt.fine_min)) continue;
                 std::sort(mv.begin(), mv.end());
                 GSlot gc;
-                gc.f1 = c == 0 ? kFDst : kFSrc;
+                gc.f1 = field;
                 gc.b1 = db.rb - uint32_t(opt.cgrid);
-                gc.f2 = kFSport;
+                gc.f2 = f2s[k];  // (no port bits: b2 = 0)
                 gc.b2 = 0;
                 gc.rules = mv;
                 gc.fill(pl.rr);
@@ -1448,7 +1452,7 @@ bool CompileOptions::from_env(CompileOptions &o, std::string &err) {
     if (set) o.fine_gain = double(v) / 100.0;
     if (!env_knob("NFFACL_TUNE_FINE_MIN", 1, 1 << 20, v, set, err)) return false;
     if (set) o.fine_min = static_cast<int>(v);
-    if (!env_knob("NFFACL_TUNE_FINE_SLOTS", 1, 15, v, set, err)) return false;
+    if (!env_knob("NFFACL_TUNE_FINE_SLOTS", 0, 15, v, set, err)) return false;
     if (set) o.fine_slots = static_cast<int>(v);
     if (!env_knob("NFFACL_TUNE_DIR_PER_RULE", 1, 64, v, set, err)) return false;
     if (set) o.dir_per_rule = static_cast<int>(v);

@@ -335,7 +335,7 @@ bool Tune::from_env(Tune &t, std::string &err) {
     if (set) t.rounds = static_cast<int>(v);
     if (!env_knob("NFFACL_TUNE_LDS", 0, 1, v, set, err)) return false;
     if (set) t.lds = static_cast<int>(v);
-    if (!env_knob("NFFACL_TUNE_PIPE", 0, 1, v, set, err)) return false;
+    if (!env_knob("NFFACL_TUNE_PIPE", 0, 2, v, set, err)) return false;
     if (set) t.pipe = static_cast<int>(v);
     if (!env_knob("NFFACL_TUNE_HOST_DMA", 0, 1, v, set, err)) return false;
     if (set) t.host_dma = static_cast<int>(v);
@@ -551,7 +551,7 @@ static IndexedLaunch indexed_launch(const nffacl_engine *eng, const DevTable *t)
         if (t->meta.slots_g) {  // generalized slots: the generic kernel, always 4 rounds (its scratch)
             L.tm = dev::kTabFlatLdsG;
             L.lds_bytes = lds4;  // > kLdsBytes is refused by the launch check below
-        } else if (tu.pipe && t->meta.flat_uncond && lds4 <= kLdsBytes && !tu.rounds) {
+        } else if (tu.pipe && (t->meta.flat_uncond || tu.pipe == 2) && lds4 <= kLdsBytes && !tu.rounds) {
             // the pipelined walk (its scratch: FlatScratch<4>)
             L.tm = dev::kTabFlatLdsP;
             L.lds_bytes = lds4;

@@ -38,7 +38,8 @@ struct Tune {
     int per_cu = 0;  // NFFACL_TUNE_PER_CU: workgroups per CU (0 = kernel default)
     int rounds = 0;  // NFFACL_TUNE_ROUNDS: flat walks, loads in flight (0 = compiled, 2 or 4)
     int lds = 1;     // NFFACL_TUNE_LDS: 0 keeps INDEXED tables in global memory
-    int pipe = 1;    // NFFACL_TUNE_PIPE: flat-LDS positional tables take the pipelined walk (classify_flat_pipe)
+    int pipe = 1;    // NFFACL_TUNE_PIPE: 1 flat-LDS positional tables with many candidates per packet
+                     // (flat_uncond: C5) take the pipelined walk (classify_flat_pipe); 2 all of them; 0 none
     // nffacl_classify_host (capi.cpp): pinned input read by the kernel over
     // PCIe (0) or DMA'd to HBM first (1); buffers = streams in flight (2..4);
     // packets per chunk, log2
