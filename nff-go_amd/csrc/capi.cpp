@@ -282,6 +282,16 @@ int engine_shell(int hip_device, nffacl_engine **out) {
         delete eng;
         return NFFACL_ERR_HIP;
     }
+    if (eng->tune.dyn) {  // (allocated here: a launch may be captured into a graph)
+        const size_t bytes = size_t(nffacl_engine::kDynStreams) * kDynBlockWords * sizeof(uint32_t);
+        e = hipMalloc(reinterpret_cast<void **>(&eng->d_dyn), bytes);
+        if (e == hipSuccess) e = hipMemset(eng->d_dyn, 0, bytes);
+        if (e != hipSuccess) {
+            set_last_error(std::string("pull heads: ") + hipGetErrorString(e));
+            nffacl_engine_destroy(eng);
+            return NFFACL_ERR_HIP;
+        }
+    }
     *out = eng;
     return NFFACL_OK;
 }
@@ -345,6 +355,7 @@ void nffacl_engine_destroy(nffacl_engine *eng) {
         if (eng->streams[b]) (void)hipStreamDestroy(eng->streams[b]);
         if (eng->done[b]) (void)hipEventDestroy(eng->done[b]);
     }
+    if (eng->d_dyn) (void)hipFree(eng->d_dyn);
     delete eng;
 }
 

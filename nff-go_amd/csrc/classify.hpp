@@ -356,6 +356,12 @@ struct IndexedArgs {
     // checks of its global-memory walk, and the host word they flag
     uint32_t tab_dwords;
     uint32_t *oob;
+    // batch kernels: batches handed out at run time (engine.hip BatchSource)
+    // from the pull heads at `dyn` (nullptr: a fixed grid stride); a pull
+    // takes at most dyn_g batches, fewer as a head drains (dyn_wpx: waves
+    // per head)
+    uint32_t *dyn;
+    uint32_t dyn_g, dyn_gmin, dyn_wpx;
 };
 
 // Table placement (kernel template argument).

@@ -114,7 +114,105 @@ __device__ __forceinline__ uint32_t classify_any(const IndexedArgs &a, const Fie
     return 0u;
 }
 
-// Grid-stride over 64-packet batches.
+// Which 64-packet batches a wave classifies.  heads == nullptr: a fixed grid
+// stride from the wave's global index.  Otherwise batches are pulled at run
+// time, so that a workgroup that starts late (its CU held by a resident
+// consumer, service.hip) takes fewer of them instead of stretching the
+// launch by a whole share.  Eight pull heads, one per group of workgroups
+// sharing an XCD (blockIdx % 8: a label, never relied on for correctness),
+// each own 1/8 of the batches.  A head's range opens with one static chunk
+// per wave of its group, of 1 + (j % 8) batches for the group's j-th wave
+// (no pull at the start, and the staggered lengths spread the group's first
+// pulls over time: a head takes ~88 pulls per microsecond,
+// MI355X_MICROARCH.md "dequeue"; short, so that a late wave's chunk is a
+// short tail); then one returning atomicAdd on the head
+// takes up to dyn_g batches (a guided size, smaller as the head drains,
+// never below dyn_gmin), and a wave whose head is drained pulls from the
+// other seven.  The last wave to finish zeroes the heads for the next
+// launch on the same stream (dyn_heads: one block per stream).
+// (Round 5: the pull's result read a chunk later, its latency hidden, made
+// the compiler carry the batch state per lane and classify wrong batches;
+// the pull is read at once.)
+struct BatchSource {
+    uint32_t *heads;
+    uint64_t nb, b, end, step;  // batches; the current chunk [b, end); the grid stride
+    uint32_t home, tried, g, gmax, gmin, wpx, wpb, groups;
+
+    // waves of group x, and the batches their static chunks take
+    __device__ uint64_t group_waves(uint32_t x) const { return x < groups ? uint64_t((groups - 1 - x) / 8 + 1) * wpb : 0; }
+    __device__ static uint64_t static_len(uint64_t j) {  // sum over waves i < j of (1 + i % 8)
+        const uint64_t r = j & 7u;
+        return j + (j >> 3) * 28u + r * (r - 1) / 2;
+    }
+    __device__ uint32_t pull(uint32_t x, uint32_t n) const {
+        uint32_t s = 0;
+        if (lane_id() == 0) s = atomicAdd(heads + x * kDynHeadStride, n);
+        return __builtin_amdgcn_readfirstlane(s);
+    }
+    // the next chunk from the heads (b = end = nb when all are drained)
+    __device__ void refill() {
+        while (tried < 8) {
+            const uint32_t x = (home + tried) & 7u;
+            const uint64_t lo = (nb * x >> 3) + static_len(group_waves(x)), hi = nb * (x + 1) >> 3;
+            if (lo < hi) {
+                const uint64_t s = lo + pull(x, g);
+                if (s < hi) {
+                    b = s;
+                    end = s + g < hi ? s + g : hi;
+                    const uint64_t per = (hi - end) / (2u * wpx);
+                    g = per < gmin ? gmin : per > gmax ? gmax : static_cast<uint32_t>(per);
+                    return;
+                }
+            }
+            ++tried;
+        }
+        b = end = nb;
+    }
+    // packet index of the wave's first batch (>= n: none)
+    __device__ uint64_t first(uint32_t *h, uint64_t n, const IndexedArgs &a, uint64_t wave, uint64_t waves) {
+        heads = h;
+        nb = (n + 63) >> 6;
+        if (!heads) {
+            b = wave;
+            step = waves;
+            return b * 64;
+        }
+        home = blockIdx.x & 7u;
+        tried = 0;
+        gmax = g = a.dyn_g;
+        gmin = a.dyn_gmin;
+        wpx = a.dyn_wpx;
+        wpb = blockDim.x >> 6;
+        groups = gridDim.x;
+        // this wave's static chunk: the j-th of its group
+        const uint64_t j = uint64_t(blockIdx.x >> 3) * wpb + (wave - uint64_t(blockIdx.x) * wpb);
+        const uint64_t hi = nb * (home + 1) >> 3;
+        b = (nb * home >> 3) + static_len(j);
+        end = b + 1 + (j & 7u);
+        if (end > hi) end = hi;
+        if (b >= end) refill();
+        return b * 64;
+    }
+    __device__ uint64_t next() {
+        if (!heads) {
+            b += step;
+        } else if (++b >= end) {
+            refill();
+        }
+        return b * 64;
+    }
+    // every wave, after its last batch: the last one resets the heads
+    __device__ void finish(uint64_t waves) const {
+        if (!heads) return;
+        uint32_t c = 0;
+        if (lane_id() == 0) c = atomicAdd(heads + 8 * kDynHeadStride, 1u);
+        c = __builtin_amdgcn_readfirstlane(c);
+        if (c == waves - 1 && lane_id() <= 8)
+            __hip_atomic_store(heads + lane_id() * kDynHeadStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+};
+
+// Batches of 64 packets (BatchSource: a grid stride or, load mode 4, pulled).
 //  * rows (any stride): the next batch's 64-byte rows are loaded while the
 //    current batch is classified (software pipelining, 16 VGPRs);
 //  * COAL (stride == 64): lane-contiguous loads + quad transpose, lane l
@@ -129,7 +227,8 @@ k_indexed_slots(const uint8_t *__restrict__ slots, uint32_t stride, uint64_t n, 
     const uint32_t lane = lane_id();
     const uint32_t wpb = blockDim.x >> 6;
     const uint64_t wave0 = uint64_t(blockIdx.x) * wpb + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint64_t step = uint64_t(gridDim.x) * wpb * 64;
+    const uint64_t waves = uint64_t(gridDim.x) * wpb;
+    const uint64_t step = waves * 64;
     constexpr bool RS = MODE == 4 || MODE == 5 || MODE == 6;  // lane-contiguous loads + permlane row swaps
     constexpr bool RSPF = MODE == 5;             // RS + the next batch's loads in flight (16 VGPRs)
     constexpr bool RSIN = MODE == 6;             // RS + the next batch's loads issued by the walk (pf below)
@@ -137,13 +236,15 @@ k_indexed_slots(const uint8_t *__restrict__ slots, uint32_t stride, uint64_t n, 
     constexpr bool NT = MODE >= 2;
     constexpr bool PF = MODE == 3;  // coalesced + next-batch register prefetch
     const uint32_t mine = COAL ? coal_packet(lane) : lane;  // packet of this lane within the batch
-    uint64_t base = wave0 * 64;
+    // pulled batches: load mode 4 (the other modes prefetch the batch a grid stride ahead)
+    BatchSource src;
+    uint64_t base = src.first(MODE == 4 ? a.dyn : nullptr, n, a, wave0, waves);
     uint32_t d[16];
     u32x4 nv[4];
     if (!COAL && !RS && base < n) load16(slots + (base + lane < n ? base + lane : 0) * stride, d);
     if (PF && base + 64 <= n) load_coal<NT>(slots + base * 64, lane, nv);
     if ((RSPF || RSIN) && base + 64 <= n) load_rowswap<NT>(slots + base * 64, lane, nv);
-    for (; base < n; base += step) {
+    for (; base < n; base = src.next()) {
         const uint64_t idx = base + mine;
         const bool live = idx < n;
         const uint8_t *pkt = slots + (live ? idx : 0) * stride;
@@ -216,6 +317,7 @@ k_indexed_slots(const uint8_t *__restrict__ slots, uint32_t stride, uint64_t n, 
             if (lane == 0) permit_out[base >> 6] = permit;
         }
     }
+    src.finish(waves);
 }
 
 // (Round 3: compiled for 6 waves per SIMD — 80 VGPRs, a few spills — with
@@ -229,9 +331,10 @@ k_indexed_frames(const uint8_t *__restrict__ frames, const uint64_t *__restrict_
     if (TM != kTabGlobal && TM != kTabFlat && TM != kTabFlat4) stage_table(a);
     const uint32_t lane = lane_id();
     const uint32_t wpb = blockDim.x >> 6;
-    const uint64_t S = uint64_t(gridDim.x) * wpb * 64;  // grid stride in packets
-    uint64_t base = (uint64_t(blockIdx.x) * wpb + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) * 64;
-    if (base >= n) return;
+    const uint64_t waves = uint64_t(gridDim.x) * wpb;
+    const uint64_t S = waves * 64;  // grid stride in packets
+    const uint64_t wave0 = uint64_t(blockIdx.x) * wpb + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint64_t base = wave0 * 64;
     auto desc_at = [&](uint64_t b) -> uint64_t {  // (branch-free, see load_frames_rs)
         return *(b + lane < n ? desc + b + lane : reinterpret_cast<const uint64_t *>(&g_zero16));
     };
@@ -271,6 +374,7 @@ k_indexed_frames(const uint8_t *__restrict__ frames, const uint64_t *__restrict_
         classify_batch(b, ds, d);
     };
     if (PF) {
+        if (base >= n) return;
         u32x4 A[4], B[4];
         uint64_t dsA = desc_at(base), dsB = 0;
         load_frames_rs(frames, dsA, lane, A);
@@ -294,15 +398,20 @@ k_indexed_frames(const uint8_t *__restrict__ frames, const uint64_t *__restrict_
             if (b2 >= n) break;
             base = b2;
         }
-    } else {
+    } else {  // (pulled batches: BatchSource)
+        BatchSource src;
+        base = src.first(a.dyn, n, a, wave0, waves);
         uint64_t ds_next = desc_at(base);
-        for (; base < n; base += S) {
+        while (base < n) {
             const uint64_t ds = ds_next;
             u32x4 v[4];
             load_frames_rs(frames, ds, lane, v);
-            ds_next = desc_at(base + S);  // issued after this batch's frame loads
+            const uint64_t nx = src.next();
+            ds_next = desc_at(nx);  // issued after this batch's frame loads
             run_batch(base, ds, v);
+            base = nx;
         }
+        src.finish(waves);
     }
 }
 
@@ -335,6 +444,16 @@ bool Tune::from_env(Tune &t, std::string &err) {
     if (set) t.rounds = static_cast<int>(v);
     if (!env_knob("NFFACL_TUNE_LDS", 0, 1, v, set, err)) return false;
     if (set) t.lds = static_cast<int>(v);
+    if (!env_knob("NFFACL_TUNE_DYN", 0, 2, v, set, err)) return false;
+    if (set) t.dyn = static_cast<int>(v);
+    if (!env_knob("NFFACL_TUNE_DYN_GMAX", 1, 64, v, set, err)) return false;
+    if (set) t.dyn_gmax = static_cast<int>(v);
+    if (!env_knob("NFFACL_TUNE_DYN_GMIN", 1, 64, v, set, err)) return false;
+    if (set) t.dyn_gmin = static_cast<int>(v);
+    if (!env_knob("NFFACL_TUNE_DYN_PULLS", 1, 64, v, set, err)) return false;
+    if (set) t.dyn_pulls = static_cast<int>(v);
+    if (!env_knob("NFFACL_TUNE_DYN_TAIL", 1, 64, v, set, err)) return false;
+    if (set) t.dyn_tail = static_cast<int>(v);
     if (!env_knob("NFFACL_TUNE_PIPE", 0, 2, v, set, err)) return false;
     if (set) t.pipe = static_cast<int>(v);
     if (!env_knob("NFFACL_TUNE_HOST_DMA", 0, 1, v, set, err)) return false;
@@ -688,6 +807,31 @@ int prepare_kernels() {
     return NFFACL_OK;
 }
 
+// The pull heads of launches on `stream` (nullptr: none free, grid stride).
+static uint32_t *dyn_heads(nffacl_engine *eng, hipStream_t stream) {
+    if (!eng->d_dyn) return nullptr;
+    std::lock_guard<std::mutex> g(eng->dyn_mu);
+    for (int i = 0; i < eng->dyn_used; ++i)
+        if (eng->dyn_stream[i] == stream) return eng->d_dyn + size_t(i) * kDynBlockWords;
+    if (eng->dyn_used == nffacl_engine::kDynStreams) return nullptr;
+    eng->dyn_stream[eng->dyn_used] = stream;
+    return eng->d_dyn + size_t(eng->dyn_used++) * kDynBlockWords;
+}
+
+// Pulled batches for a launch of `grid` workgroups of `block` threads over n
+// packets: pulls of up to ~1/4 of a wave's share (at most 16 batches), so
+// that the heads see a few pulls per wave (one head saturates near 88
+// pulls per microsecond: MI355X_MICROARCH.md, dequeue).
+static void dyn_args(nffacl_engine *eng, hipStream_t stream, uint32_t grid, uint32_t block, uint64_t n,
+                     dev::IndexedArgs &a) {
+    a.dyn = dyn_heads(eng, stream);
+    const uint64_t waves = uint64_t(grid) * (block / 64), nb = (n + 63) / 64;
+    const Tune &tu = eng->tune;
+    a.dyn_g = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(tu.dyn_gmax, nb / (waves * tu.dyn_pulls))));
+    a.dyn_gmin = std::min<uint32_t>(a.dyn_g, static_cast<uint32_t>(tu.dyn_gmin));
+    a.dyn_wpx = static_cast<uint32_t>(std::max<uint64_t>(1, waves * tu.dyn_tail / 16));
+}
+
 template <int NS, int TM>
 static void launch_slots_tm(int mode, const IndexedLaunch &L, uint32_t grid, hipStream_t stream,
                             const uint8_t *d_slots, uint32_t stride, uint64_t n, const dev::IndexedArgs &a,
@@ -758,6 +902,15 @@ int launch_slots(nffacl_engine *eng, DevTable *t, const uint8_t *d_slots, uint32
         int mode = stride == 64 ? eng->tune.coal : 0;
         if (stride == 64 && !eng->tune.coal_set && (L.tm == dev::kTabFlatLds4U || L.tm == dev::kTabFlatLdsG))
             mode = 5;
+        // pulled batches (BatchSource): the flat-LDS walks (C5: 0.5234 / 0.5262
+        // vs 0.5364 ms alone, +9 % instead of +80 % beside busy consumers);
+        // not the short per-lane walks (C2 0.316 vs 0.220 ms: its waves pull in
+        // lockstep and wait on the heads, and a wave's chunk of consecutive
+        // batches spreads its group's loads over 10x the pages of the grid
+        // stride: 0.27 ms with one pull per wave; profiles/r5_ab/dyn/)
+        const bool flat = L.tm == dev::kTabFlatLds || L.tm == dev::kTabFlatLds4 || L.tm == dev::kTabFlatLds4U ||
+                          L.tm == dev::kTabFlatLdsG || L.tm == dev::kTabFlatLdsP;
+        if (mode == 4 && (eng->tune.dyn == 2 || (eng->tune.dyn == 1 && flat))) dyn_args(eng, stream, grid, L.block, n, a);
         // (the pipelined walk: load mode 4 — mode 6, the next batch's loads
         // issued from inside the walk, spilled and ran 0.64 vs 0.53 ms on C5:
         // NFFACL_TUNE_COAL=6, profiles/r5_ab/)
@@ -795,6 +948,8 @@ int launch_frames(nffacl_engine *eng, DevTable *t, const uint8_t *d_frames,
             return NFFACL_ERR_INVALID_ARG;
         }
         const uint32_t grid = grid_for(eng, n, L.block, L.per_cu);
+        // (pulled batches: C3 0.442 vs 0.396 ms; NFFACL_TUNE_DYN=2 only)
+        if (L.tm != dev::kTabSplit && eng->tune.dyn == 2) dyn_args(eng, stream, grid, L.block, n, a);
         dispatch_indexed(L.ns, L.tm, [&](auto nsc, auto tmc) {
             launch_frames_tm<decltype(nsc)::value, decltype(tmc)::value>(L, grid, stream, d_frames, d_desc, n, a,
                                                                        d_port, d_permit);

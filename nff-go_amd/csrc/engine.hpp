@@ -38,6 +38,12 @@ struct Tune {
     int per_cu = 0;  // NFFACL_TUNE_PER_CU: workgroups per CU (0 = kernel default)
     int rounds = 0;  // NFFACL_TUNE_ROUNDS: flat walks, loads in flight (0 = compiled, 2 or 4)
     int lds = 1;     // NFFACL_TUNE_LDS: 0 keeps INDEXED tables in global memory
+    int dyn = 1;     // NFFACL_TUNE_DYN: batch kernels pull their batches (engine.hip BatchSource):
+                     // 1 the flat-LDS slot walks, 2 every indexed batch kernel, 0 none (grid stride)
+    // pull sizes: at most dyn_gmax batches and about a dyn_pulls-th of a
+    // wave's share; near a head's end (head's remaining batches) /
+    // (waves x dyn_tail / 16), at least dyn_gmin
+    int dyn_gmax = 16, dyn_gmin = 4, dyn_pulls = 4, dyn_tail = 2;
     int pipe = 1;    // NFFACL_TUNE_PIPE: 1 flat-LDS positional tables with many candidates per packet
                      // (flat_uncond: C5) take the pipelined walk (classify_flat_pipe); 2 all of them; 0 none
     // nffacl_classify_host (capi.cpp): pinned input read by the kernel over
@@ -50,6 +56,11 @@ struct Tune {
     // false (+ `err`) if a set variable is out of range
     static bool from_env(Tune &t, std::string &err);
 };
+
+// Pull heads of the batch kernels (engine.hip BatchSource): eight heads and a
+// finish counter, a 128-byte line each, per stream an engine launches on.
+constexpr uint32_t kDynHeadStride = 32;
+constexpr uint32_t kDynBlockWords = 9 * kDynHeadStride;
 
 int upload_table(nffacl_engine *eng, const nffacl_rules &rules, TablePtr &out);
 // An engine without a table (launch shape of `hip_device` only): the device
@@ -93,6 +104,14 @@ struct nffacl_engine {
     hipStream_t streams[kHostBufs] = {};
     hipEvent_t done[kHostBufs] = {};
     uint32_t staged_stride = 0;
+    // BatchSource heads: block i serves dyn_stream[i] (launches on one stream
+    // are ordered, and each launch leaves its block zeroed for the next);
+    // streams beyond kDynStreams launch with the fixed grid stride
+    static constexpr int kDynStreams = 64;
+    std::mutex dyn_mu;
+    uint32_t *d_dyn = nullptr;
+    hipStream_t dyn_stream[kDynStreams] = {};
+    int dyn_used = 0;
 };
 
 namespace nffacl {

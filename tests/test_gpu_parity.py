@@ -668,3 +668,47 @@ def test_frames_ragged_and_short(torch_cuda, algo, n):
     want = oracle.classify_frames(frames, desc, a4, a6, threads=THREADS)
     np.testing.assert_array_equal(port.cpu().numpy().view(np.uint32), want)
     np.testing.assert_array_equal(permit.cpu().numpy().view(np.uint64), permit_bits(want))
+
+
+@pytest.mark.parametrize("cfg", ["c2", "c3", "c5"])
+def test_pulled_batches_gpu(torch_cuda, monkeypatch, cfg):
+    """Batches pulled from the per-stream heads (NFFACL_TUNE_DYN=2) ==
+    the fixed grid stride (DYN=0) == the oracle: ragged sizes back to back on
+    one stream (each launch must leave its heads zeroed for the next), on 64-B
+    slots and IMIX frames, and launches alternating over two streams."""
+    torch = torch_cuda
+    g = synth.gen_rules(synth.SPECS[cfg], synth.RULE_SEEDS[cfg])
+    rules, (a4, a6) = _rules_and_arrays(g.text)
+    sizes = [1, 63, 64 * 7 + 5, (1 << 16) + 3, (1 << 20) + 17, 200]
+    nmax = max(sizes)
+    slots = synth.gen_slots(g, nmax, 41)
+    frames, desc = synth.gen_imix(g, nmax, 42)
+    d_slots, d_frames = to_dev(torch, slots), to_dev(torch, frames)
+    d_desc = to_dev(torch, desc.view(np.int64))
+    outs = {}
+    for dyn in ("0", "2"):  # (2: every indexed batch kernel pulls, the default 1 only the flat-LDS walks)
+        monkeypatch.setenv("NFFACL_TUNE_DYN", dyn)
+        with nffacl.Engine(rules) as eng:
+            s2 = torch.cuda.Stream()
+            res = []
+            for k, n in enumerate(sizes):
+                st = torch.cuda.current_stream() if k % 3 != 2 else s2
+                port = torch.empty(n, dtype=torch.int32, device="cuda")  # (every word is written)
+                fport = torch.empty(n, dtype=torch.int32, device="cuda")
+                bits = torch.empty((n + 63) // 64, dtype=torch.int64, device="cuda")
+                with torch.cuda.stream(st):
+                    eng.classify_device(d_slots, 64, n, port, bits, st)
+                    eng.classify_frames_device(d_frames, d_desc, n, fport, None, st)
+                res.append((port, bits, fport))
+            torch.cuda.synchronize()
+            outs[dyn] = [[t.cpu().numpy() for t in r] for r in res]
+    for k, n in enumerate(sizes):
+        for a, b in zip(outs["0"][k], outs["2"][k]):
+            np.testing.assert_array_equal(a, b)
+    m = (1 << 16) + 3
+    k = sizes.index(m)
+    want = oracle.classify_slots(slots[:m * 64], 64, m, a4, a6, threads=THREADS)
+    np.testing.assert_array_equal(outs["2"][k][0].view(np.uint32), want)
+    np.testing.assert_array_equal(outs["2"][k][1].view(np.uint64), permit_bits(want))
+    want_f = oracle.classify_frames(frames, desc[:m], a4, a6, threads=THREADS)
+    np.testing.assert_array_equal(outs["2"][k][2].view(np.uint32), want_f)

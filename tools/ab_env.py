@@ -61,6 +61,7 @@ def with_env(env, f):
                 os.environ[k] = v
 
 
+print(f"{cfg}: inputs ready", file=sys.stderr, flush=True)  # (progress: a silent GPU run reads as hung)
 ref = None
 exact = {}
 for name, env in variants.items():
@@ -71,6 +72,7 @@ for name, env in variants.items():
     if ref is None:
         ref = got
     exact[name] = bool((got == ref).all())
+    print(f"{name}: bit-exact {exact[name]}", file=sys.stderr, flush=True)
 times = {k: [] for k in variants}
 for _ in range(rounds):
     for name, env in variants.items():
@@ -85,6 +87,7 @@ for _ in range(rounds):
             torch.cuda.synchronize()
             return [a.elapsed_time(b) for a, b in evs]
         times[name] += with_env(env, timed)
+    print(f"round {_}: " + " ".join(f"{k} {np.median(v):.4f}" for k, v in times.items()), file=sys.stderr, flush=True)
 out = {k: {"median_ms": float(np.median(v)), "min_ms": float(np.min(v)), "Gpps": n / float(np.median(v)) / 1e6,
            "bit_exact_vs_first": exact[k]} for k, v in times.items()}
 print(json.dumps({"config": cfg, "packets": n, "rounds": rounds, "variants": out,
