@@ -698,10 +698,15 @@ static IndexedLaunch indexed_launch(const nffacl_engine *eng, const DevTable *t)
         // beat two of 1024 (0.2119 vs 0.2161 ms on C2; 512 / 640 / 896:
         // 0.2229 / 0.2216 / 0.2177, profiles/r3_ab/blocks/)
         L.block = L.tm == dev::kTabLdsNP ? 768u : 1024u;
-        // lane form: one workgroup per CU (its VGPRs allow no second one)
+        // lane form: one workgroup per CU (its VGPRs allow no second one).
+        // LDS-staged INDEXED: twice the workgroups that fit a CU at once
+        // (two of 768 threads), so that each takes half a share and one that
+        // starts late (its CU's LDS held by a resident consumer, §4.7) adds
+        // half the tail: C2 0.2145 vs 0.2200 ms alone (profiles/r5_ab/pcu/)
         L.per_cu = L.tm == dev::kTabSplit
                        ? 1u
-                       : static_cast<uint32_t>(std::max<size_t>(1, std::min<size_t>(2, kLdsBytes / std::max<size_t>(staged, 16))));
+                       : 2u * static_cast<uint32_t>(
+                                  std::max<size_t>(1, std::min<size_t>(2, kLdsBytes / std::max<size_t>(staged, 16))));
         L.lds_bytes = std::max<size_t>(staged, 16);
     }
     if (tu.block) L.block = static_cast<uint32_t>(tu.block);
