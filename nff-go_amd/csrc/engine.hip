@@ -907,8 +907,10 @@ int launch_slots(nffacl_engine *eng, DevTable *t, const uint8_t *d_slots, uint32
         int mode = stride == 64 ? eng->tune.coal : 0;
         if (stride == 64 && !eng->tune.coal_set && (L.tm == dev::kTabFlatLds4U || L.tm == dev::kTabFlatLdsG))
             mode = 5;
-        // pulled batches (BatchSource): the flat-LDS walks (C5: 0.5234 / 0.5262
-        // vs 0.5364 ms alone, +9 % instead of +80 % beside busy consumers);
+        // pulled batches (BatchSource): the flat-LDS walks (C5: 0.5111 vs
+        // 0.5341 ms alone with pulls of 12-16 batches — 0.5159 / 0.5208 /
+        // 0.5247 with at least 8 / 16 / 4 — and +9-13 % instead of +80 %
+        // beside busy consumers, profiles/r5_ab/dyn/);
         // not the short per-lane walks (C2 0.316 vs 0.220 ms: its waves pull in
         // lockstep and wait on the heads, and a wave's chunk of consecutive
         // batches spreads its group's loads over 10x the pages of the grid

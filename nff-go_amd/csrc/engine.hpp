@@ -43,7 +43,7 @@ struct Tune {
     // pull sizes: at most dyn_gmax batches and about a dyn_pulls-th of a
     // wave's share; near a head's end (head's remaining batches) /
     // (waves x dyn_tail / 16), at least dyn_gmin
-    int dyn_gmax = 16, dyn_gmin = 4, dyn_pulls = 4, dyn_tail = 2;
+    int dyn_gmax = 16, dyn_gmin = 12, dyn_pulls = 4, dyn_tail = 2;
     int pipe = 1;    // NFFACL_TUNE_PIPE: 1 flat-LDS positional tables with many candidates per packet
                      // (flat_uncond: C5) take the pipelined walk (classify_flat_pipe); 2 all of them; 0 none
     // nffacl_classify_host (capi.cpp): pinned input read by the kernel over

@@ -712,3 +712,29 @@ def test_pulled_batches_gpu(torch_cuda, monkeypatch, cfg):
     np.testing.assert_array_equal(outs["2"][k][1].view(np.uint64), permit_bits(want))
     want_f = oracle.classify_frames(frames, desc[:m], a4, a6, threads=THREADS)
     np.testing.assert_array_equal(outs["2"][k][2].view(np.uint32), want_f)
+
+
+def test_pulled_batches_many_streams_gpu(torch_cuda, monkeypatch):
+    """More streams than an engine has blocks of pull heads (64): launches on
+    the streams past them take the grid stride; every verdict equals the
+    oracle, and a stream that launched before keeps its heads."""
+    torch = torch_cuda
+    monkeypatch.setenv("NFFACL_TUNE_DYN", "2")
+    g = synth.gen_rules(synth.SPECS["c5"], synth.RULE_SEEDS["c5"])
+    rules, (a4, a6) = _rules_and_arrays(g.text)
+    n = 64 * 37 + 11
+    slots = synth.gen_slots(g, n, 43)
+    want = oracle.classify_slots(slots, 64, n, a4, a6, threads=THREADS)
+    d_slots = to_dev(torch, slots)
+    with nffacl.Engine(rules) as eng:
+        streams = [torch.cuda.Stream() for _ in range(70)]
+        outs = []
+        for rep in range(2):
+            for st in streams:
+                port = torch.empty(n, dtype=torch.int32, device="cuda")
+                with torch.cuda.stream(st):
+                    eng.classify_device(d_slots, 64, n, port, None, st)
+                outs.append(port)
+        torch.cuda.synchronize()
+        for port in outs:
+            np.testing.assert_array_equal(port.cpu().numpy().view(np.uint32), want)
