@@ -81,6 +81,8 @@ struct SvcArgs {
     uint64_t hot_ticks;     // a mailbox answered within this window is read whole every pass
     uint64_t life_ticks;    // leave after this long in any case
     uint32_t idle_naps;     // burst consumer: s_sleep(8) (~0.2 us) naps of an idle wave between bell reads
+    uint32_t post_naps;     // burst consumer: s_sleep(2) (~50 ns) naps after an answer, before the next poll
+                            // (NFFACL_TUNE_SVC_POST_NAPS, default 12)
                             // (NFFACL_TUNE_SVC_IDLE_NAPS)
     uint32_t full_poll;     // burst consumer: hot waves read the whole mailbox every pass (default; 0: the
                             // header, then the packets on a new tag — NFFACL_TUNE_SVC_FULLPOLL=0)
@@ -579,6 +581,14 @@ __global__ void __launch_bounds__(64) k_service_burst(SvcArgs a) {
 #if NFFACL_EXP_SVCSTAT
         t_ans = wall_clock64();
 #endif
+        // Wait ~0.6 us before the next poll: one issued at once reaches the
+        // mailbox before the caller has seen this answer and posted its next
+        // burst, returns empty, and the request waits for the poll after it —
+        // a whole PCIe round trip.  C2 rules, 16 / 32 clones: 87-103 /
+        // 147-160 Mpps without the nap, 122-124 / 182-191 with 12 naps (6 / 8
+        // / 10 / 15: 97-102 / 100-112 / 107-119 / 120-121 at 16 clones;
+        // NFFACL_TUNE_SVC_POST_NAPS, profiles/r5_ab/burst/)
+        for (uint32_t i = 0; i < a.post_naps; ++i) __builtin_amdgcn_s_sleep(2);
     }
     if (lane == 0) {
         uint64_t *st = a.stats + size_t(blockIdx.x) * kSvcStatWords;
@@ -1108,6 +1118,12 @@ int service_create(int hip_device, uint32_t mailboxes, uint32_t idle_us, bool bu
             return NFFACL_ERR_INVALID_ARG;
         }
         s->args.idle_naps = set ? static_cast<uint32_t>(v) : 0u;
+        if (!env_knob("NFFACL_TUNE_SVC_POST_NAPS", 0, 200, v, set, err)) {
+            set_last_error(err);
+            release_service(s);
+            return NFFACL_ERR_INVALID_ARG;
+        }
+        s->args.post_naps = set ? static_cast<uint32_t>(v) : 12u;
         if (!env_knob("NFFACL_TUNE_SVC_TRACE", 0, 1, v, set, err)) {
             set_last_error(err);
             release_service(s);
