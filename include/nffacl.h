@@ -283,7 +283,12 @@ enum nffacl_parse_flags {
  * d_port[i]  <- L3ACLPort (may be NULL)
  * d_permit_bits[i/64] bit i%64 <- L3ACLPermit (may be NULL; ceil(n/64) words;
  *   bits past n in the last word are 0).
- * Asynchronous on `stream` (hipStream_t, NULL = default stream). */
+ * Asynchronous on `stream` (hipStream_t, NULL = default stream).  Launches
+ * of one engine on one stream run in stream order; the large-table kernels
+ * hand out their batches through per-stream counters of the engine, so a
+ * launch captured into a graph must not be replayed concurrently with
+ * launches of the same engine on the stream it was captured from (or set
+ * NFFACL_TUNE_DYN=0 before creating the engine). */
 NFFACL_API int nffacl_classify_device(nffacl_engine *eng, const uint8_t *d_slots, uint32_t stride,
                            uint64_t n, uint32_t *d_port, uint64_t *d_permit_bits,
                            void *stream);
