@@ -65,6 +65,29 @@ def test_one_device_group_c2_vs_oracle(torch_cuda, n):
         np.testing.assert_array_equal(b, _bits(want))
 
 
+def test_one_device_group_c5_vs_engine_and_oracle(torch_cuda):
+    """The large-table path (HYBRID flat-LDS, ~5 MB of entries broadcast from
+    the root): the group's verdicts equal an Engine's on the same rules and
+    the oracle."""
+    torch = torch_cuda
+    g = synth.gen_rules(synth.SPECS["c5"], synth.RULE_SEEDS["c5"])
+    n = (1 << 16) + 3
+    slots = synth.gen_slots(g, n, 53)
+    a4, a6 = ro.parse_text_table(g.text.encode()).arrays()
+    want = oracle.classify_slots(slots, 64, n, a4, a6, threads=16)
+    rules = nffacl.L3Rules.parse_text(g.text)
+    with nffacl.Group([0], rules) as grp:
+        p, b = _run(torch, grp, slots, n)
+    np.testing.assert_array_equal(p, want)
+    np.testing.assert_array_equal(b, _bits(want))
+    with nffacl.Engine(rules) as eng:
+        d = torch.from_numpy(slots).to("cuda")
+        port = torch.empty(n, dtype=torch.int32, device="cuda")
+        eng.classify_device(d, 64, n, port)
+        torch.cuda.synchronize()
+    np.testing.assert_array_equal(port.cpu().numpy().view(np.uint32), p)
+
+
 def test_group_arguments_and_local_device(torch_cuda):
     g, _, _ = _c2(64)
     rules = nffacl.L3Rules.parse_text(g.text)
