@@ -738,3 +738,35 @@ def test_pulled_batches_many_streams_gpu(torch_cuda, monkeypatch):
         torch.cuda.synchronize()
         for port in outs:
             np.testing.assert_array_equal(port.cpu().numpy().view(np.uint32), want)
+
+
+@pytest.mark.parametrize("cfg", ["c2", "c5"])
+def test_graph_capture_replay_gpu(torch_cuda, cfg):
+    """A classify launch captured into a HIP graph (torch.cuda.CUDAGraph) and
+    replayed back to back: every replay equals the oracle (C5's pulled-batch
+    heads are left zeroed by each replay for the next)."""
+    torch = torch_cuda
+    g = synth.gen_rules(synth.SPECS[cfg], synth.RULE_SEEDS[cfg])
+    rules, (a4, a6) = _rules_and_arrays(g.text)
+    n = (1 << 16) + 3
+    slots = synth.gen_slots(g, n, 47)
+    want = oracle.classify_slots(slots, 64, n, a4, a6, threads=THREADS)
+    d_slots = to_dev(torch, slots)
+    port = torch.zeros(n, dtype=torch.int32, device="cuda")
+    bits = torch.zeros((n + 63) // 64, dtype=torch.int64, device="cuda")
+    with nffacl.Engine(rules) as eng:
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):  # warm-up launch outside the capture
+            eng.classify_device(d_slots, 64, n, port, bits, s)
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            eng.classify_device(d_slots, 64, n, port, bits, torch.cuda.current_stream())
+        for _ in range(3):
+            port.zero_()
+            bits.zero_()
+            graph.replay()
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(port.cpu().numpy().view(np.uint32), want)
+            np.testing.assert_array_equal(bits.cpu().numpy().view(np.uint64), permit_bits(want))
+        del graph
