@@ -1485,21 +1485,40 @@ bool compile_table(const nffacl_rules &rules, int algo, const CompileOptions &op
     // profiles/r1_configs_k/) — unless its inline table outgrows LDS, where
     // HYBRID keeps the directories in LDS and the lists compact in HBM.
     if (algo == NFFACL_ALGO_HYBRID && !hybrid_encodable(rec4, out.n4, rec6, out.n6)) algo = NFFACL_ALGO_INDEXED;
+    // HYBRID, and never a flat-LDS image past the staged-image limit (the
+    // launch refuses one, table_consistent): should the fine 2-D grids push
+    // it there (layout knobs: NFFACL_TUNE_FINE_A = 10 at C5 made 271 KB),
+    // build without them, and failing that with global directories
+    auto hybrid = [&](uint32_t n4, uint32_t n6) {
+        auto build = [&](const CompileOptions &o) {
+            out = CompiledTable{};
+            out.n4 = n4;
+            out.n6 = n6;
+            out.algo = NFFACL_ALGO_HYBRID;
+            build_hybrid(rec4, n4, rec6, n6, o, out);
+        };
+        auto over = [&] {  // (table_consistent's limits: flat-LDS image / lane-form directories)
+            const size_t b = size_t(out.lds_dwords) * sizeof(uint32_t);
+            return out.idx4.entry_dwords == kHybEnt4Dwords ? b > kHybLdsDirMaxBytes : b > kLdsTableBytes;
+        };
+        build(opt);
+        if (!over()) return;
+        CompileOptions o = opt;
+        o.fine_a = 0;
+        build(o);
+        if (!over()) return;
+        o.flat = 1;
+        build(o);
+    };
     if (algo == NFFACL_ALGO_HYBRID) {
-        out.algo = NFFACL_ALGO_HYBRID;
-        build_hybrid(rec4, out.n4, rec6, out.n6, opt, out);
+        hybrid(out.n4, out.n6);
     } else if (algo != NFFACL_ALGO_LINEAR && indexable(rules)) {
         out.algo = NFFACL_ALGO_INDEXED;
         build_family(rec4, kRec4Dwords, false, out.n4, out.blob, out.idx4);
         build_family(rec6, kRec6Dwords, true, out.n6, out.blob, out.idx6);
         if (algo == NFFACL_ALGO_AUTO && out.blob.size() * 4 > kLdsTableBytes &&
             hybrid_encodable(rec4, out.n4, rec6, out.n6)) {
-            const uint32_t n4 = out.n4, n6 = out.n6;
-            out = CompiledTable{};
-            out.n4 = n4;
-            out.n6 = n6;
-            out.algo = NFFACL_ALGO_HYBRID;
-            build_hybrid(rec4, n4, rec6, n6, opt, out);
+            hybrid(out.n4, out.n6);
         }
     } else {
         out.algo = NFFACL_ALGO_LINEAR;

@@ -593,3 +593,18 @@ def test_hybrid_fine_grids_when_offsets_overflow(case):
     fine = [info.fam[0].dims[k] for k in range(4, info.fam[0].n_slots) if info.fam[0].dims[k].n_rules]
     assert fine and all(d.max_list < 300 for d in fine)  # the C5 rules' own grids stay, without the hot bucket
     assert info.fam[0].dims[0].dir8 == 0 and info.fam[0].dims[0].off_dir16 != 0  # u16 form
+
+
+@pytest.mark.parametrize("env", [{"NFFACL_TUNE_FINE_A": "10"}, {"NFFACL_TUNE_FINE_A": "9", "NFFACL_TUNE_FINE_P": "7"}])
+def test_hybrid_oversized_fine_grids_fall_back(monkeypatch, env):
+    """Layout knobs whose fine 2-D grids would push the flat-LDS image past
+    the staged-image limit (FINE_A = 10 at C5: 271 KB) compile without the
+    grids instead (or, failing that, with global directories): the image
+    always fits and the walk still gives the oracle's first match."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    g = synth.gen_rules(synth.SPECS["c5"], synth.RULE_SEEDS["c5"])
+    n = 1 << 12
+    slots = synth.gen_slots(g, n, synth.PACKET_SEEDS["c5"] + 13)
+    info = check_hybrid(g.text, slots, n)
+    assert info.lds_dwords * 4 <= 135 * 1024
