@@ -88,7 +88,9 @@ struct CompileOptions {
     int uncond = -1;        // NFFACL_TUNE_UNCOND: flat-LDS branch-free entry loads (-1 = policy)
     // NFFACL_TUNE_FINE_A / _P: fine 2-D address x port slots of the flat-LDS
     // form (positional slots 4..7), a address bits x p port bits; a = 0: none
-    int fine_a = 8;          // 8 x 4 on slots 4-5: C5 0.583 vs 0.626 ms (profiles/r4_ab/fine/)
+    int fine_a = 9;          // address bits of the fine grids: 9 with the 4-bit directories (C5 0.4941 vs
+                             // 0.5128 ms at 8: a third fewer 1-D entries, 3.9 vs 5.0 MB; profiles/r5_ab/fine/);
+                             // round 4, u8 directories: 8 x 4 on slots 4-5 0.583 vs 0.626 (profiles/r4_ab/fine/)
     int fine_p = 5;          // 8 x 5: C5 0.5741 / 0.5718 vs 0.5829 / 0.5825 ms in two sweeps (ab_c5_fine_sweep*)
     double fine_gain = 0.5;  // NFFACL_TUNE_FINE_G (1/100): a rule moves below this fraction of its 1-D cover
     int fine_min = 256;      // NFFACL_TUNE_FINE_MIN: fewest moved rules worth a fine slot

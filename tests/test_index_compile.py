@@ -550,7 +550,7 @@ def test_hybrid_fine_slots_and_param_block(monkeypatch, cfg, env):
     fine = [info.fam[0].dims[k] for k in range(4, info.fam[0].n_slots) if info.fam[0].dims[k].n_rules]
     if env.get("NFFACL_TUNE_FINE_A") == "0":
         assert not fine and info.fam[0].n_slots == 4
-    else:  # default: 8 x 4 grids on slots 4-5 (dst x dport, src x dport)
+    else:  # default: 9 x 5 grids on slots 4-5 (dst x dport, src x dport)
         assert fine and all(d.kind2 != KIND_NONE for d in fine)
         if cfg == "c5" and not env:
             assert info.fam[0].n_slots == 6
