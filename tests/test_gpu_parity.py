@@ -770,3 +770,26 @@ def test_graph_capture_replay_gpu(torch_cuda, cfg):
             np.testing.assert_array_equal(port.cpu().numpy().view(np.uint32), want)
             np.testing.assert_array_equal(bits.cpu().numpy().view(np.uint64), permit_bits(want))
         del graph
+
+
+@pytest.mark.parametrize("fine_slots", ["7", "11", "15"])
+def test_c5_more_fine_grids_gpu(torch_cuda, monkeypatch, fine_slots):
+    """Fine grids on three / all four positional grid slots (NFFACL_TUNE_FINE_SLOTS,
+    NS = 7 / 8 kernels): slots and IMIX frames equal the oracle."""
+    torch = torch_cuda
+    monkeypatch.setenv("NFFACL_TUNE_FINE_SLOTS", fine_slots)
+    g = synth.gen_rules(synth.SPECS["c5"], synth.RULE_SEEDS["c5"])
+    rules, (a4, a6) = _rules_and_arrays(g.text)
+    n = (1 << 16) + 5
+    slots = synth.gen_slots(g, n, 61)
+    with nffacl.Engine(rules, algo=nffacl.ALGO_HYBRID) as eng:
+        p, b = classify(torch, eng, slots, 64, n)
+        want = oracle.classify_slots(slots, 64, n, a4, a6, threads=THREADS)
+        np.testing.assert_array_equal(p, want)
+        np.testing.assert_array_equal(b, permit_bits(want))
+        frames, desc = synth.gen_imix(g, 1 << 14, 62)
+        port = torch.zeros(1 << 14, dtype=torch.int32, device="cuda")
+        eng.classify_frames_device(to_dev(torch, frames), to_dev(torch, desc.view(np.int64)), 1 << 14, port)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(port.cpu().numpy().view(np.uint32),
+                                      oracle.classify_frames(frames, desc, a4, a6, threads=THREADS))
