@@ -700,10 +700,11 @@ static IndexedLaunch indexed_launch(const nffacl_engine *eng, const DevTable *t)
         }
     }
     if (L.tm != dev::kTabGlobal) {
-        // the no-port kernel: two 768-thread workgroups per CU (24 waves)
-        // beat two of 1024 (0.2119 vs 0.2161 ms on C2; 512 / 640 / 896:
-        // 0.2229 / 0.2216 / 0.2177, profiles/r3_ab/blocks/)
-        L.block = L.tm == dev::kTabLdsNP ? 768u : 1024u;
+        // 1024-thread workgroups: with twice the resident workgroups per CU
+        // launched (below) C2 runs 0.2038-0.2057 vs 0.2142 ms with 768
+        // (profiles/r5_ab/blocks/; round 3, one launch per resident slot,
+        // 768 had won: 0.2119 vs 0.2161, profiles/r3_ab/blocks/)
+        L.block = 1024u;
         // lane form: one workgroup per CU (its VGPRs allow no second one).
         // LDS-staged INDEXED: twice the workgroups that fit a CU at once
         // (two of 768 threads), so that each takes half a share and one that
