@@ -707,7 +707,7 @@ static IndexedLaunch indexed_launch(const nffacl_engine *eng, const DevTable *t)
         L.block = 1024u;
         // lane form: one workgroup per CU (its VGPRs allow no second one).
         // LDS-staged INDEXED: twice the workgroups that fit a CU at once
-        // (two of 768 threads), so that each takes half a share and one that
+        // (two of 1024 threads), so that each takes half a share and one that
         // starts late (its CU's LDS held by a resident consumer, §4.7) adds
         // half the tail: C2 0.2145 vs 0.2200 ms alone (profiles/r5_ab/pcu/)
         L.per_cu = L.tm == dev::kTabSplit
