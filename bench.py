@@ -457,6 +457,57 @@ def call_shapes(cfg: str, text: str, gen, cpu_mpps, local: int):
     return res
 
 
+def text_of(cfg: str) -> str:
+    return build_rules(cfg)[0]
+
+
+def group_leg(st: dict, args, engine_ms: float, text: str, local: int) -> dict:
+    """The C-ABI device group (nffacl_group_classify_device, one process
+    driving every visible GPU: the reference's clones-in-one-process
+    deployment, flow/scheduler.go:283-289) over the same resident batch:
+    K launches timed like the headline, for groups of the first 1, 2, 4, ...
+    visible devices (root = this rank's device).  At one device it must match
+    the Engine's rate (no collective runs); on a multi-GPU node it is the
+    curve a Go host would get (RCCL scatter / gather over xGMI, DESIGN.md
+    §6).  Verdicts bit-exact vs the Engine's own classify of the batch."""
+    import torch
+    import nffacl
+    ndev = torch.cuda.device_count()
+    devs = [local] + [d for d in range(ndev) if d != local]
+    rules = nffacl.L3Rules.parse_text(text)
+    n, stream, d_slots = st["n"], st["stream"], st["d_slots"]
+    dev = d_slots.device
+    port = torch.empty(n, dtype=torch.int32, device=dev)
+    permit = torch.empty((n + 63) // 64, dtype=torch.int64, device=dev)
+    res = {"devices_visible": ndev, "packets": n, "engine_ms": engine_ms, "curve": []}
+    sizes = sorted({min(ndev, 1 << k) for k in range(8)})
+    exact = True
+    for size in sizes:
+        try:
+            grp = nffacl.Group(devs[:size], rules)
+        except nffacl.NFError as e:
+            res["curve"].append({"devices": size, "error": str(e)})
+            exact = False
+            break
+        with grp:
+            for _ in range(max(args.warmup, 3)):
+                grp.classify_device(d_slots, 64, n, port, permit, stream)
+            torch.cuda.synchronize(dev)
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+            for _ in range(args.steps):
+                grp.classify_device(d_slots, 64, n, port, permit, stream)
+            b.record(stream)
+            torch.cuda.synchronize(dev)
+            ms = a.elapsed_time(b) / args.steps
+        same = bool(torch.equal(port.cpu(), st["port"].cpu()))
+        exact = exact and same
+        res["curve"].append({"devices": size, "ms": round(ms, 4), "mpps": round(n / ms / 1e3, 1),
+                             "vs_engine": round(engine_ms / ms, 4), "bit_exact_vs_engine": same})
+    res["bit_exact_vs_engine"] = exact
+    return res
+
+
 def compact_shapes(res: dict) -> dict:
     """One config's call-shape record as it goes into the JSON line: per
     shape the rate, latency, exactness and same-CPU ratio (the consumer's
@@ -482,6 +533,9 @@ def summary(out: dict, ok: bool, cfg: str) -> dict:
     for k in ("host_inclusive_mpps", "host_inclusive_bit_exact_sample"):
         if k in out:
             s[k] = out[k]
+    grp = out.get("device_group") or {}
+    if grp.get("curve"):
+        s["device_group"] = [{k: c.get(k) for k in ("devices", "mpps", "vs_engine")} for c in grp["curve"]]
     for c, r in (out.get("call_shapes") or {}).items():
         b = r.get("burst32_16_clones") or {}
         b32 = r.get("burst32_32_clones") or {}
@@ -513,6 +567,8 @@ def main():
                     help="N>1: skip the root-scattered (scatter+classify+gather) measurement")
     ap.add_argument("--no-shapes", action="store_true",
                     help="N=1: skip the call-shape record (scalar calls / bursts through the resident consumer)")
+    ap.add_argument("--no-group", action="store_true",
+                    help="N=1: skip the C-ABI device-group leg (nffacl_group_classify_device)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend for N>1 (nccl = RCCL on ROCm)")
     args = ap.parse_args()
@@ -603,6 +659,9 @@ def main():
         ok = ok and cb["bit_exact_vs_gpu"]
     elif rank == 0:
         out["cpu_baseline"] = None
+    if rank == 0 and world == 1 and not args.no_group and not st["frames_mode"] and not st["l2_mode"]:
+        out["device_group"] = group_leg(st, args, rec["ms_per_step"], text_of(cfg), local)
+        ok = ok and out["device_group"].get("bit_exact_vs_engine", False)
     shapes = {}
     do_shapes = rank == 0 and world == 1 and not args.no_shapes and cfg in ("c1", "c2", "c3", "c5")
     if do_shapes:

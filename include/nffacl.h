@@ -62,7 +62,7 @@
 extern "C" {
 #endif
 
-#define NFFACL_ABI_VERSION 6
+#define NFFACL_ABI_VERSION 7
 
 /* Only the entry points below are exported from libnffacl.so (built with
  * -fvisibility=hidden). */
@@ -214,6 +214,31 @@ NFFACL_API void nffacl_engine_destroy(nffacl_engine *eng);
 NFFACL_API int nffacl_engine_algo(const nffacl_engine *eng);
 /* Bytes of the active device table (rule records + index), for reporting. */
 NFFACL_API int nffacl_engine_table_bytes(const nffacl_engine *eng, uint64_t *bytes);
+
+/* The kernel the active table's launches over dense 64-byte slots take
+ * (inspection and tests; ABI 7). */
+enum nffacl_walk {
+    NFFACL_WALK_LINEAR = 0,          /* wave-uniform rule scan (k_linear_slots) */
+    NFFACL_WALK_INDEXED_GLOBAL = 1,  /* per-lane candidate lists, table in global memory */
+    NFFACL_WALK_INDEXED_LDS = 2,     /* per-lane candidate lists, table staged in LDS */
+    NFFACL_WALK_HYBRID_LANE = 3,     /* LDS directories, per-lane walks of HBM entries */
+    NFFACL_WALK_FLAT = 4,            /* flat candidate walk, directories in global memory */
+    NFFACL_WALK_FLAT_LDS = 5,        /* flat candidate walk, directories in LDS (classify_flat) */
+    NFFACL_WALK_FLAT_LDS_GENERIC = 6,/* the same over generalized (compacted) slots */
+    NFFACL_WALK_FLAT_LDS_PIPELINED = 7 /* pipelined family-split walk (classify_flat_pipe) */
+};
+typedef struct nffacl_kernel_info {
+    int32_t walk;        /* enum nffacl_walk */
+    uint32_t slots;      /* key slots the kernel walks (its NS) */
+    uint32_t rounds;     /* flat walks: entry-load rounds per window (2 or 4); else 0 */
+    uint32_t block;      /* threads per workgroup */
+    uint32_t per_cu;     /* workgroups launched per CU */
+    int32_t load_mode;   /* packet load mode at stride 64 (engine.hip) */
+    uint32_t pulled;     /* 1: waves pull their batches at run time (BatchSource) */
+    uint32_t reserved;
+    uint64_t lds_bytes;  /* dynamic LDS per workgroup */
+} nffacl_kernel_info;
+NFFACL_API int nffacl_engine_kernel_info(nffacl_engine *eng, nffacl_kernel_info *out);
 
 /* Host-side compilation of a rule set into the device table blob, without a
  * device (tooling / inspection; the engine runs the same compiler).  Call with
@@ -537,7 +562,13 @@ NFFACL_API int nffacl_l2_classify_host(nffacl_l2engine *eng, const uint8_t *h_sl
  * host, uploads the table to hip_devices[0] (the root) and ncclBroadcasts
  * it to the others over xGMI.  The group owns its tables (the rule set may
  * be freed afterwards); a rule reload is a new group.  Devices must be
- * distinct.  NFFACL_ERR_NO_DEVICE without HIP devices. */
+ * distinct.  NFFACL_ERR_NO_DEVICE without HIP devices; NFFACL_ERR_HIP with
+ * the last error "RCCL not available: ..." when librccl cannot be loaded —
+ * RCCL is opened here (dlopen), so nothing else in the library needs it.
+ * Every RCCL call and device switch is checked; a failure inside a group
+ * call closes the group and returns NFFACL_ERR_HIP.  (Groups of more than
+ * one device have run on no multi-GPU node yet: their scatter / gather
+ * parity is unverified on hardware) */
 typedef struct nffacl_group nffacl_group;
 NFFACL_API int nffacl_group_create(const int *hip_devices, int n, const nffacl_rules *rules, nffacl_group **out);
 NFFACL_API int nffacl_group_size(const nffacl_group *g);
@@ -553,6 +584,13 @@ NFFACL_API int nffacl_group_size(const nffacl_group *g);
 NFFACL_API int nffacl_group_classify_device(nffacl_group *g, const uint8_t *d_slots, uint32_t stride, uint64_t n,
                                             uint32_t *d_port, uint64_t *d_permit_bits, void *stream);
 NFFACL_API void nffacl_group_destroy(nffacl_group *g);
+/* The group's shard plan (pure; ABI 7): shard i of n packets over n_devices
+ * devices is [*off, *off + *len) — shards of ceil(ceil(n / N) / 64) * 64
+ * packets in device order, the last ones shorter or empty, *off always a
+ * multiple of 64 (so the shard's permit words start at *off / 64 and no
+ * word straddles two devices).  NFFACL_ERR_INVALID_ARG for N outside 1..64,
+ * i outside 0..N-1, n > 2^48 or NULL outputs. */
+NFFACL_API int nffacl_group_shard(uint64_t n, int n_devices, int i, uint64_t *off, uint64_t *len);
 
 /* ---- misc ------------------------------------------------------------- */
 NFFACL_API const char *nffacl_strerror(int status);

@@ -286,6 +286,9 @@ int engine_shell(int hip_device, nffacl_engine **out) {
         const size_t bytes = size_t(nffacl_engine::kDynStreams) * kDynBlockWords * sizeof(uint32_t);
         e = hipMalloc(reinterpret_cast<void **>(&eng->d_dyn), bytes);
         if (e == hipSuccess) e = hipMemset(eng->d_dyn, 0, bytes);
+        // (the null-stream memset is not ordered before launches on
+        // non-blocking streams — torch's, the group's: complete it here)
+        if (e == hipSuccess) e = hipDeviceSynchronize();
         if (e != hipSuccess) {
             set_last_error(std::string("pull heads: ") + hipGetErrorString(e));
             nffacl_engine_destroy(eng);
@@ -363,6 +366,11 @@ int nffacl_engine_algo(const nffacl_engine *eng) {
     if (!eng) return NFFACL_ERR_INVALID_ARG;
     const TablePtr t = acquire_table(const_cast<nffacl_engine *>(eng));
     return t ? t->meta.algo : NFFACL_ERR_INVALID_ARG;
+}
+
+int nffacl_engine_kernel_info(nffacl_engine *eng, nffacl_kernel_info *out) {
+    if (!eng || !out) return NFFACL_ERR_INVALID_ARG;
+    return slots_kernel_info(eng, out);
 }
 
 int nffacl_engine_table_bytes(const nffacl_engine *eng, uint64_t *bytes) {

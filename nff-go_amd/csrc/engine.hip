@@ -219,8 +219,14 @@ struct BatchSource {
 //    classifying packet coal_packet(l) of its wave's batch; no register
 //    prefetch (it would push the kernel past 64 VGPRs, i.e. below 8 waves per
 //    SIMD) — 32 resident waves per CU keep 128 KiB of loads in flight.
+// (experiment builds: NFFACL_EXP_MAXVGPR caps the slot kernels' VGPRs)
+#ifdef NFFACL_EXP_MAXVGPR
+#define NFFACL_SLOTS_VGPR __attribute__((amdgpu_num_vgpr(NFFACL_EXP_MAXVGPR)))
+#else
+#define NFFACL_SLOTS_VGPR
+#endif
 template <int NS, int TM, int MODE>
-__global__ void __launch_bounds__(1024)
+__global__ void __launch_bounds__(1024) NFFACL_SLOTS_VGPR
 k_indexed_slots(const uint8_t *__restrict__ slots, uint32_t stride, uint64_t n, IndexedArgs a,
                 uint32_t *__restrict__ port_out, uint64_t *__restrict__ permit_out) {
     if (TM != kTabGlobal && TM != kTabFlat && TM != kTabFlat4) stage_table(a);
@@ -640,6 +646,12 @@ static bool table_consistent(const DevTable *t) {
     return m.idx4.entry_dwords == kEnt4Dwords && m.idx6.entry_dwords == kEnt6Dwords;
 }
 
+// Widest table the pipelined walk takes (experiment builds may raise it:
+// make EXTRA=-DNFFACL_PIPE_MAX_NS=8, tools/ns7_hunt.py).
+#ifndef NFFACL_PIPE_MAX_NS
+#define NFFACL_PIPE_MAX_NS 6
+#endif
+
 // Launch shape of an indexed table; Tune overrides (frozen at engine creation).
 static IndexedLaunch indexed_launch(const nffacl_engine *eng, const DevTable *t) {
     const Tune &tu = eng->tune;
@@ -671,7 +683,7 @@ static IndexedLaunch indexed_launch(const nffacl_engine *eng, const DevTable *t)
             L.tm = dev::kTabFlatLdsG;
             L.lds_bytes = lds4;  // > kLdsBytes is refused by the launch check below
         } else if (tu.pipe && (t->meta.flat_uncond || tu.pipe == 2) && lds4 <= kLdsBytes && !tu.rounds &&
-                   ns <= 6) {
+                   ns <= NFFACL_PIPE_MAX_NS) {
             // (NS <= 6: the NS = 7 pipelined kernel misclassified 1-7 of 2^16
             // packets per launch, nondeterministically, under
             // NFFACL_TUNE_FINE_SLOTS=7 — cause open; 7-8 slots, reached only
@@ -820,8 +832,19 @@ int prepare_kernels() {
 }
 
 // The pull heads of launches on `stream` (nullptr: none free, grid stride).
+// A head block is reused by the next launch on the same handle, so the
+// handle must name ONE ordered stream and the launch must run when it is
+// enqueued: hipStreamPerThread names a different stream on every thread, and
+// a launch captured into a graph may be replayed beside another launch on
+// the same stream — both take the grid stride.
 static uint32_t *dyn_heads(nffacl_engine *eng, hipStream_t stream) {
-    if (!eng->d_dyn) return nullptr;
+    if (!eng->d_dyn || stream == hipStreamPerThread) return nullptr;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(stream, &cs) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    if (cs != hipStreamCaptureStatusNone) return nullptr;
     std::lock_guard<std::mutex> g(eng->dyn_mu);
     for (int i = 0; i < eng->dyn_used; ++i)
         if (eng->dyn_stream[i] == stream) return eng->d_dyn + size_t(i) * kDynBlockWords;
@@ -842,6 +865,31 @@ static void dyn_args(nffacl_engine *eng, hipStream_t stream, uint32_t grid, uint
     a.dyn_g = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(tu.dyn_gmax, nb / (waves * tu.dyn_pulls))));
     a.dyn_gmin = std::min<uint32_t>(a.dyn_g, static_cast<uint32_t>(tu.dyn_gmin));
     a.dyn_wpx = static_cast<uint32_t>(std::max<uint64_t>(1, waves * tu.dyn_tail / 16));
+}
+
+// Load mode of a slots launch: long flat walks (kTabFlatLds4U, C5) default
+// to mode 5, the next batch's packets in flight: 0.6278 / 0.6312 vs 0.6340 /
+// 0.6328 ms (profiles/r3_ab/c5_mode5/); everything else to mode 4.
+static int slots_mode(const nffacl_engine *eng, const IndexedLaunch &L, uint32_t stride) {
+    int mode = stride == 64 ? eng->tune.coal : 0;
+    if (stride == 64 && !eng->tune.coal_set && (L.tm == dev::kTabFlatLds4U || L.tm == dev::kTabFlatLdsG)) mode = 5;
+    return mode;
+}
+
+static bool flat_lds_walk(int tm) {
+    return tm == dev::kTabFlatLds || tm == dev::kTabFlatLds4 || tm == dev::kTabFlatLds4U || tm == dev::kTabFlatLdsG ||
+           tm == dev::kTabFlatLdsP;
+}
+
+// Pulled batches (BatchSource): the flat-LDS walks (C5: 0.5111 vs 0.5341 ms
+// alone with pulls of 12-16 batches — 0.5159 / 0.5208 / 0.5247 with at
+// least 8 / 16 / 4 — and +9-13 % instead of +80 % beside busy consumers,
+// profiles/r5_ab/dyn/); not the short per-lane walks (C2 0.316 vs 0.220 ms:
+// its waves pull in lockstep and wait on the heads, and a wave's chunk of
+// consecutive batches spreads its group's loads over 10x the pages of the
+// grid stride: 0.27 ms with one pull per wave; profiles/r5_ab/dyn/).
+static bool slots_pull(const nffacl_engine *eng, const IndexedLaunch &L, int mode) {
+    return mode == 4 && (eng->tune.dyn == 2 || (eng->tune.dyn == 1 && flat_lds_walk(L.tm)));
 }
 
 template <int NS, int TM>
@@ -908,23 +956,8 @@ int launch_slots(nffacl_engine *eng, DevTable *t, const uint8_t *d_slots, uint32
             return NFFACL_ERR_INVALID_ARG;
         }
         const uint32_t grid = grid_for(eng, n, L.block, L.per_cu);
-        // long flat walks (kTabFlatLds4U, C5) default to mode 5, the next
-        // batch's packets in flight: 0.6278 / 0.6312 vs 0.6340 / 0.6328 ms
-        // (profiles/r3_ab/c5_mode5/); everything else to mode 4
-        int mode = stride == 64 ? eng->tune.coal : 0;
-        if (stride == 64 && !eng->tune.coal_set && (L.tm == dev::kTabFlatLds4U || L.tm == dev::kTabFlatLdsG))
-            mode = 5;
-        // pulled batches (BatchSource): the flat-LDS walks (C5: 0.5111 vs
-        // 0.5341 ms alone with pulls of 12-16 batches — 0.5159 / 0.5208 /
-        // 0.5247 with at least 8 / 16 / 4 — and +9-13 % instead of +80 %
-        // beside busy consumers, profiles/r5_ab/dyn/);
-        // not the short per-lane walks (C2 0.316 vs 0.220 ms: its waves pull in
-        // lockstep and wait on the heads, and a wave's chunk of consecutive
-        // batches spreads its group's loads over 10x the pages of the grid
-        // stride: 0.27 ms with one pull per wave; profiles/r5_ab/dyn/)
-        const bool flat = L.tm == dev::kTabFlatLds || L.tm == dev::kTabFlatLds4 || L.tm == dev::kTabFlatLds4U ||
-                          L.tm == dev::kTabFlatLdsG || L.tm == dev::kTabFlatLdsP;
-        if (mode == 4 && (eng->tune.dyn == 2 || (eng->tune.dyn == 1 && flat))) dyn_args(eng, stream, grid, L.block, n, a);
+        const int mode = slots_mode(eng, L, stride);
+        if (slots_pull(eng, L, mode)) dyn_args(eng, stream, grid, L.block, n, a);
         // (the pipelined walk: load mode 4 — mode 6, the next batch's loads
         // issued from inside the walk, spilled and ran 0.64 vs 0.53 ms on C5:
         // NFFACL_TUNE_COAL=6, profiles/r5_ab/)
@@ -978,6 +1011,38 @@ int launch_frames(nffacl_engine *eng, DevTable *t, const uint8_t *d_frames,
     }
     HIP_TRY(hipGetLastError());
     HIP_TRY(t->note_use(stream));
+    return NFFACL_OK;
+}
+
+// The kernel the active table's 64-byte-slot launches take (ABI 7,
+// nffacl_engine_kernel_info): tests assert which walk ran.
+int slots_kernel_info(nffacl_engine *eng, nffacl_kernel_info *out) {
+    const TablePtr t = acquire_table(eng);
+    if (!t) return NFFACL_ERR_INVALID_ARG;
+    *out = nffacl_kernel_info{};
+    if (t->meta.algo == NFFACL_ALGO_LINEAR) {
+        out->walk = NFFACL_WALK_LINEAR;
+        out->block = 256;
+        out->per_cu = 8;
+        return NFFACL_OK;
+    }
+    const IndexedLaunch L = indexed_launch(eng, t.get());
+    switch (L.tm) {
+    case dev::kTabLds: case dev::kTabLdsNP: out->walk = NFFACL_WALK_INDEXED_LDS; break;
+    case dev::kTabSplit: out->walk = NFFACL_WALK_HYBRID_LANE; break;
+    case dev::kTabFlat: case dev::kTabFlat4: out->walk = NFFACL_WALK_FLAT; break;
+    case dev::kTabFlatLds: case dev::kTabFlatLds4: case dev::kTabFlatLds4U: out->walk = NFFACL_WALK_FLAT_LDS; break;
+    case dev::kTabFlatLdsG: out->walk = NFFACL_WALK_FLAT_LDS_GENERIC; break;
+    case dev::kTabFlatLdsP: out->walk = NFFACL_WALK_FLAT_LDS_PIPELINED; break;
+    default: out->walk = NFFACL_WALK_INDEXED_GLOBAL; break;
+    }
+    out->slots = static_cast<uint32_t>(L.ns);
+    out->rounds = L.tm == dev::kTabFlat || L.tm == dev::kTabFlatLds ? 2u : flat_lds_walk(L.tm) || L.tm == dev::kTabFlat4 ? 4u : 0u;
+    out->block = L.block;
+    out->per_cu = L.per_cu;
+    out->lds_bytes = L.lds_bytes;
+    out->load_mode = slots_mode(eng, L, 64);
+    out->pulled = slots_pull(eng, L, out->load_mode) && eng->d_dyn ? 1 : 0;
     return NFFACL_OK;
 }
 

@@ -122,6 +122,8 @@ inline TablePtr acquire_table(nffacl_engine *eng) {
     return eng->active;
 }
 int prepare_kernels();
+// nffacl_engine_kernel_info: the slot kernel of the active table.
+int slots_kernel_info(nffacl_engine *eng, nffacl_kernel_info *out);
 // Both record the launch on `t` (DeviceBlob::note_use) so that a retired
 // table outlives the work enqueued with it.
 int launch_slots(nffacl_engine *eng, DevTable *t, const uint8_t *d_slots, uint32_t stride,

@@ -21,8 +21,11 @@
 //    verdicts (ports and permit words) back into the root's arrays.  All of
 //    it is enqueued on the caller's root stream (and the group's per-device
 //    streams): the call returns at once, like nffacl_classify_device.
+// RCCL is opened (dlopen) by the first nffacl_group_create only, so the
+// library itself does not depend on it: single-GPU users need no RCCL.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
-#include <rccl/rccl.h>
+#include <rccl/rccl.h>  // (types and prototypes only: the calls go through Rccl below)
 #include <sched.h>
 
 #include <algorithm>
@@ -43,24 +46,98 @@ using namespace nffacl;
 
 namespace {
 
-// Current device restored on scope exit (one thread drives every device).
+// Current device restored on scope exit (one thread drives every device);
+// `ok` false (and the last error set) when the switch failed.
 struct OnDevice {
     int prev = 0;
+    bool ok = true;
     explicit OnDevice(int dev) {
         (void)hipGetDevice(&prev);
-        (void)hipSetDevice(dev);
+        const hipError_t e = hipSetDevice(dev);
+        ok = e == hipSuccess;
+        if (!ok) set_last_error(std::string("hipSetDevice(") + std::to_string(dev) + "): " + hipGetErrorString(e));
     }
     ~OnDevice() { (void)hipSetDevice(prev); }
 };
 
-#define NCCL_TRY(expr)                                                                      \
-    do {                                                                                    \
-        const ncclResult_t r_ = (expr);                                                     \
-        if (r_ != ncclSuccess) {                                                            \
-            set_last_error(std::string(#expr) + ": " + ncclGetErrorString(r_));            \
-            return NFFACL_ERR_HIP;                                                          \
-        }                                                                                   \
-    } while (0)
+// The RCCL entry points the group uses, resolved from librccl at run time.
+struct Rccl {
+    decltype(&ncclCommInitAll) comm_init_all = nullptr;
+    decltype(&ncclCommDestroy) comm_destroy = nullptr;
+    decltype(&ncclBroadcast) broadcast = nullptr;
+    decltype(&ncclSend) send = nullptr;
+    decltype(&ncclRecv) recv = nullptr;
+    decltype(&ncclGroupStart) group_start = nullptr;
+    decltype(&ncclGroupEnd) group_end = nullptr;
+    decltype(&ncclGetErrorString) error_string = nullptr;
+    std::string err;  // why loading failed ("" = loaded)
+};
+
+const Rccl &rccl() {
+    static Rccl r;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void *h = nullptr;
+        for (const char *name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1", "/opt/rocm/lib/librccl.so"})
+            if ((h = dlopen(name, RTLD_NOW | RTLD_LOCAL)) != nullptr) break;
+        if (!h) {
+            const char *e = dlerror();
+            r.err = std::string("RCCL not available: ") + (e ? e : "librccl.so not found");
+            return;
+        }
+        auto sym = [&](auto &fp, const char *name) {
+            fp = reinterpret_cast<std::remove_reference_t<decltype(fp)>>(dlsym(h, name));
+            if (!fp && r.err.empty()) r.err = std::string("RCCL symbol missing: ") + name;
+        };
+        sym(r.comm_init_all, "ncclCommInitAll");
+        sym(r.comm_destroy, "ncclCommDestroy");
+        sym(r.broadcast, "ncclBroadcast");
+        sym(r.send, "ncclSend");
+        sym(r.recv, "ncclRecv");
+        sym(r.group_start, "ncclGroupStart");
+        sym(r.group_end, "ncclGroupEnd");
+        sym(r.error_string, "ncclGetErrorString");
+    });
+    return r;
+}
+
+// One RCCL group (ncclGroupStart .. ncclGroupEnd) whose calls are all
+// checked: the first failing call or device switch is remembered, the group
+// is still closed (RCCL requires it), and end() reports the first failure —
+// a call rejected inside the group must not leave a peer waiting on a
+// receive that was never posted without the caller hearing of it.
+struct CheckedGroup {
+    const Rccl &R;
+    const char *what;
+    std::string err;
+    bool open = false;
+    CheckedGroup(const Rccl &r, const char *w) : R(r), what(w) {
+        const ncclResult_t e = R.group_start();
+        if (e != ncclSuccess) err = std::string("ncclGroupStart: ") + R.error_string(e);
+        open = e == ncclSuccess;
+    }
+    bool ok() const { return err.empty(); }
+    void nccl(ncclResult_t e, const char *call) {
+        if (e != ncclSuccess && err.empty()) err = std::string(call) + ": " + R.error_string(e);
+    }
+    void device(int dev) {
+        const hipError_t e = hipSetDevice(dev);
+        if (e != hipSuccess && err.empty()) err = std::string("hipSetDevice: ") + hipGetErrorString(e);
+    }
+    int end() {
+        if (open) {
+            const ncclResult_t e = R.group_end();
+            open = false;
+            if (e != ncclSuccess && err.empty()) err = std::string("ncclGroupEnd: ") + R.error_string(e);
+        }
+        if (err.empty()) return NFFACL_OK;
+        set_last_error(std::string(what) + ": " + err);
+        return NFFACL_ERR_HIP;
+    }
+    ~CheckedGroup() {
+        if (open) (void)R.group_end();
+    }
+};
 
 // CPU -> NUMA node map of this host (sysfs), built once.
 const std::vector<int> &cpu_nodes() {
@@ -130,7 +207,7 @@ void group_release(nffacl_group *g) {
         }
     }
     for (ncclComm_t c : g->comms)
-        if (c) (void)ncclCommDestroy(c);
+        if (c) (void)rccl().comm_destroy(c);
     g->tabs.clear();  // retired stream-ordered through each device's table home
     for (nffacl_engine *e : g->engs)
         if (e) nffacl_engine_destroy(e);
@@ -142,6 +219,7 @@ int ensure_staging(nffacl_group *g, size_t per, uint32_t stride) {
     for (int i = 1; i < g->n; ++i) {
         if (g->cap[i] >= per && g->cap_stride >= stride) continue;
         OnDevice od(g->devs[i]);
+        if (!od.ok) return NFFACL_ERR_HIP;
         HIP_TRY(hipStreamSynchronize(g->streams[i]));  // the previous call's use of the old buffers
         if (g->d_in[i]) (void)hipFree(g->d_in[i]);
         if (g->d_out[i]) (void)hipFree(g->d_out[i]);
@@ -203,6 +281,17 @@ int nffacl_local_device(void) {
     return cached;
 }
 
+int nffacl_group_shard(uint64_t n, int n_devices, int i, uint64_t *off, uint64_t *len) {
+    if (!off || !len || n_devices <= 0 || n_devices > 64 || i < 0 || i >= n_devices || n > (uint64_t(1) << 48))
+        return NFFACL_ERR_INVALID_ARG;
+    // 64-aligned shards (a permit word never straddles two devices); the
+    // root keeps the first, trailing devices may get none (n < 64 (N - 1))
+    const uint64_t per = ((n + uint64_t(n_devices) - 1) / uint64_t(n_devices) + 63) / 64 * 64;
+    *off = std::min<uint64_t>(n, per * uint64_t(i));
+    *len = std::min<uint64_t>(n, per * uint64_t(i + 1)) - *off;
+    return NFFACL_OK;
+}
+
 int nffacl_group_create(const int *hip_devices, int n, const nffacl_rules *rules, nffacl_group **out) {
     if (!out) return NFFACL_ERR_INVALID_ARG;
     *out = nullptr;
@@ -218,6 +307,11 @@ int nffacl_group_create(const int *hip_devices, int n, const nffacl_rules *rules
         for (int j = 0; j < i; ++j)
             if (hip_devices[j] == hip_devices[i]) return NFFACL_ERR_INVALID_ARG;  // one rank per device
     }
+    const Rccl &R = rccl();
+    if (!R.err.empty()) {
+        set_last_error(R.err);
+        return NFFACL_ERR_HIP;
+    }
     nffacl_group *g = new (std::nothrow) nffacl_group();
     if (!g) return NFFACL_ERR_NOMEM;
     g->n = n;
@@ -232,28 +326,26 @@ int nffacl_group_create(const int *hip_devices, int n, const nffacl_rules *rules
         group_release(g);
         return st;
     };
-    int prev = 0;
-    (void)hipGetDevice(&prev);
     for (int i = 0; i < n; ++i) {
         const int st = engine_shell(g->devs[i], &g->engs[i]);
-        if (st != NFFACL_OK) {
-            (void)hipSetDevice(prev);
-            return fail(st);
-        }
+        if (st != NFFACL_OK) return fail(st);
         if (i > 0) {
             OnDevice od(g->devs[i]);
+            if (!od.ok) return fail(NFFACL_ERR_HIP);
             if (hipStreamCreateWithFlags(&g->streams[i], hipStreamNonBlocking) != hipSuccess) {
                 set_last_error("group stream");
                 return fail(NFFACL_ERR_HIP);
             }
         }
     }
-    (void)hipSetDevice(prev);
     g->comms.assign(n, nullptr);
-    if (ncclCommInitAll(g->comms.data(), n, g->devs.data()) != ncclSuccess) {
-        set_last_error("ncclCommInitAll failed");
-        g->comms.clear();
-        return fail(NFFACL_ERR_HIP);
+    {
+        const ncclResult_t e = R.comm_init_all(g->comms.data(), n, g->devs.data());
+        if (e != ncclSuccess) {
+            set_last_error(std::string("ncclCommInitAll: ") + R.error_string(e));
+            g->comms.clear();
+            return fail(NFFACL_ERR_HIP);
+        }
     }
     // compile once on the host; upload to the root, broadcast the image
     std::vector<uint32_t> words;
@@ -262,6 +354,7 @@ int nffacl_group_create(const int *hip_devices, int n, const nffacl_rules *rules
     if (st != NFFACL_OK) return fail(st);
     for (int i = 0; i < n; ++i) {
         OnDevice od(g->devs[i]);
+        if (!od.ok) return fail(NFFACL_ERR_HIP);
         DevTable &t = *g->tabs[i];
         if (i > 0) {
             t.meta = g->tabs[0]->meta;
@@ -275,19 +368,23 @@ int nffacl_group_create(const int *hip_devices, int n, const nffacl_rules *rules
         }
     }
     if (n > 1) {
-        if (ncclGroupStart() != ncclSuccess) return fail(NFFACL_ERR_HIP);
-        for (int i = 0; i < n; ++i) {
-            OnDevice od(g->devs[i]);
-            (void)ncclBroadcast(g->tabs[0]->d_blob, g->tabs[i]->d_blob, words.size(), ncclUint32, 0, g->comms[i],
-                                g->engs[i]->home.stream);
+        int prev = 0;
+        (void)hipGetDevice(&prev);
+        CheckedGroup grp(R, "table broadcast");
+        for (int i = 0; i < n && grp.ok(); ++i) {
+            grp.device(g->devs[i]);
+            if (grp.ok())
+                grp.nccl(R.broadcast(g->tabs[0]->d_blob, g->tabs[i]->d_blob, words.size(), ncclUint32, 0, g->comms[i],
+                                     g->engs[i]->home.stream),
+                         "ncclBroadcast");
         }
-        if (ncclGroupEnd() != ncclSuccess) {
-            set_last_error("ncclBroadcast of the table image failed");
-            return fail(NFFACL_ERR_HIP);
-        }
+        st = grp.end();
+        (void)hipSetDevice(prev);
+        if (st != NFFACL_OK) return fail(st);
     }
     for (int i = 0; i < n; ++i) {
         OnDevice od(g->devs[i]);
+        if (!od.ok) return fail(NFFACL_ERR_HIP);
         if (hipStreamSynchronize(g->engs[i]->home.stream) != hipSuccess) {
             set_last_error("group table broadcast");
             return fail(NFFACL_ERR_HIP);
@@ -302,74 +399,65 @@ int nffacl_group_size(const nffacl_group *g) { return g ? g->n : NFFACL_ERR_INVA
 
 int nffacl_group_classify_device(nffacl_group *g, const uint8_t *d_slots, uint32_t stride, uint64_t n,
                                  uint32_t *d_port, uint64_t *d_permit, void *stream) {
-    if (!g || (n && !d_slots) || stride < 64 || stride % 16 != 0 || (!d_port && !d_permit))
+    if (!g || (n && !d_slots) || stride < 64 || stride % 16 != 0 || (!d_port && !d_permit) || n > (uint64_t(1) << 48))
         return NFFACL_ERR_INVALID_ARG;
     if (n == 0) return NFFACL_OK;
     std::lock_guard<std::mutex> lk(g->mu);
+    const Rccl &R = rccl();
     hipStream_t rs = static_cast<hipStream_t>(stream);
-    // 64-aligned shards (permit words stay whole), the root keeps the first
-    const uint64_t per = ((n + g->n - 1) / g->n + 63) / 64 * 64;
-    auto off_of = [&](int i) { return std::min<uint64_t>(n, per * uint64_t(i)); };
-    auto len_of = [&](int i) { return std::min<uint64_t>(n, per * uint64_t(i + 1)) - off_of(i); };
-    int st = ensure_staging(g, per, stride);
+    std::vector<uint64_t> off(g->n), len(g->n);
+    for (int i = 0; i < g->n; ++i) (void)nffacl_group_shard(n, g->n, i, &off[i], &len[i]);
+    int st = ensure_staging(g, len[0], stride);  // (the root's shard is the largest)
     if (st != NFFACL_OK) return st;
     int prev = 0;
     (void)hipGetDevice(&prev);
     // scatter: the root's sends to every peer in one group
     if (g->n > 1) {
-        NCCL_TRY(ncclGroupStart());
-        for (int i = 1; i < g->n; ++i) {
-            const uint64_t len = len_of(i);
-            if (!len) continue;
-            (void)hipSetDevice(g->devs[0]);
-            (void)ncclSend(d_slots + off_of(i) * stride, len * stride, ncclUint8, i, g->comms[0], rs);
-            (void)hipSetDevice(g->devs[i]);
-            (void)ncclRecv(g->d_in[i], len * stride, ncclUint8, 0, g->comms[i], g->streams[i]);
+        CheckedGroup grp(R, "group scatter");
+        for (int i = 1; i < g->n && grp.ok(); ++i) {
+            if (!len[i]) continue;
+            grp.device(g->devs[0]);
+            if (grp.ok())
+                grp.nccl(R.send(d_slots + off[i] * stride, len[i] * stride, ncclUint8, i, g->comms[0], rs), "ncclSend");
+            grp.device(g->devs[i]);
+            if (grp.ok()) grp.nccl(R.recv(g->d_in[i], len[i] * stride, ncclUint8, 0, g->comms[i], g->streams[i]), "ncclRecv");
         }
-        const ncclResult_t r = ncclGroupEnd();
+        st = grp.end();
         (void)hipSetDevice(prev);
-        if (r != ncclSuccess) {
-            set_last_error(std::string("group scatter: ") + ncclGetErrorString(r));
-            return NFFACL_ERR_HIP;
-        }
+        if (st != NFFACL_OK) return st;
     }
     // every shard on its own device
     for (int i = 0; i < g->n; ++i) {
-        const uint64_t len = len_of(i);
-        if (!len) continue;
+        if (!len[i]) continue;
         OnDevice od(g->devs[i]);
-        st = i == 0 ? launch_slots(g->engs[0], g->tabs[0].get(), d_slots, stride, len, d_port, d_permit, rs)
-                    : launch_slots(g->engs[i], g->tabs[i].get(), g->d_in[i], stride, len, d_port ? g->d_out[i] : nullptr,
+        if (!od.ok) return NFFACL_ERR_HIP;
+        st = i == 0 ? launch_slots(g->engs[0], g->tabs[0].get(), d_slots, stride, len[0], d_port, d_permit, rs)
+                    : launch_slots(g->engs[i], g->tabs[i].get(), g->d_in[i], stride, len[i], d_port ? g->d_out[i] : nullptr,
                                    d_permit ? g->d_perm[i] : nullptr, g->streams[i]);
         if (st != NFFACL_OK) return st;
     }
-    // gather the verdicts back into the root's arrays
+    // gather the verdicts back into the root's arrays (permit words: off / 64, off is 64-aligned)
     if (g->n > 1) {
-        NCCL_TRY(ncclGroupStart());
-        for (int i = 1; i < g->n; ++i) {
-            const uint64_t len = len_of(i);
-            if (!len) continue;
-            const uint64_t off = off_of(i);
+        CheckedGroup grp(R, "group gather");
+        for (int i = 1; i < g->n && grp.ok(); ++i) {
+            if (!len[i]) continue;
             if (d_port) {
-                (void)hipSetDevice(g->devs[i]);
-                (void)ncclSend(g->d_out[i], len, ncclUint32, 0, g->comms[i], g->streams[i]);
-                (void)hipSetDevice(g->devs[0]);
-                (void)ncclRecv(d_port + off, len, ncclUint32, i, g->comms[0], rs);
+                grp.device(g->devs[i]);
+                if (grp.ok()) grp.nccl(R.send(g->d_out[i], len[i], ncclUint32, 0, g->comms[i], g->streams[i]), "ncclSend");
+                grp.device(g->devs[0]);
+                if (grp.ok()) grp.nccl(R.recv(d_port + off[i], len[i], ncclUint32, i, g->comms[0], rs), "ncclRecv");
             }
             if (d_permit) {
-                const uint64_t words = (len + 63) / 64;
-                (void)hipSetDevice(g->devs[i]);
-                (void)ncclSend(g->d_perm[i], words, ncclUint64, 0, g->comms[i], g->streams[i]);
-                (void)hipSetDevice(g->devs[0]);
-                (void)ncclRecv(d_permit + off / 64, words, ncclUint64, i, g->comms[0], rs);
+                const uint64_t words = (len[i] + 63) / 64;
+                grp.device(g->devs[i]);
+                if (grp.ok()) grp.nccl(R.send(g->d_perm[i], words, ncclUint64, 0, g->comms[i], g->streams[i]), "ncclSend");
+                grp.device(g->devs[0]);
+                if (grp.ok()) grp.nccl(R.recv(d_permit + off[i] / 64, words, ncclUint64, i, g->comms[0], rs), "ncclRecv");
             }
         }
-        const ncclResult_t r = ncclGroupEnd();
+        st = grp.end();
         (void)hipSetDevice(prev);
-        if (r != ncclSuccess) {
-            set_last_error(std::string("group gather: ") + ncclGetErrorString(r));
-            return NFFACL_ERR_HIP;
-        }
+        if (st != NFFACL_OK) return st;
     }
     return NFFACL_OK;
 }

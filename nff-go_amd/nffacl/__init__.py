@@ -156,6 +156,19 @@ _group_create = _sig("nffacl_group_create", _i, _vp, _i, _vp, _pp)
 _group_size = _sig("nffacl_group_size", _i, _vp)
 _group_classify = _sig("nffacl_group_classify_device", _i, _vp, _vp, _u32, ctypes.c_uint64, _vp, _vp, _vp)
 _group_destroy = _sig("nffacl_group_destroy", None, _vp)
+_group_shard = _sig("nffacl_group_shard", _i, _u64, _i, _i, ctypes.POINTER(_u64), ctypes.POINTER(_u64))
+
+
+class KernelInfo(ctypes.Structure):
+    """nffacl_kernel_info (ABI 7): the kernel an engine's slot launches take."""
+    _fields_ = [("walk", ctypes.c_int32), ("slots", ctypes.c_uint32), ("rounds", ctypes.c_uint32),
+                ("block", ctypes.c_uint32), ("per_cu", ctypes.c_uint32), ("load_mode", ctypes.c_int32),
+                ("pulled", ctypes.c_uint32), ("reserved", ctypes.c_uint32), ("lds_bytes", ctypes.c_uint64)]
+
+
+WALK_LINEAR, WALK_INDEXED_GLOBAL, WALK_INDEXED_LDS, WALK_HYBRID_LANE = 0, 1, 2, 3
+WALK_FLAT, WALK_FLAT_LDS, WALK_FLAT_LDS_GENERIC, WALK_FLAT_LDS_PIPELINED = 4, 5, 6, 7
+_kernel_info = _sig("nffacl_engine_kernel_info", _i, _vp, ctypes.POINTER(KernelInfo))
 _device_numa_node = _sig("nffacl_device_numa_node", _i, _i)
 _service_create = _sig("nffacl_service_create", _i, _i, _u32, _u32, _pp)
 _service_classify = _sig("nffacl_service_classify", _i, _vp, _vp, _vp, _u32, _u32, ctypes.POINTER(_u32))
@@ -190,7 +203,7 @@ EXPORTED_SYMBOLS = [
     "nffacl_rules_prepare", "nffacl_service_create", "nffacl_service_classify", "nffacl_service_get_stats",
     "nffacl_service_destroy", "nffacl_service_create_burst", "nffacl_service_classify_burst",
     "nffacl_service_pause", "nffacl_pick_device", "nffacl_group_create", "nffacl_group_size",
-    "nffacl_group_classify_device", "nffacl_group_destroy",
+    "nffacl_group_classify_device", "nffacl_group_destroy", "nffacl_group_shard", "nffacl_engine_kernel_info",
 ]
 
 
@@ -211,6 +224,15 @@ def pick_device(cpu: int, cpu_node, dev_node) -> int:
     dn = np.ascontiguousarray(dev_node, np.int32)
     return _pick_device(cpu, cn.ctypes.data if len(cn) else None, len(cn), dn.ctypes.data if len(dn) else None,
                         len(dn))
+
+
+def group_shard(n: int, n_devices: int, i: int):
+    """nffacl_group_shard: (offset, length) of device i's shard of n packets."""
+    off, ln = _u64(), _u64()
+    st = _group_shard(n, n_devices, i, ctypes.byref(off), ctypes.byref(ln))
+    if st != OK:
+        _raise(st, "nffacl_group_shard")
+    return off.value, ln.value
 
 
 class Group:
@@ -426,6 +448,14 @@ class Engine:
         if st != OK:
             _raise(st, "nffacl_engine_table_bytes")
         return b.value
+
+    def kernel_info(self) -> KernelInfo:
+        """nffacl_engine_kernel_info: the kernel the active table's slot launches take."""
+        k = KernelInfo()
+        st = _kernel_info(self._h, ctypes.byref(k))
+        if st != OK:
+            _raise(st, "nffacl_engine_kernel_info")
+        return k
 
     def swap_rules(self, rules: L3Rules):
         st = _engine_swap(self._h, rules.handle)

@@ -39,8 +39,9 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    # 3: generalized slots in nffacl_table_info; 5: burst service; 6: device groups, nffacl_pick_device
-    assert nffacl.abi_version() == 6
+    # 3: generalized slots in nffacl_table_info; 5: burst service; 6: device groups, nffacl_pick_device;
+    # 7: nffacl_group_shard, nffacl_engine_kernel_info
+    assert nffacl.abi_version() == 7
 
 
 def test_exports_are_c_linkage_only():
@@ -122,3 +123,48 @@ def test_group_without_device_reports_no_device():
     with pytest.raises(nffacl.NFError) as e:
         nffacl.Group([], rules)
     assert e.value.status == nffacl.ERR_INVALID_ARG
+
+
+@pytest.mark.parametrize("ndev", range(1, 9))
+def test_group_shard_plan(ndev):
+    """the device group's shard plan (group.cpp, the
+    pure nffacl_group_shard) for N = 1..8 devices — empty batches, batches
+    smaller than 64 N (trailing devices get nothing), ragged tails, and the
+    permit words each shard's verdicts go back to: the shards tile [0, n) in
+    device order, every offset is a multiple of 64, every shard is at most
+    ceil(ceil(n / N) / 64) * 64 packets, and the shards' permit words
+    [off / 64, off / 64 + ceil(len / 64)) tile the batch's ceil(n / 64) words
+    with no word shared by two devices."""
+    sizes = {0, 1, 37, 63, 64, 65, 64 * ndev - 1, 64 * ndev, 64 * ndev + 1, 64 * ndev * 3 + 17, 1000003,
+             (1 << 20) + 37, 1 << 24}
+    for n in sorted(sizes):
+        per = ((n + ndev - 1) // ndev + 63) // 64 * 64
+        pos, words = 0, 0
+        for i in range(ndev):
+            off, ln = nffacl.group_shard(n, ndev, i)
+            assert off == min(n, pos) and off % 64 == 0 or (ln == 0 and off == n), (n, i, off, ln)
+            assert ln <= per
+            if ln:
+                assert off == pos
+                assert off // 64 == words  # the shard's first permit word follows the previous shard's last
+                words += (ln + 63) // 64
+                assert ln == per or off + ln == n  # only the last non-empty shard is short
+            pos += ln
+        assert pos == n and words == (n + 63) // 64
+        # the root keeps the first (largest) shard: the staging on devices 1.. never needs more
+        assert nffacl.group_shard(n, ndev, 0)[1] == min(n, per)
+
+
+def test_group_shard_rejects_bad_arguments():
+    for args in ((10, 0, 0), (10, 65, 0), (10, 2, 2), (10, 2, -1), ((1 << 48) + 1, 2, 0)):
+        with pytest.raises(nffacl.NFError) as e:
+            nffacl.group_shard(*args)
+        assert e.value.status == nffacl.ERR_INVALID_ARG
+
+
+def test_library_needs_no_rccl():
+    """RCCL is dlopen'ed by nffacl_group_create only, so
+    single-GPU users need no RCCL: the library has no link dependency on it."""
+    out = subprocess.run(["readelf", "-d", str(nffacl.LIB_PATH)], check=True, capture_output=True, text=True).stdout
+    needed = re.findall(r"\(NEEDED\).*\[(.*)\]", out)
+    assert needed and not any("rccl" in x for x in needed), needed

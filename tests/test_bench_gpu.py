@@ -55,6 +55,12 @@ def test_bench_n1_with_extra_configs(gpu_available):
     # past the first (76.185 B for C3's IMIX mix)
     assert 76.0 < d["configs"]["c3"]["config"]["algorithmic_bytes_per_packet"] < 76.5
     assert d["configs"]["c5"]["config"]["rules_ip4"] + d["configs"]["c5"]["config"]["rules_ip6"] == 100000
+    # the C-ABI device group over the same batch: one
+    # device = no collective, the Engine's kernel; bit-exact vs the Engine
+    grp = d["device_group"]
+    assert grp["bit_exact_vs_engine"] and grp["curve"][0]["devices"] == 1
+    assert 0.5 < grp["curve"][0]["vs_engine"] < 2.0, grp
+    assert d["summary"]["device_group"][0]["devices"] == 1
 
 
 def test_bench_two_ranks_one_gpu_scatter(gpu_available):
