@@ -717,26 +717,37 @@ __device__ __forceinline__ void stage_table(const IndexedArgs &a) {
 
 // ---- HYBRID (table.hpp "hybrid table") --------------------------------------
 
-// Top-L-bits mask of a big-endian word, L in 0..32 (one 64-bit shift).
-__device__ __forceinline__ uint32_t prefix_mask(uint32_t L) {
-    return static_cast<uint32_t>(0xFFFFFFFF00000000ull >> L);
-}
-
 // 12-byte pieces of the exact flat-form entries (table.hpp): an IPv4 entry
 // is two (the compiler issues dwordx4 + dwordx2), an IPv6 entry four.
 typedef uint32_t u32x3 __attribute__((ext_vector_type(3), aligned(4)));
 
 __device__ __forceinline__ u32x3 ld3(const uint32_t *__restrict__ p) { return *reinterpret_cast<const u32x3 *>(p); }
 
-// Mismatch bits of an exact entry's first six words (both families): top
-// address words under their prefix lengths (IPv6: capped at 32), protocol,
-// ports — acl.go:526-539 / 546-557 for IPv4 completely, for IPv6 up to the
-// low address words.  ks/kd: big-endian src/dst (top) words.
-__device__ __forceinline__ uint32_t hyb_miss(const u32x3 &A, const u32x3 &B, uint32_t ks, uint32_t kd, uint32_t proto,
-                                             uint32_t ports) {
-    const uint32_t sl = min(B.z & 0xFFu, 32u), dl = min((B.z >> 8) & 0xFFu, 32u);
+// Position of the first set bit from the top (v_ffbh_u32), 0xFFFFFFFF for 0
+// — defined here for 0, unlike __builtin_clz (hence the one-line asm).
+__device__ __forceinline__ uint32_t ffbh_raw(uint32_t x) {
+    uint32_t r;
+    asm("v_ffbh_u32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+
+// Does an exact entry's first six words (both families) reject the packet?
+// Top address words under their prefix lengths (IPv6: the top word, any
+// length), protocol, ports — acl.go:526-539 / 546-557 for IPv4 completely,
+// for IPv6 up to the low address words.  ks/kd: big-endian src/dst (top)
+// words.  An address word x = key ^ rule misses its prefix of length L iff
+// its first differing bit lies above L: ffbh(x) < L (x = 0: 0xFFFFFFFF, no
+// miss at any L; L >= 32 with x != 0: a miss), one compare, no mask.
+// (Round 6: the masks were 0xFFFFFFFF00000000 >> L, one v_lshrrev_b64 each;
+// a 64-bit instruction whose 32-bit operand is the allocation's last VGPR
+// reads the next wave's v0 on MI355X — the NS = 7 pipelined walk's wrong
+// verdicts, DESIGN.md §4.3 — so no kernel shifts by a variable 64 bits here.)
+__device__ __forceinline__ bool hyb_miss(const u32x3 &A, const u32x3 &B, uint32_t ks, uint32_t kd, uint32_t proto,
+                                         uint32_t ports) {
+    const uint32_t sl = B.z & 0xFFu, dl = (B.z >> 8) & 0xFFu;
     const uint32_t pm = ((proto ^ A.z) & 0xFFu) & (0u - ((A.z >> 8) & 1u));
-    return ((ks ^ A.x) & prefix_mask(sl)) | ((kd ^ A.y) & prefix_mask(dl)) | pm | port_miss(ports, B.x, B.y);
+    const bool ms = ffbh_raw(ks ^ A.x) < sl, md = ffbh_raw(kd ^ A.y) < dl;
+    return ms || md || (pm | port_miss(ports, B.x, B.y)) != 0u;
 }
 
 // IPv6 address words 1..3 of an exact entry (C = src1 src2 src3, D = dst1
@@ -749,12 +760,12 @@ __device__ __forceinline__ uint32_t first_diff96(uint32_t x1, uint32_t x2, uint3
     return x1 != 0u ? p1 : x2 != 0u ? p2 : p3;
 }
 
-__device__ __forceinline__ uint32_t hyb_miss6(const u32x3 &C, const u32x3 &D, uint32_t lens, const uint32_t (&s)[4],
-                                              const uint32_t (&t)[4]) {
+__device__ __forceinline__ bool hyb_miss6(const u32x3 &C, const u32x3 &D, uint32_t lens, const uint32_t (&s)[4],
+                                          const uint32_t (&t)[4]) {
     const uint32_t sl = lens & 0xFFu, dl = (lens >> 8) & 0xFFu;
     const uint32_t ps = 32u + first_diff96(s[1] ^ C.x, s[2] ^ C.y, s[3] ^ C.z);
     const uint32_t pd = 32u + first_diff96(t[1] ^ D.x, t[2] ^ D.y, t[3] ^ D.z);
-    return (ps < sl ? 1u : 0u) | (pd < dl ? 1u : 0u);
+    return ps < sl || pd < dl;
 }
 
 // ---- FLAT: a wave's candidates, 64 at a time --------------------------------
@@ -1049,7 +1060,7 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
             const uint32_t o = owner[j];
             const uint32_t oks = bperm(ks, o), okd = bperm(kd, o);
             const uint32_t opt = bperm(f.ports, o);
-            pass[j] = valid[j] && hyb_miss(A[j], B[j], oks, okd, oproto[j], opt) == 0u;
+            pass[j] = valid[j] && !hyb_miss(A[j], B[j], oks, okd, oproto[j], opt);
             idx[j] = A[j].z >> kEntIndexShift;
             any6 |= pass[j] && six[j];
         }
@@ -1069,7 +1080,7 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
                         os[q] = bperm(sb[q], owner[j]);
                         ot[q] = bperm(tb[q], owner[j]);
                     }
-                    if (pass[j] && six[j]) pass[j] = hyb_miss6(C[j], D[j], B[j].z, os, ot) == 0u;
+                    if (pass[j] && six[j]) pass[j] = !hyb_miss6(C[j], D[j], B[j].z, os, ot);
                 }
             }
         }
@@ -1109,7 +1120,7 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
             const uint32_t ri = RA.z >> kEntIndexShift;
             const bool want = in_fam && ri < uint32_t(best >> 32);
             if (!ballot(want)) break;  // residual list ascends too
-            bool ok = want && hyb_miss(RA, RB, ks, kd, f.proto, f.ports) == 0u;
+            bool ok = want && !hyb_miss(RA, RB, ks, kd, f.proto, f.ports);
             if (fam && ballot(ok)) {
                 uint32_t sb[4] = {0, 0, 0, 0}, tb[4] = {0, 0, 0, 0};
 #pragma unroll
@@ -1117,7 +1128,7 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
                     sb[q] = __builtin_bswap32(f.s[q]);
                     tb[q] = __builtin_bswap32(f.t[q]);
                 }
-                if (ok) ok = hyb_miss6(g3(e + 6), g3(e + 9), RB.z, sb, tb) == 0u;
+                if (ok) ok = !hyb_miss6(g3(e + 6), g3(e + 9), RB.z, sb, tb);
             }
             best = ok ? (uint64_t(ri) << 32 | (RB.z >> kHybOutShift)) : best;
         }
@@ -1368,7 +1379,7 @@ __device__ __forceinline__ uint32_t classify_flat_pipe(const IndexedArgs &a, con
             const uint32_t o = mk[j] >> 19;
             const uint32_t oks = bperm(ks, o), okd = bperm(kd, o), opt = bperm(f.ports, o);
             const bool valid = w + 64u * j + lane < T4;
-            const bool pass = valid & (hyb_miss(A[j], B[j], oks, okd, mk[j] & 0xFFu, opt) == 0u);
+            const bool pass = valid & !hyb_miss(A[j], B[j], oks, okd, mk[j] & 0xFFu, opt);
             post(pass, o, A[j], B[j]);
         }
     };
@@ -1400,10 +1411,11 @@ __device__ __forceinline__ uint32_t classify_flat_pipe(const IndexedArgs &a, con
                 ot[q] = bperm(__builtin_bswap32(f.t[q]), o);
             }
             const bool valid = w6 + lane < T6;
-            // (one combined mismatch word: no short-circuit branch)
-            const uint32_t miss6 = hyb_miss(A6[0], B6[0], oks, okd, mk6[0] & 0xFFu, opt) |
-                                   hyb_miss6(C6, D6, B6[0].z, os, ot);
-            const bool pass6 = valid && miss6 == 0u;
+            // (one combined miss: no short-circuit branch)
+            const bool m4 = hyb_miss(A6[0], B6[0], oks, okd, mk6[0] & 0xFFu, opt);
+            const bool m6 = hyb_miss6(C6, D6, B6[0].z, os, ot);
+            const bool miss6 = m4 || m6;
+            const bool pass6 = valid & !miss6;
             post(pass6, o, A6[0], B6[0]);
         }
         if constexpr (R1 > 0) {
@@ -1451,7 +1463,7 @@ __device__ __forceinline__ uint32_t classify_flat_pipe(const IndexedArgs &a, con
             const uint32_t ri = RA.z >> kEntIndexShift;
             const bool want = in_fam && ri < uint32_t(best >> 32);
             if (!ballot(want)) break;  // residual list ascends too
-            bool ok = want && hyb_miss(RA, RB, ks, kd, f.proto, f.ports) == 0u;
+            bool ok = want && !hyb_miss(RA, RB, ks, kd, f.proto, f.ports);
             if (fam && ballot(ok)) {
                 uint32_t sb[4] = {0, 0, 0, 0}, tb[4] = {0, 0, 0, 0};
 #pragma unroll
@@ -1459,7 +1471,7 @@ __device__ __forceinline__ uint32_t classify_flat_pipe(const IndexedArgs &a, con
                     sb[q] = __builtin_bswap32(f.s[q]);
                     tb[q] = __builtin_bswap32(f.t[q]);
                 }
-                if (ok) ok = hyb_miss6(ld3(e + 6), ld3(e + 9), RB.z, sb, tb) == 0u;
+                if (ok) ok = !hyb_miss6(ld3(e + 6), ld3(e + 9), RB.z, sb, tb);
             }
             best = ok ? (uint64_t(ri) << 32 | (RB.z >> kHybOutShift)) : best;
         }
