@@ -43,11 +43,22 @@ using Clock = std::chrono::steady_clock;
 
 namespace {
 
-// Tickets this thread has submitted and not collected, per batcher id (the
-// back-pressure bound in submit_impl).
-thread_local std::unordered_map<uint64_t, int64_t> t_own_tickets;
+// This thread's outstanding-ticket counter per batcher id (the counters
+// live in the batcher, nffacl_batcher::owners; the back-pressure bound in
+// submit_impl).  A ticket's burst remembers its counter, so a ticket
+// collected on another thread still decrements its submitter's count.
+thread_local std::unordered_map<uint64_t, std::atomic<int64_t> *> t_own_tickets;
 std::atomic<uint64_t> g_batcher_ids{1};
-constexpr std::chrono::milliseconds kSubmitForeignBound{30000};
+
+// This thread's counter in `b` (under b->mu).
+std::atomic<int64_t> *own_counter(nffacl_batcher *b) {
+    auto it = t_own_tickets.find(b->id);
+    if (it != t_own_tickets.end()) return it->second;
+    b->owners.emplace_back(new std::atomic<int64_t>(0));
+    std::atomic<int64_t> *c = b->owners.back().get();
+    t_own_tickets.emplace(b->id, c);
+    return c;
+}
 
 
 // Mapped (device-addressable) and coherent (fine-grained): the GPU reads the
@@ -254,14 +265,23 @@ int create_impl(nffacl_engine *eng, bool own, uint32_t stride, uint32_t max_batc
             return fail(NFFACL_ERR_INVALID_ARG);
         }
         if (set) b->submit_bound = std::chrono::milliseconds(v);
+        if (!env_knob("NFFACL_TUNE_BATCH_FOREIGN_MS", 1, 600000, v, set, err)) {
+            set_last_error(err);
+            return fail(NFFACL_ERR_INVALID_ARG);
+        }
+        if (set) b->foreign_bound = std::chrono::milliseconds(v);
     }
     b->bufs.reset(new (std::nothrow) BatchBuf[nbuf]);
     if (!b->bufs) return fail(NFFACL_ERR_NOMEM);
     for (uint32_t i = 0; i < nbuf; ++i) {
         BatchBuf &x = b->bufs[i];
         x.claimed.reset(new (std::nothrow) std::atomic<uint64_t>[max_batch]);
-        if (!x.claimed) return fail(NFFACL_ERR_NOMEM);
-        for (uint32_t k = 0; k < max_batch; ++k) x.claimed[k].store(0, std::memory_order_relaxed);
+        x.owner.reset(new (std::nothrow) std::atomic<int64_t> *[max_batch]);
+        if (!x.claimed || !x.owner) return fail(NFFACL_ERR_NOMEM);
+        for (uint32_t k = 0; k < max_batch; ++k) {
+            x.claimed[k].store(0, std::memory_order_relaxed);
+            x.owner[k] = nullptr;
+        }
         hipError_t e = hipHostMalloc(reinterpret_cast<void **>(&x.h_slots), size_t(max_batch) * stride, kHostFlags);
         if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&x.h_port), size_t(max_batch) * 4, kHostFlags);
         if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void **>(&x.d_slots), x.h_slots, 0);
@@ -311,13 +331,11 @@ int submit_impl(nffacl_batcher *b, DevTable *table, const uint8_t *const *frames
             // for) no amount of waiting may free one, so that wait is bounded
             // by submit_bound.  A caller holding no ticket waits for the
             // other threads' batches (a GPU shared with resident consumers,
-            // a first launch) up to kSubmitForeignBound.
+            // a first launch) up to foreign_bound.
             const auto now = Clock::now();
             if (first_wait == Clock::time_point{}) first_wait = now;
-            const auto own = t_own_tickets.find(b->id);
-            const bool self = own != t_own_tickets.end() && own->second > 0;
-            const auto give_up = first_wait + (self ? std::chrono::duration_cast<std::chrono::milliseconds>(b->submit_bound)
-                                                    : std::max(b->submit_bound, kSubmitForeignBound));
+            const bool self = own_counter(b)->load(std::memory_order_acquire) > 0;
+            const auto give_up = first_wait + (self ? b->submit_bound : b->foreign_bound);
             if (now >= give_up) {
                 set_last_error(self ? "batcher submit: every buffer holds bursts not yet waited for (this thread's own)"
                                     : "batcher submit: no buffer freed within the bound");
@@ -338,6 +356,8 @@ int submit_impl(nffacl_batcher *b, DevTable *table, const uint8_t *const *frames
         x = &cur;
         off = cur.count;
         burst = cur.bursts++;
+        cur.owner[burst] = own_counter(b);
+        cur.owner[burst]->fetch_add(1, std::memory_order_acq_rel);
         if (off == 0) cur.opened = Clock::now();
         cur.count += n;
         cur.readers.fetch_add(1, std::memory_order_relaxed);
@@ -355,7 +375,6 @@ int submit_impl(nffacl_batcher *b, DevTable *table, const uint8_t *const *frames
         if (len < b->stride) std::memset(dst + len, 0, b->stride - len);
     }
     x->written.fetch_add(n, std::memory_order_release);
-    ++t_own_tickets[b->id];
     return NFFACL_OK;
 }
 
@@ -402,10 +421,7 @@ int wait_impl(nffacl_batcher *b, const nffacl_ticket *t, uint32_t *ports, uint64
     if (x.seq.load(std::memory_order_acquire) != t->seq) return NFFACL_ERR_INVALID_ARG;
     const int st = x.status.load(std::memory_order_relaxed);
     if (ports && st == NFFACL_OK) std::memcpy(ports, x.h_port + t->off, size_t(t->n) * 4);
-    {
-        auto own = t_own_tickets.find(b->id);  // (collected on another thread than its submit: no entry)
-        if (own != t_own_tickets.end() && own->second > 0 && --own->second == 0) t_own_tickets.erase(own);
-    }
+    if (std::atomic<int64_t> *own = x.owner[t->reserved]) own->fetch_sub(1, std::memory_order_acq_rel);  // its submitter's
     if (x.readers.fetch_sub(1, std::memory_order_acq_rel) == 1) {  // the batch's last burst
         std::lock_guard<std::mutex> g(b->mu);
         if (x.state == BatchBuf::DONE) free_buffer(b, x);  // else the completer frees it once it marks it DONE

@@ -61,6 +61,9 @@ struct BatchBuf {
     // second wait on the same ticket is rejected instead of freeing the
     // buffer twice)
     std::unique_ptr<std::atomic<uint64_t>[]> claimed;
+    // per burst number: the submitting thread's outstanding-ticket counter
+    // (nffacl_batcher::owners), decremented by whichever thread collects it
+    std::unique_ptr<std::atomic<int64_t> *[]> owner;
     std::chrono::steady_clock::time_point opened;
     uint8_t *h_slots = nullptr;   // mapped pinned host memory
     uint32_t *h_port = nullptr;
@@ -81,7 +84,14 @@ struct nffacl_batcher {
     // longest back-pressure wait of a submit before NFFACL_ERR_TIMEOUT
     // (NFFACL_TUNE_BATCH_SUBMIT_MS, tests)
     std::chrono::milliseconds submit_bound{1000};
+    // the same for a caller holding no uncollected ticket, who waits on other
+    // threads' batches (NFFACL_TUNE_BATCH_FOREIGN_MS)
+    std::chrono::milliseconds foreign_bound{30000};
     uint64_t id = 0;  // process-unique (this thread's own tickets, batcher.cpp)
+    // one outstanding-ticket counter per submitting thread, owned here (a
+    // ticket may be collected on another thread, or after its submitter
+    // exited); under `mu`
+    std::vector<std::unique_ptr<std::atomic<int64_t>>> owners;
     uint32_t nbuf = 0;
     std::unique_ptr<nffacl::BatchBuf[]> bufs;
 

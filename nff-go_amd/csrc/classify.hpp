@@ -983,7 +983,10 @@ __device__ __forceinline__ uint32_t classify_flat(const IndexedArgs &a, const Fi
                     // entry address is then one multiply-shift-add away
                     const uint32_t w = v6 ? kHybEnt6Dwords : kHybEnt4Dwords;
                     const uint32_t fb = v6 ? a.f6.off_ent_base : a.f4.off_ent_base;
-                    W.delta[pos] = ((fb + (st[s] - so) * w) << 2) | (v6 ? 1u : 0u);
+                    // (signed 24-bit multiply, full rate: |st - so| < 2^23,
+                    // table_consistent; a 32-bit v_mul_lo_u32 is quarter rate)
+                    W.delta[pos] = ((fb + static_cast<uint32_t>(__mul24(static_cast<int>(st[s] - so), static_cast<int>(w))))
+                                    << 2) | (v6 ? 1u : 0u);
                 } else {
                     W.delta[pos] = ((st[s] - so) << 1) | (v6 ? 1u : 0u);
                 }
@@ -1318,7 +1321,10 @@ __device__ __forceinline__ uint32_t classify_flat_pipe(const IndexedArgs &a, con
                 if (ln[s] != 0u && so < w + 64u * RR && so + ln[s] > w) {
                     const uint32_t pos = so > w ? so - w : 0u;
                     W.mark[pos] = (lane << 19 | static_cast<uint32_t>(s) << 16 | pos << 8 | (f.proto & 0xFFu)) + 1u;
-                    W.delta[pos] = (fb + (st[s] - so) * ew) << 2;
+                    // (signed 24-bit multiply, full rate: |st - so| < 2^23,
+                    // table_consistent; v_mul_lo_u32 is quarter rate)
+                    W.delta[pos] = (fb + static_cast<uint32_t>(__mul24(static_cast<int>(st[s] - so), static_cast<int>(ew))))
+                                   << 2;
                 }
                 so += ln[s];
             }

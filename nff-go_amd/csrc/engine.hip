@@ -630,9 +630,10 @@ struct IndexedLaunch {
 static bool table_consistent(const DevTable *t) {
     const CompiledTable &m = t->meta;
     const size_t dw = m.blob.size();
-    // entry numbers (and list offsets) stay below 2^24: the kernels scale
-    // them with 24-bit multiplies (classify.hpp times_ew, classify_flat)
-    if (dw / kHybEnt4Dwords >= (size_t(1) << 24)) return false;
+    // entry numbers (and list offsets) stay below 2^23: the kernels scale
+    // them with 24-bit multiplies (classify.hpp times_ew, classify_flat;
+    // the window deltas multiply entry - candidate numbers as signed 24-bit)
+    if (dw / kHybEnt4Dwords >= (size_t(1) << 23)) return false;
     if (m.algo == NFFACL_ALGO_HYBRID && (m.lds_dwords == 0 || m.idx4.entry_dwords == kHybEnt4Dwords))
         return m.idx4.entry_dwords == kHybEnt4Dwords && m.idx6.entry_dwords == kHybEnt6Dwords &&
                m.off_rec4 <= dw && m.off_rec6 <= dw &&

@@ -252,6 +252,64 @@ def test_unwaited_tickets_bound_submit(torch_cuda, workload, monkeypatch):
 
 
 @pytest.mark.gpu
+def test_tickets_collected_on_another_thread(torch_cuda, workload, monkeypatch):
+    """a ticket collected on another thread than its
+    submit still counts down its SUBMITTER's outstanding tickets (the counter
+    rides with the burst), so the submitter is not taken for the holder of
+    buffers it no longer holds: thread A's bursts are collected by thread B;
+    thread C then fills every buffer and collects only after 0.6 s; A's next
+    submit waits for C's buffers under the foreign bound
+    (NFFACL_TUNE_BATCH_FOREIGN_MS, 3 s here) instead of failing after its own
+    200 ms bound, and every verdict is exact."""
+    import threading
+    import time
+    g, ptrs, lens, want = _c2_ptrs(workload)
+    eng = nffacl.Engine(nffacl.L3Rules.parse_text(g.text))
+    nbuf = 3
+    monkeypatch.setenv("NFFACL_TUNE_BATCH_SUBMIT_MS", "200")
+    monkeypatch.setenv("NFFACL_TUNE_BATCH_FOREIGN_MS", "3000")
+    b = nffacl.Batcher(eng, stride=80, max_batch=1024, max_delay_us=100, nbuf=nbuf)
+    monkeypatch.delenv("NFFACL_TUNE_BATCH_SUBMIT_MS")
+    monkeypatch.delenv("NFFACL_TUNE_BATCH_FOREIGN_MS")
+    burst = lambda i: (ptrs[32 * i:32 * (i + 1)], lens[32 * i:32 * (i + 1)])  # noqa: E731
+    try:
+        ts = []
+        for i in range(nbuf):  # thread A (this one)
+            ts.append(b.submit(*burst(i)))
+            time.sleep(0.002)
+        got = {}
+
+        def collect(tickets, first, delay=0.0):
+            time.sleep(delay)
+            for k, t in enumerate(tickets):
+                got[first + k] = b.wait(t, timeout_us=2_000_000)
+        tb = threading.Thread(target=collect, args=(ts, 0))  # thread B collects A's tickets
+        tb.start()
+        tb.join()
+        tc_tickets = []
+
+        def fill_then_collect():  # thread C
+            for i in range(nbuf, 2 * nbuf):
+                tc_tickets.append(b.submit(*burst(i)))
+                time.sleep(0.002)
+            collect(tc_tickets, nbuf, delay=0.6)
+        tc = threading.Thread(target=fill_then_collect)
+        tc.start()
+        time.sleep(0.1)  # C holds every buffer now
+        t0 = time.monotonic()
+        t = b.submit(*burst(2 * nbuf))  # A: not its own tickets -> waits for C's
+        waited = time.monotonic() - t0
+        np.testing.assert_array_equal(b.wait(t, timeout_us=2_000_000), want[32 * 2 * nbuf:32 * (2 * nbuf + 1)])
+        tc.join()
+        assert waited > 0.3, waited
+        for i in range(2 * nbuf):
+            np.testing.assert_array_equal(got[i], want[32 * i:32 * (i + 1)])
+    finally:
+        b.close()
+        eng.close()
+
+
+@pytest.mark.gpu
 def test_ticket_keeps_rules_alive(torch_cuda, workload):
     """A rule set made inline and dropped by the caller right after submit
     (b.submit(..., rules=L3Rules.parse_text(t))) stays alive until the
