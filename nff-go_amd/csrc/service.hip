@@ -82,6 +82,8 @@ struct SvcArgs {
     uint64_t life_ticks;    // leave after this long in any case
     uint32_t idle_naps;     // burst consumer: s_sleep(8) (~0.2 us) naps of an idle wave between bell reads
     uint32_t post_naps;     // burst consumer: s_sleep(2) (~50 ns) naps after an answer, before the next poll
+                            // (the starting value when nap_adapt)
+    uint32_t nap_adapt;     // burst consumer: each wave adapts its nap to its caller's turnaround
                             // (NFFACL_TUNE_SVC_POST_NAPS, default 12)
                             // (NFFACL_TUNE_SVC_IDLE_NAPS)
     uint32_t full_poll;     // burst consumer: hot waves read the whole mailbox every pass (default; 0: the
@@ -381,6 +383,9 @@ __global__ void __launch_bounds__(64) k_service(SvcArgs a) {
 // NFFACL_TUNE_SVC_FULLPOLL=0) 56 / 103; whole-mailbox polls issued after
 // the answer 67 / 132 — profiles/r4_service/.)  A request is one rule set:
 // no grouping, the descriptor is wave-uniform.
+// Longest adaptive post-answer nap (s_sleep 2 units, ~50 ns each: ~2 us).
+constexpr uint32_t kSvcNapMax = 40;
+
 __global__ void __launch_bounds__(64) k_service_burst(SvcArgs a) {
     __shared__ FlatScratch<2> W;
     __shared__ u32x4 img[64 * kSvcBurstLoads];
@@ -404,6 +409,8 @@ __global__ void __launch_bounds__(64) k_service_burst(SvcArgs a) {
 #endif
     const uint32_t box = mb * kSvcBurstBoxBytes;
     const uint32_t bell = a.box_bytes + mb * 4u;
+    uint32_t nap = a.post_naps;  // the post-answer nap (wave-uniform; adapted when a.nap_adapt)
+    bool answered = false;       // this pass's poll is the first after an answer
     while (true) {
         // one poll per pass, issued here (see above)
         const uint64_t now = wall_clock64();
@@ -448,6 +455,11 @@ __global__ void __launch_bounds__(64) k_service_burst(SvcArgs a) {
         poll_ticks += t_data - now;
 #endif
         if (tag == done) {
+            // the first poll after an answer came back empty: the caller had
+            // not posted yet, and its request now waits a whole extra round
+            // trip — nap longer after the next answer
+            if (answered && a.nap_adapt) nap = min(nap + 3u, kSvcNapMax);
+            answered = false;
             if (now - last > a.idle_ticks) break;
             // an idle wave naps between bell reads (its reads share the
             // link's request slots with the hot waves' polls)
@@ -505,6 +517,9 @@ __global__ void __launch_bounds__(64) k_service_burst(SvcArgs a) {
             ++n_torn;
             continue;
         }
+        // found on the first poll after the answer: probe a shorter nap
+        if (answered && a.nap_adapt && nap > 0u) --nap;
+        answered = false;
         u32x4 h0;
         h0.x = __builtin_amdgcn_readlane(hh.x, 0);
         h0.y = __builtin_amdgcn_readlane(hh.y, 0);
@@ -588,7 +603,12 @@ __global__ void __launch_bounds__(64) k_service_burst(SvcArgs a) {
         // 147-160 Mpps without the nap, 122-124 / 182-191 with 12 naps (6 / 8
         // / 10 / 15: 97-102 / 100-112 / 107-119 / 120-121 at 16 clones;
         // NFFACL_TUNE_SVC_POST_NAPS, profiles/r5_ab/burst/)
-        for (uint32_t i = 0; i < a.post_naps; ++i) __builtin_amdgcn_s_sleep(2);
+        // Round 6: each wave adapts the nap to its own caller (nap_adapt):
+        // +3 after an empty first poll (a whole PCIe round trip lost), -1
+        // after a first poll that found the request — it settles just past
+        // the caller's turnaround, whichever host it runs on.
+        for (uint32_t i = 0; i < nap; ++i) __builtin_amdgcn_s_sleep(2);
+        answered = true;
     }
     if (lane == 0) {
         uint64_t *st = a.stats + size_t(blockIdx.x) * kSvcStatWords;
@@ -1124,6 +1144,12 @@ int service_create(int hip_device, uint32_t mailboxes, uint32_t idle_us, bool bu
             return NFFACL_ERR_INVALID_ARG;
         }
         s->args.post_naps = set ? static_cast<uint32_t>(v) : 12u;
+        if (!env_knob("NFFACL_TUNE_SVC_NAP_ADAPT", 0, 1, v, set, err)) {
+            set_last_error(err);
+            release_service(s);
+            return NFFACL_ERR_INVALID_ARG;
+        }
+        s->args.nap_adapt = !set || v != 0 ? 1u : 0u;
         if (!env_knob("NFFACL_TUNE_SVC_TRACE", 0, 1, v, set, err)) {
             set_last_error(err);
             release_service(s);
