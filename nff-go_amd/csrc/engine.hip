@@ -365,7 +365,15 @@ k_indexed_frames(const uint8_t *__restrict__ frames, const uint64_t *__restrict_
     // VGPRs to spare): also the next batch's 64-byte frame lines, into the
     // other of two register buffers (ping-pong, no copies), and the
     // descriptors of the batch after.
-    constexpr bool PF = TM == kTabSplit;  // (flat-LDS: +0.6 % on C3, profiles/r1_flat_lds/cold/)
+// (Round 6, VERDICT round 5 item 6, experiment builds NFFACL_EXP_FRAMES_PF:
+// 1 = the next batch's frame lines in flight + descriptors two ahead, 2 =
+// descriptors two batches ahead only — C3 0.4106 / 0.4157 and 0.4099 /
+// 0.4065 vs 0.4127 / 0.4089 ms in alternating processes: within noise, the
+// scattered frame reads still set the rate; profiles/r6_ab/c3pf/)
+#ifndef NFFACL_EXP_FRAMES_PF
+#define NFFACL_EXP_FRAMES_PF 0
+#endif
+    constexpr bool PF = TM == kTabSplit || (NFFACL_EXP_FRAMES_PF == 1 && TM == kTabFlatLds);  // (flat-LDS: +0.6 % on C3, profiles/r1_flat_lds/cold/)
     // (flat-LDS, round 2: one prefetch buffer with copies, 2 rounds — 124
     // VGPRs, no spill — ran 0.487 vs 0.469 ms on C3: the frame loads are not
     // what the walk waits on; profiles/r2_valu/pfab/.  Round 3: the same
@@ -403,6 +411,17 @@ k_indexed_frames(const uint8_t *__restrict__ frames, const uint64_t *__restrict_
             run_batch(b1, dsB, B);
             if (b2 >= n) break;
             base = b2;
+        }
+    } else if (NFFACL_EXP_FRAMES_PF == 2 && !a.dyn) {  // experiment: descriptors two batches ahead (grid stride)
+        uint64_t ds_next = desc_at(base), ds_next2 = desc_at(base + S);
+        while (base < n) {
+            const uint64_t ds = ds_next;
+            u32x4 v[4];
+            load_frames_rs(frames, ds, lane, v);
+            ds_next = ds_next2;
+            ds_next2 = desc_at(base + 2 * S);
+            run_batch(base, ds, v);
+            base += S;
         }
     } else {  // (pulled batches: BatchSource)
         BatchSource src;

@@ -12,8 +12,8 @@ if [ -z "$NOTEST" ]; then
 fi
 for rep in 1 2; do for cfg in ${CFGS:-c2}; do for lib in "$@"; do
   NFFACL_LIB=$R/$lib timeout -k 10 300 python tools/ab_env.py $cfg ${ROUNDS:-4} d=NFFACL_AB:0 \
-      > "$OUT/${cfg}_$(basename $lib .so)_$rep.json" 2>> "$OUT/err.log" || { echo "ab $cfg $lib failed"; exit 1; }
-  echo "$cfg $lib $rep $(python -c "import json,sys;d=json.load(open(sys.argv[1]));print(d['variants']['d']['median_ms'])" "$OUT/${cfg}_$(basename $lib .so)_$rep.json")"
+      > "$OUT/${cfg}_$(dirname $lib | tr / _)_$rep.json" 2>> "$OUT/err.log" || { echo "ab $cfg $lib failed"; exit 1; }
+  echo "$cfg $lib $rep $(python -c "import json,sys;d=json.load(open(sys.argv[1]));print(d['variants']['d']['median_ms'])" "$OUT/${cfg}_$(dirname $lib | tr / _)_$rep.json")"
 done; done; done
 if [ -n "$PMC" ]; then
   cd /tmp && export TMPDIR=/tmp
