@@ -772,6 +772,46 @@ def test_graph_capture_replay_gpu(torch_cuda, cfg):
         del graph
 
 
+def test_per_thread_stream_launches_gpu(torch_cuda):
+    """hipStreamPerThread is ONE handle value for a
+    different stream on every thread, so launches on it from two threads may
+    run at once; they must not share one block of pull heads (the engine
+    takes the grid stride for that handle).  Two threads x 6 launches of C5
+    (a pulled-batch walk by default) on hipStreamPerThread, every launch
+    equal to the oracle."""
+    import threading
+    torch = torch_cuda
+    g = synth.gen_rules(synth.SPECS["c5"], synth.RULE_SEEDS["c5"])
+    rules, (a4, a6) = _rules_and_arrays(g.text)
+    n = (1 << 18) + 11
+    slots = synth.gen_slots(g, n, 43)
+    want = oracle.classify_slots(slots, 64, n, a4, a6, threads=THREADS)
+    d_slots = to_dev(torch, slots)
+    per_thread = 2  # hipStreamPerThread ((hipStream_t)2, hip_runtime_api.h)
+    errors, outs = [], {}
+    with nffacl.Engine(rules) as eng:
+        assert eng.kernel_info().pulled == 1  # the walk pulls its batches on ordinary streams
+
+        def worker(t):
+            try:
+                ports = [torch.empty(n, dtype=torch.int32, device="cuda") for _ in range(6)]
+                for p in ports:
+                    eng.classify_device(d_slots, 64, n, p, None, per_thread)
+                torch.cuda.synchronize()
+                outs[t] = [p.cpu().numpy().view(np.uint32) for p in ports]
+            except Exception as e:  # surfaced below
+                errors.append(e)
+        ths = [threading.Thread(target=worker, args=(t,)) for t in range(2)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+    assert not errors, errors
+    for t in range(2):
+        for p in outs[t]:
+            np.testing.assert_array_equal(p, want)
+
+
 @pytest.mark.parametrize("fine_slots,ns", [(None, 6), ("7", 7), ("11", 8), ("15", 8)])
 def test_c5_more_fine_grids_gpu(torch_cuda, monkeypatch, fine_slots, ns):
     """Fine grids on two (default) / three / all four positional grid slots
