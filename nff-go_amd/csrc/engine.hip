@@ -219,9 +219,14 @@ struct BatchSource {
 //    classifying packet coal_packet(l) of its wave's batch; no register
 //    prefetch (it would push the kernel past 64 VGPRs, i.e. below 8 waves per
 //    SIMD) — 32 resident waves per CU keep 128 KiB of loads in flight.
-// (experiment builds: NFFACL_EXP_MAXVGPR caps the slot kernels' VGPRs)
+// (experiment builds: NFFACL_EXP_MAXVGPR / _MAXSGPR cap the slot kernels'
+// registers.  Round 6: C2's kernel holds 87 SGPRs, past the 80 that admit 8
+// waves per SIMD (MI355X_MICROARCH.md, residency); capped at 80 (78, 7 SGPR
+// spills) it ran 0.2109 / 0.2091 vs 0.2061 / 0.2063 ms, profiles/r6_ab/s80/)
 #ifdef NFFACL_EXP_MAXVGPR
 #define NFFACL_SLOTS_VGPR __attribute__((amdgpu_num_vgpr(NFFACL_EXP_MAXVGPR)))
+#elif defined(NFFACL_EXP_MAXSGPR)
+#define NFFACL_SLOTS_VGPR __attribute__((amdgpu_num_sgpr(NFFACL_EXP_MAXSGPR)))
 #else
 #define NFFACL_SLOTS_VGPR
 #endif
