@@ -723,6 +723,41 @@ typedef uint32_t u32x3 __attribute__((ext_vector_type(3), aligned(4)));
 
 __device__ __forceinline__ u32x3 ld3(const uint32_t *__restrict__ p) { return *reinterpret_cast<const u32x3 *>(p); }
 
+// Pair gathers (round 6): the two lanes of a pair (2i, 2i + 1) read ONE
+// candidate's entry per load instruction — the even lane a 12-byte piece, the
+// odd lane the next — so a wave instruction touches 32 entries' lines, not 64.
+// Scattered loads cost the TA/TCP a cycle per line touched (prof_r6_c5: TA
+// busy 85 % of the kernel's cycles, VALU 17 %, LDS 13 %).  The pair's loads:
+// X = the even lane's candidate's pieces (p | p + 1), Y = the odd lane's; then
+// pair_unpack trades across the pair (one DPP move per word, unconditional,
+// both arms of the selects) so that every lane holds its own candidate's
+// pieces p in X and p + 1 in Y — what two plain loads would have given it.
+// Measured (profiles/r6_ab/pair/): C5 0.5084 / 0.5058 and 0.5136 / 0.5224 ms
+// vs 0.5246 / 0.5235 and 0.5275 / 0.5241 without — 1.5-3 %, not the halving a
+// per-line TA cost predicts: the L2 requests (one per entry line, unchanged)
+// and their latency set the rest.  In classify_flat (C3) the same loads ran
+// even (0.408 / 0.409 vs 0.413 / 0.407 ms) and were not kept; the pipelined
+// walk uses them.
+#ifndef NFFACL_PAIR_GATHER
+#define NFFACL_PAIR_GATHER 1
+#endif
+__device__ __forceinline__ void pair_offsets(uint32_t o, bool odd, uint32_t &oe, uint32_t &od) {
+    const uint32_t p = dpp<0xB1>(o);  // quad_perm [1,0,3,2]: the partner's offset
+    oe = (odd ? p : o) + (odd ? 12u : 0u);
+    od = (odd ? o : p) + (odd ? 12u : 0u);
+}
+__device__ __forceinline__ void pair_unpack(bool odd, u32x3 &X, u32x3 &Y) {
+    u32x3 lo, hi;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const uint32_t r = dpp<0xB1>(odd ? X[c] : Y[c]);
+        lo[c] = odd ? r : X[c];
+        hi[c] = odd ? Y[c] : r;
+    }
+    X = lo;
+    Y = hi;
+}
+
 // Position of the first set bit from the top (v_ffbh_u32), 0xFFFFFFFF for 0
 // — defined here for 0, unlike __builtin_clz (hence the one-line asm).
 __device__ __forceinline__ uint32_t ffbh_raw(uint32_t x) {
@@ -1270,6 +1305,11 @@ __device__ __forceinline__ void flat_bounds_lds(const IndexedArgs &a, const Fiel
 #ifndef NFFACL_EXP_PIPE
 #define NFFACL_EXP_PIPE 0
 #endif
+// 1: one mark pass per pass, marks carrying entry offsets (round 6); 0: the
+// round-5 windows (marks + deltas per window), kept for A/B builds
+#ifndef NFFACL_PIPE_ONEMARK
+#define NFFACL_PIPE_ONEMARK 1
+#endif
 
 template <int NS, class PF>
 __device__ __forceinline__ uint32_t classify_flat_pipe(const IndexedArgs &a, const Fields &f, FlatScratch<4> &W,
@@ -1301,6 +1341,156 @@ __device__ __forceinline__ uint32_t classify_flat_pipe(const IndexedArgs &a, con
     };
     W.best[lane] = ~0ull;
     const uint8_t *tab8 = reinterpret_cast<const uint8_t *>(a.tab);
+#if NFFACL_PIPE_ONEMARK
+    // Round 6: ONE mark pass per pass for both families.  A mark carries its
+    // list's entry offset instead of its window position:
+    //   mark = owner lane << 26 | slot << 23 | (st - so + 2^22) mod 2^23
+    // (ascending in stream order, as the prefix max needs; never 0), so the
+    // candidate at stream number k reads its entry at family-relative
+    // (mark mod 2^23) - 2^22 + k without a delta array — whose 1 KiB now
+    // holds marks: 512 positions, the IPv4 window's 448 (7 rounds) at 0..447
+    // and the IPv6 round's 64 at 448..511, marked together.  The owner's
+    // protocol comes by one more ds_bpermute.  (Entry numbers < 2^22 per
+    // family: indexed_launch.)
+    uint32_t *const M = reinterpret_cast<uint32_t *>(&W);  // W.mark[256] + W.delta[256], contiguous
+    const bool odd = (lane & 1u) != 0u;                    // (pair gathers)
+    static_assert(sizeof(W.mark) + sizeof(W.delta) == 512 * sizeof(uint32_t), "512 marks");
+    constexpr uint32_t kBias = 1u << 22, kOffMask = (1u << 23) - 1u;
+    constexpr uint32_t kW4 = 448u, kP6 = 448u;  // IPv4 window length; the IPv6 round's first position
+    auto mark_all = [&](uint32_t w4, uint32_t w6) {
+        if (NFFACL_EXP_PIPE == 3) return;
+        wave_lds_sync();  // (the previous pass's mark reads come first)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) M[64 * j + lane] = 0u;
+        wave_lds_sync();
+        const uint32_t w = v6 ? w6 : w4, lim = v6 ? 64u : kW4, pb = v6 ? kP6 : 0u;
+        uint32_t so = off;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            if (ln[s] != 0u && so < w + lim && so + ln[s] > w)
+                M[pb + (so > w ? so - w : 0u)] =
+                    lane << 26 | static_cast<uint32_t>(s) << 23 | ((st[s] - so + kBias) & kOffMask);
+            so += ln[s];
+        }
+        wave_lds_sync();
+    };
+    // Locate rounds j0 .. j0 + RR - 1 of the family window marked at pb,
+    // continuing the prefix max from `carry`, and issue their entry loads
+    // (lanes past the stream load the table's first bytes, untested).
+    // mk[j] = the candidate's mark (its owner lane in bits 26..31).
+    auto locate = [&](uint32_t pb, uint32_t w, uint32_t T, uint32_t j0, uint32_t &carry, auto six, auto rr,
+                      uint32_t (&mk)[4], u32x3 (&A)[4], u32x3 (&B)[4], u32x3 &C, u32x3 &D) {
+        constexpr bool SIX = decltype(six)::value;
+        constexpr uint32_t ent_bytes = 4u * (SIX ? kHybEnt6Dwords : kHybEnt4Dwords);
+        constexpr int RR = decltype(rr)::value;
+        static_assert(!SIX || RR == 1, "IPv6 rounds: one per pass");
+        const uint32_t fb4 = 4u * (SIX ? a.f6.off_ent_base : a.f4.off_ent_base);
+        uint32_t scan[RR];
+#pragma unroll
+        for (int j = 0; j < RR; ++j)
+            scan[j] = NFFACL_EXP_PIPE == 3 ? kBias : wave_incl_max(M[pb + 64u * (j0 + j) + lane]);
+#pragma unroll
+        for (int j = 0; j < RR; ++j) {
+            const uint32_t m = max(scan[j], carry);
+            carry = __builtin_amdgcn_readlane(m, 63);
+            mk[j] = m;
+            const uint32_t k = w + 64u * (j0 + j) + lane;
+            // family-relative entry number (< 2^22 for every valid k)
+            const uint32_t en = (m & kOffMask) - kBias + k;
+            uint32_t o = k < T ? fb4 + __umul24(en, ent_bytes) : 0u;
+            if (NFFACL_EXP_PIPE == 1) o = 4u * a.f4.off_ent_base;
+            if (NFFACL_EXP_PIPE == 3) o = 4u * a.f4.off_ent_base + __umul24(k & 4095u, ent_bytes);
+            if (NFFACL_PAIR_GATHER) {  // unpacked by the round's test
+                uint32_t oe, od;
+                pair_offsets(o, odd, oe, od);
+                const uint32_t *xe = reinterpret_cast<const uint32_t *>(tab8 + oe);
+                const uint32_t *xd = reinterpret_cast<const uint32_t *>(tab8 + od);
+                A[j] = ld3(xe);
+                B[j] = ld3(xd);
+                if constexpr (SIX) {
+                    C = ld3(xe + 6);
+                    D = ld3(xd + 6);
+                }
+            } else {
+                const uint32_t *e = reinterpret_cast<const uint32_t *>(tab8 + o);
+                A[j] = ld3(e);
+                B[j] = ld3(e + 3);
+                if constexpr (SIX) {
+                    C = ld3(e + 6);
+                    D = ld3(e + 9);
+                }
+            }
+        }
+    };
+    // Test round j of a window: the owner packet's fields by ds_bpermute;
+    // a passing candidate posts (rule index << 32 | output code) to the
+    // owner's LDS minimum.
+    auto post = [&](bool pass, uint32_t o, const u32x3 &A, const u32x3 &B) {
+        if (NFFACL_EXP_PIPE == 2) {  // keep the loads alive without testing: one cheap use
+            if ((A.x ^ B.z) == 0x5A5A5A5Au) W.best[lane] = 0u;
+            return;
+        }
+        if (pass)
+            atomicMin(reinterpret_cast<unsigned long long *>(&W.best[o]),
+                      static_cast<unsigned long long>(A.z >> kEntIndexShift) << 32 | (B.z >> kHybOutShift));
+    };
+    auto test4 = [&](uint32_t w, uint32_t j0, auto rr, const uint32_t (&mk)[4], const u32x3 (&A)[4],
+                     const u32x3 (&B)[4]) {
+        constexpr int RR = decltype(rr)::value;
+#pragma unroll
+        for (int j = 0; j < RR; ++j) {
+            const uint32_t o = mk[j] >> 26;
+            const uint32_t oks = bperm(ks, o), okd = bperm(kd, o), opt = bperm(f.ports, o), opr = bperm(f.proto, o);
+            const bool valid = w + 64u * (j0 + j) + lane < T4;
+            u32x3 ea = A[j], eb = B[j];
+            if (NFFACL_PAIR_GATHER) pair_unpack(odd, ea, eb);
+            const bool pass = valid & !hyb_miss(ea, eb, oks, okd, opr & 0xFFu, opt);
+            post(pass, o, ea, eb);
+        }
+    };
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
+    using I4 = std::integral_constant<int, 4>;
+    // One pass: one mark pass, then up to one IPv6 round from w6 and IPv4
+    // rounds 0 .. R0 - 1 (<= 4) and R0 .. R0 + R1 - 1 (<= 3) from w4, issued
+    // and tested in classify_flat_pipe's order (IPv6 round and first IPv4
+    // rounds issued, IPv6 tested, the last IPv4 rounds issued, IPv4 tested).
+    auto pass = [&](uint32_t w4, uint32_t w6, bool do6, auto r0, auto r1) {
+        constexpr int R0 = decltype(r0)::value, R1 = decltype(r1)::value;
+        uint32_t mk6[4], mkA[4], mkB[4];
+        u32x3 A6[4], B6[4], C6, D6, AA[4], BA[4], AB[4], BB[4], cd;
+        mark_all(w4, w6);
+        uint32_t c6 = 0, c4 = 0;
+        if (do6) locate(kP6, w6, T6, 0u, c6, std::true_type{}, I1{}, mk6, A6, B6, C6, D6);
+        if constexpr (R0 > 0) locate(0u, w4, T4, 0u, c4, std::false_type{}, r0, mkA, AA, BA, cd, cd);
+        if (do6) {  // the IPv6 round: every lane's address words 1..3 against its owner's
+            const uint32_t o = mk6[0] >> 26;
+            const uint32_t oks = bperm(ks, o), okd = bperm(kd, o), opt = bperm(f.ports, o), opr = bperm(f.proto, o);
+            uint32_t os[4] = {0, 0, 0, 0}, ot[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int q = 1; q < 4; ++q) {
+                os[q] = bperm(__builtin_bswap32(f.s[q]), o);
+                ot[q] = bperm(__builtin_bswap32(f.t[q]), o);
+            }
+            const bool valid = w6 + lane < T6;
+            if (NFFACL_PAIR_GATHER) {
+                pair_unpack(odd, A6[0], B6[0]);
+                pair_unpack(odd, C6, D6);
+            }
+            // (one combined miss: no short-circuit branch)
+            const bool m4 = hyb_miss(A6[0], B6[0], oks, okd, opr & 0xFFu, opt);
+            const bool m6 = hyb_miss6(C6, D6, B6[0].z, os, ot);
+            const bool miss6 = m4 || m6;
+            const bool pass6 = valid & !miss6;
+            post(pass6, o, A6[0], B6[0]);
+        }
+        if constexpr (R1 > 0) locate(0u, w4, T4, static_cast<uint32_t>(R0), c4, std::false_type{}, r1, mkB, AB, BB, cd, cd);
+        if constexpr (R0 > 0) test4(w4, 0u, r0, mkA, AA, BA);
+        if (w4 == 0u) prefetch();  // (the first pass)
+        if constexpr (R1 > 0) test4(w4, static_cast<uint32_t>(R0), r1, mkB, AB, BB);
+    };
+#else
     // Mark the lists of family `fam6` overlapping the window [w, w + 64 RR):
     // mark[pos] = (owner lane << 19 | slot << 16 | pos << 8 | owner's protocol)
     // + 1 at the list's first position in the window, delta[pos] = byte
@@ -1432,6 +1622,7 @@ __device__ __forceinline__ uint32_t classify_flat_pipe(const IndexedArgs &a, con
         if (w4 == 0u) prefetch();  // (the first pass)
         if constexpr (R1 > 0) test4(w4 + 256u, r1, mkB, AB, BB);
     };
+#endif
     using I0 = std::integral_constant<int, 0>;
     uint32_t w4 = 0, w6 = 0;
     while (true) {

@@ -711,7 +711,9 @@ static IndexedLaunch indexed_launch(const nffacl_engine *eng, const DevTable *t)
             L.tm = dev::kTabFlatLdsG;
             L.lds_bytes = lds4;  // > kLdsBytes is refused by the launch check below
         } else if (tu.pipe && (t->meta.flat_uncond || tu.pipe == 2) && lds4 <= kLdsBytes && !tu.rounds &&
-                   ns <= NFFACL_PIPE_MAX_NS) {
+                   ns <= NFFACL_PIPE_MAX_NS &&
+                   // its marks carry entry offsets in 23 bits (classify_flat_pipe)
+                   t->meta.blob.size() / kHybEnt4Dwords < (size_t(1) << 22) - (size_t(1) << 16)) {
             // the pipelined walk (its scratch: FlatScratch<4>)
             L.tm = dev::kTabFlatLdsP;
             L.lds_bytes = lds4;

@@ -119,12 +119,18 @@ def _miss6(C, D, lens, s, t):
     return (1 if ps < sl else 0) | (1 if pd < dl else 0)
 
 
+ONEMARK = True  # classify_flat_pipe's round-6 form (NFFACL_PIPE_ONEMARK=1); False: round 5's windows
+
+
 class Scratch:
-    """One wave's FlatScratch<4> (persists across the wave's batches)."""
+    """One wave's FlatScratch<4> (persists across the wave's batches): the
+    round-5 form's mark[256] / delta[256], or the round-6 form's 512 marks
+    over the same bytes (M)."""
 
     def __init__(self, rng):
         self.mark = [int(x) for x in rng.integers(0, 1 << 32, 256, dtype=np.uint64)]
         self.delta = [int(x) for x in rng.integers(0, 1 << 32, 256, dtype=np.uint64)]
+        self.M = self.mark + self.delta
         self.best = [int(x) for x in rng.integers(0, 1 << 63, 64, dtype=np.uint64)]
 
 
@@ -227,6 +233,50 @@ def walk_batch(blob, info, ns, F, base, n, W, trace=None, where=None):
                     miss |= _miss6(C, D, B[2], sw[o], tw[o])
                 post(k < T and miss == 0, o, A, B, (len(passes) - 1, name, j, l, k))
 
+    BIAS, OMASK = 1 << 22, (1 << 23) - 1
+
+    def mark_all(w4, w6):
+        """One mark pass: IPv4 lists over [w4, w4 + 448) at 0..447, IPv6 over
+        [w6, w6 + 64) at 448..511; mark = lane << 26 | slot << 23 | (st - so + 2^22) mod 2^23."""
+        for j in range(512):
+            W.M[j] = 0
+        for l in range(64):
+            w, lim, pb = (w6, 64, 448) if is6[l] else (w4, 448, 0)
+            so = off[l]
+            for s in range(ns):
+                if ln[l][s] != 0 and so < w + lim and so + ln[l][s] > w:
+                    W.M[pb + (so - w if so > w else 0)] = (l << 26 | s << 23 | ((st[l][s] - so + BIAS) & OMASK)) & M32
+                so = (so + ln[l][s]) & M32
+
+    def locate1(pb, w, T, j0, carry, six, RR):
+        ent_bytes = 4 * (ENT6 if six else ENT4)
+        fb4 = 4 * (f6.off_ent_base if six else f4.off_ent_base)
+        out = []
+        for j in range(j0, j0 + RR):
+            rnd = []
+            m = carry
+            for l in range(64):
+                m = max(m, W.M[pb + 64 * j + l])
+                k = w + 64 * j + l
+                en = ((m & OMASK) - BIAS + k) & M32
+                o = (fb4 + en * ent_bytes) & M32 if k < T else 0
+                A, B = ld(o, 3), ld(o + 12, 3)
+                C = ld(o + 24, 3) if six else None
+                D = ld(o + 36, 3) if six else None
+                rnd.append((m, k, A, B, C, D))
+            carry = m  # readlane(m, 63)
+            out.append(rnd)
+        return out, carry
+
+    def test1(rounds, T, six, name, j0):
+        for jj, rnd in enumerate(rounds):
+            for l, (mk, k, A, B, C, D) in enumerate(rnd):
+                o = (mk >> 26) & 63
+                miss = _miss(A, B, ks[o], kd[o], proto[o] & 0xFF, ports[o])
+                if six:
+                    miss |= _miss6(C, D, B[2], sw[o], tw[o])
+                post(k < T and miss == 0, o, A, B, (len(passes) - 1, name, j0 + jj, l, k))
+
     w4 = w6 = 0
     while True:
         if w4 >= T4 and w6 >= T6:
@@ -236,22 +286,39 @@ def walk_batch(blob, info, ns, F, base, n, W, trace=None, where=None):
         r = (rem4 + 63) // 64
         R0, R1 = (4, 3) if r >= 7 else (4, r - 4) if r >= 4 else (r, 0)
         passes.append((w4, w6, do6, R0, R1))
-        r6 = ra = rb = None
-        if do6:
-            mark(True, w6, 1)
-            r6 = locate(w6, T6, True, 1)
-        if R0:
-            mark(False, w4, R0)
-            ra = locate(w4, T4, False, R0)
-        if do6:
-            test(r6, T6, True, 'v6')
-        if R1:
-            mark(False, w4 + 256, R1)
-            rb = locate(w4 + 256, T4, False, R1)
-        if R0:
-            test(ra, T4, False, 'A')
-        if R1:
-            test(rb, T4, False, 'B')
+        if ONEMARK:
+            mark_all(w4, w6)
+            r6 = ra = rb = None
+            c4 = 0
+            if do6:
+                r6, _ = locate1(448, w6, T6, 0, 0, True, 1)
+            if R0:
+                ra, c4 = locate1(0, w4, T4, 0, 0, False, R0)
+            if do6:
+                test1(r6, T6, True, 'v6', 0)
+            if R1:
+                rb, c4 = locate1(0, w4, T4, R0, c4, False, R1)
+            if R0:
+                test1(ra, T4, False, 'A', 0)
+            if R1:
+                test1(rb, T4, False, 'B', R0)
+        else:
+            r6 = ra = rb = None
+            if do6:
+                mark(True, w6, 1)
+                r6 = locate(w6, T6, True, 1)
+            if R0:
+                mark(False, w4, R0)
+                ra = locate(w4, T4, False, R0)
+            if do6:
+                test(r6, T6, True, 'v6')
+            if R1:
+                mark(False, w4 + 256, R1)
+                rb = locate(w4 + 256, T4, False, R1)
+            if R0:
+                test(ra, T4, False, 'A')
+            if R1:
+                test(rb, T4, False, 'B')
         w4 += 448
         w6 += 64
         if w4 >= T4 and w6 >= T6:
