@@ -77,6 +77,17 @@ __device__ __forceinline__ void clip_dwords(uint32_t (&d)[N], uint32_t len) {
 }
 __device__ __forceinline__ void clip16(uint32_t (&d)[16], uint32_t len) { clip_dwords<16>(d, len); }
 
+// A verdict store, nontemporal where the kernel gathers an L2-sized table
+// (NT): a C5 launch writes 64 MiB of ports through L2, where the ~4 MB of
+// rule entries want to stay — 0.5046 / 0.4958 vs 0.5103 / 0.5116 ms; the
+// streaming kernels (C2 0.2090 vs 0.2047, C3 0.4084 vs 0.4048 ms) keep plain
+// stores (profiles/r6_ab/nt/).
+template <bool NT>
+__device__ __forceinline__ void store_port(uint32_t *p, uint32_t v) {
+    if (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
 // Port vector (u32 per packet) + permit bitmap (one 64-bit ballot per wave).
 __device__ __forceinline__ void store_verdicts(uint64_t base, uint32_t lane, bool live, uint32_t res,
                                                uint32_t *__restrict__ port_out,

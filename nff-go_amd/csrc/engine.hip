@@ -317,7 +317,7 @@ k_indexed_slots(const uint8_t *__restrict__ slots, uint32_t stride, uint64_t n, 
                 if (nb + 64 <= n) load_rowswap<NT>(slots + nb * 64, lane, nv);
             }
         });
-        if (live && port_out) port_out[idx] = res;
+        if (live && port_out) store_port<TM == kTabFlatLdsP>(port_out + idx, res);
         if (permit_out) {
             // permit bit p belongs to packet p: fetch packet `lane`'s verdict from the lane holding it
             const uint32_t src = COAL ? 4u * (lane & 15u) + (lane >> 4) : lane;
