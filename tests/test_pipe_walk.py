@@ -74,3 +74,43 @@ def test_pipe_walk_second_passes():
     passes = [len(t["passes"]) for t in trace]
     assert max(passes) >= 2, passes
     assert any(t["T4"] > 448 for t in trace) and any(t["T6"] > 64 for t in trace)
+
+
+def _quad_perm_b1(v):
+    """DPP quad_perm [1,0,3,2] over 64 lanes: lane l reads lane l ^ 1."""
+    return v[np.arange(64) ^ 1]
+
+
+def test_pair_gather_exchange():
+    """classify.hpp pair_offsets / pair_unpack (the pipelined walk's pair
+    gathers), restated lane by lane: both lanes of a pair load 12-byte pieces
+    of ONE entry per instruction (even: piece p, odd: piece p + 1; X for the
+    even lane's candidate, Y for the odd lane's), then trade across the pair.
+    Every lane must end with exactly the pieces two plain loads of its own
+    entry would give — for 24-byte IPv4 and 48-byte IPv6 entries, and with
+    past-the-stream lanes pointing at offset 0."""
+    rng = np.random.default_rng(7)
+    tab = rng.integers(0, 2**32, size=1 << 14, dtype=np.uint64).astype(np.uint32)
+    tab8 = tab.view(np.uint8)
+    odd = (np.arange(64) & 1).astype(bool)
+
+    def ld3(off):  # per-lane dwordx3 at byte offsets
+        return np.stack([tab8[o:o + 12].view(np.uint32) for o in off])
+
+    for ent_bytes in (24, 48):
+        for trial in range(20):
+            n_ent = (len(tab8) - 64) // ent_bytes
+            o = rng.integers(0, n_ent, size=64).astype(np.uint32) * ent_bytes
+            o[rng.random(64) < 0.2] = 0  # lanes past the stream
+            p = _quad_perm_b1(o)
+            h = np.where(odd, 12, 0).astype(np.uint32)
+            oe = np.where(odd, p, o) + h
+            od = np.where(odd, o, p) + h
+            for base in ((0, 24) if ent_bytes == 48 else (0,)):
+                X, Y = ld3(oe + base), ld3(od + base)
+                send = np.where(odd[:, None], X, Y)
+                r = _quad_perm_b1(send)
+                lo = np.where(odd[:, None], r, X)
+                hi = np.where(odd[:, None], Y, r)
+                np.testing.assert_array_equal(lo, ld3(o + base))
+                np.testing.assert_array_equal(hi, ld3(o + base + 12))
